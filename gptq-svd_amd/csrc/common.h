@@ -1,0 +1,67 @@
+// Shared helpers for the MI355X (gfx950) TruncGPTQ kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace tg {
+
+void set_error(const char *fmt, ...);
+
+// Carve aligned sub-buffers out of a caller workspace.
+struct Arena {
+  char *base;
+  size_t cap, off = 0;
+  Arena(void *p, size_t n) : base(static_cast<char *>(p)), cap(n) {}
+  template <class T>
+  T *take(size_t count) {
+    off = (off + 255) & ~size_t(255);
+    T *p = reinterpret_cast<T *>(base + off);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= cap; }
+};
+
+// Same layout arithmetic without a base pointer (for *_workspace_size()).
+struct Sizer {
+  size_t off = 0;
+  template <class T>
+  void take(size_t count) {
+    off = (off + 255) & ~size_t(255);
+    off += count * sizeof(T);
+  }
+};
+
+inline int cdiv(int64_t a, int64_t b) { return int((a + b - 1) / b); }
+
+}  // namespace tg
+
+#define TG_ARG(cond, idx, msg)                                   \
+  do {                                                           \
+    if (!(cond)) {                                               \
+      tg::set_error("%s: argument %d: %s", __func__, idx, msg); \
+      return -(idx);                                             \
+    }                                                            \
+  } while (0)
+
+#define TG_HIP(call)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      tg::set_error("%s: %s failed: %s", __func__, #call, hipGetErrorString(e_));    \
+      return int(e_);                                                                \
+    }                                                                                \
+  } while (0)
+
+#define TG_LAUNCHED() TG_HIP(hipGetLastError())
+
+#define TG_WS(arena)                                                        \
+  do {                                                                      \
+    if (!(arena).ok()) {                                                    \
+      tg::set_error("%s: workspace too small (%zu > %zu bytes)", __func__, \
+                    (arena).off, (arena).cap);                              \
+      return -99;                                                           \
+    }                                                                       \
+  } while (0)

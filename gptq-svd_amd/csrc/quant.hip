@@ -1,0 +1,591 @@
+// Quantize / error-propagate path of TruncGPTQ on MI355X (gfx950).
+//
+// Replaces, in /root/reference/src/TruncGPTQ/gptq_utils.py:
+//   Quantizer.find_params            :249-266   -> group_params_kernel
+//   gptq_fwrd prologue (permute)     :491-495   -> permute_kernel (S/Z gathered on the fly)
+//   gptq_block_kernel (Triton)       :298-386   -> block_kernel
+//   cross-block E @ (U/diag) update  :537-545   -> cross_gemm_kernel (FP32 MFMA 32x32x2)
+//   tail RTN + unpermute             :547-557   -> finalize_kernel
+//   (packing: new, README.md:133)                -> pack kernels
+//
+// Exactness contract (tests/test_gpu_quant.py): every elementwise op is the
+// reference's IEEE f32 op in the reference's order.  FMA contraction is
+// disabled for this file; the one place an FMA chain is *intended* is the
+// cross-block GEMM, whose reduction order the reference leaves to the BLAS;
+// here it is defined as the k-ordered fmaf chain from +0 (what MFMA computes
+// and what oracle/quant_ref.c computes).
+#pragma clang fp contract(off)
+
+#include <type_traits>
+
+#include "../../include/truncgptq.h"
+#include "common.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ inline float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// ---------------------------------------------------------------------------
+// A7: static-group scale / zero (gptq_utils.py:249-266), one wave per group.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void group_params_kernel(const float *__restrict__ W, int m,
+                                                           int ldw, int g, int G, float maxq,
+                                                           int sym, float *__restrict__ scale,
+                                                           float *__restrict__ zero) {
+  const int wave = int((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wave >= m * G) return;
+  const int r = wave / G, gi = wave % G;
+  const float *p = W + size_t(r) * ldw + size_t(gi) * g;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = lane; i < g; i += 64) {
+    float v = p[i];
+    if (sym) {
+      mx = fmaxf(mx, fabsf(v));
+    } else {
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, off));
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+  }
+  if (lane == 0) {
+    float s, z;
+    if (sym) {
+      float a = mx < 1e-5f ? 1e-5f : mx;  // clamp(min=1e-5)          :259
+      s = a / maxq;                       // true IEEE division (CPU torch) :260
+      z = 0.0f;
+    } else {
+      float d = mx - mn;
+      d = d < 1e-5f ? 1e-5f : d;          // (mx - mn).clamp(min=1e-5)      :265
+      s = d / maxq;
+      z = rintf(-mn / s);                 // torch.round = half-to-even     :266
+      z = z < 0.0f ? 0.0f : (z > maxq ? maxq : z);
+    }
+    scale[size_t(r) * G + gi] = s;
+    zero[size_t(r) * G + gi] = z;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Permutation helpers (gptq_utils.py:493, :556-557).
+// ---------------------------------------------------------------------------
+__global__ void invperm_kernel(const int64_t *__restrict__ perm, int n, int32_t *__restrict__ inv,
+                               int32_t *__restrict__ perm32) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n) {
+    int p = int(perm[c]);
+    inv[p] = c;
+    perm32[c] = p;
+  }
+}
+
+__global__ void permute_kernel(const float *__restrict__ W, int n, const int32_t *__restrict__ perm,
+                               float *__restrict__ Wp) {
+  const int r = blockIdx.y;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+    Wp[size_t(r) * n + c] = W[size_t(r) * n + perm[c]];
+}
+
+// ---------------------------------------------------------------------------
+// Per-block prep: corr[c][j] = U[c, j] * (1/U[c, c])   (Triton :368-377)
+//                 SM[c][j]   = U[c, i2 + j] / U[c, c]   (:539-541)
+// ---------------------------------------------------------------------------
+__global__ void prep_block_kernel(const float *__restrict__ Ublk, int ldu, int bw, int nc,
+                                  float *__restrict__ corr, int ldcorr, float *__restrict__ SM,
+                                  int ldsm) {
+  const int c = blockIdx.x;
+  const float *urow = Ublk + size_t(c) * ldu;
+  const float d = urow[c];
+  const float inv = 1.0f / d;
+  for (int j = threadIdx.x; j < bw; j += blockDim.x) corr[size_t(c) * ldcorr + j] = urow[j] * inv;
+  for (int j = threadIdx.x; j < nc; j += blockDim.x) SM[size_t(c) * ldsm + j] = urow[bw + j] / d;
+}
+
+// ---------------------------------------------------------------------------
+// A9: the intra-block quantize + propagate loop.
+//
+// One workgroup owns RW rows and all `bw` columns of the block (rows are
+// independent).  The block's W rows live in LDS.  Columns are processed in
+// panels of P: wave 0 runs the sequential column chain for the panel with one
+// lane per row (panel columns in registers, corr broadcast from LDS); then
+// all waves apply the panel's P updates, in column order, to every later
+// column of the block.  Per element this is exactly the reference sequence
+// w_j <- w_j - e_c * corr[c][j] for c = 0, 1, ... (separately rounded mul
+// and sub), so the result is bit-identical to the Triton kernel.
+// ---------------------------------------------------------------------------
+constexpr int RW = 16;  // rows per workgroup
+constexpr int P = 32;   // panel width
+
+struct BlockArgs {
+  const float *W;
+  int ldw;  // block start (column i1), row stride
+  float *Q;
+  int ldq;
+  uint8_t *codes;
+  int ldc;
+  float *E;
+  int lde;
+  const float *corr;
+  int ldcorr;
+  // explicit s/z (tg_process_block) ...
+  const float *s;
+  int lds;
+  const float *z;
+  int ldz;
+  // ... or gathered from per-group params through the permutation
+  const float *scale;
+  const float *zero;
+  const int32_t *perm;
+  int G, g, col0;
+  int m, bw;
+  float minq, maxq;
+  int code_off;
+};
+
+template <bool GATHER>
+__device__ inline void load_sz(const BlockArgs &a, int row, int c, float &s, float &z) {
+  if (row >= a.m) {
+    s = 1.0f;
+    z = 0.0f;
+    return;
+  }
+  if (GATHER) {
+    const int gi = a.perm[a.col0 + c] / a.g;
+    s = a.scale[size_t(row) * a.G + gi];
+    z = a.zero[size_t(row) * a.G + gi];
+  } else {
+    s = a.s[size_t(row) * a.lds + c];
+    z = a.z[size_t(row) * a.ldz + c];
+  }
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
+  extern __shared__ float smem[];
+  const int bwp = a.bw + 1;           // odd row stride: lane-per-row access is conflict-free
+  float *Wb = smem;                    // [RW][bwp]
+  float *el = Wb + RW * bwp;           // [RW][P+1] panel errors
+  float *cp = el + RW * (P + 1);       // [P][P]   corr panel
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * RW;
+
+  for (int idx = tid; idx < RW * a.bw; idx += blockDim.x) {
+    const int rr = idx / a.bw, c = idx % a.bw;
+    const int row = r0 + rr;
+    Wb[rr * bwp + c] = row < a.m ? a.W[size_t(row) * a.ldw + c] : 0.0f;
+  }
+
+  for (int p0 = 0; p0 < a.bw; p0 += P) {
+    const int pw = min(P, a.bw - p0);
+    for (int idx = tid; idx < P * P; idx += blockDim.x) {
+      const int cc = idx / P, j = idx % P;
+      cp[idx] = (cc < pw && j < pw) ? a.corr[size_t(p0 + cc) * a.ldcorr + p0 + j] : 0.0f;
+    }
+    __syncthreads();
+
+    if (tid < RW) {  // sequential column chain: one lane per row
+      const int rr = tid, row = r0 + rr;
+      float wv[P], sv[P], zv[P];
+#pragma unroll
+      for (int t = 0; t < P; ++t) {
+        wv[t] = t < pw ? Wb[rr * bwp + p0 + t] : 0.0f;
+        if (t < pw) load_sz<GATHER>(a, row, p0 + t, sv[t], zv[t]);
+        else { sv[t] = 1.0f; zv[t] = 0.0f; }
+      }
+#pragma unroll
+      for (int cc = 0; cc < P; ++cc) {
+        if (cc < pw) {
+          const float x = wv[cc];
+          float t = x / sv[cc];                               // :354
+          t = t + zv[cc];
+          t = t + 0.5f;
+          const float qi = clampf(floorf(t), a.minq, a.maxq);  // :355
+          const float qv = (qi - zv[cc]) * sv[cc];             // :356
+          const float err = x - qv;                            // :358
+          if (row < a.m) {
+            const int c = p0 + cc;
+            a.Q[size_t(row) * a.ldq + c] = qv;
+            a.E[size_t(row) * a.lde + c] = err;
+            if (a.codes) a.codes[size_t(row) * a.ldc + c] = uint8_t(int(qi) + a.code_off);
+          }
+          el[rr * (P + 1) + cc] = err;
+#pragma unroll
+          for (int j = cc + 1; j < P; ++j) {  // :377-386 inside the panel
+            const float d = err * cp[cc * P + j];
+            wv[j] = wv[j] - d;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // trailing update: columns after the panel, panel errors applied in order
+    const int jbeg = p0 + pw;
+    if (jbeg < a.bw) {
+      for (int j = jbeg + tid; j < a.bw; j += blockDim.x) {
+        float cv[P];
+#pragma unroll
+        for (int cc = 0; cc < P; ++cc) cv[cc] = a.corr[size_t(p0 + cc) * a.ldcorr + j];
+#pragma unroll 2
+        for (int rr = 0; rr < RW; ++rr) {
+          float w = Wb[rr * bwp + j];
+#pragma unroll
+          for (int cc = 0; cc < P; ++cc) {
+            const float d = el[rr * (P + 1) + cc] * cv[cc];
+            w = w - d;
+          }
+          Wb[rr * bwp + j] = w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A10: cross-block update W[:, i2:] -= E @ SM with FP32 MFMA (32x32x2).
+// acc starts at +0 and walks k in ascending order through one accumulator
+// per output element, so each output is the k-ordered fmaf chain.
+// Tile 128x128 per workgroup, 4 waves each 64x64 (2x2 MFMA tiles), K-step 32.
+// ---------------------------------------------------------------------------
+constexpr int GM = 128, GN = 128, GK = 32;
+
+__global__ __launch_bounds__(256) void cross_gemm_kernel(const float *__restrict__ E, int lde,
+                                                         const float *__restrict__ SM, int ldsm,
+                                                         float *__restrict__ W, int ldw, int m,
+                                                         int nc, int K) {
+  __shared__ float As[GM][GK + 1];
+  __shared__ float Bs[GK][GN];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tm = blockIdx.y * GM, tn = blockIdx.x * GN;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  for (int k0 = 0; k0 < K; k0 += GK) {
+    {  // A tile: 128 rows x 32 k
+      const int row = tid >> 1, kb = (tid & 1) * 16;
+      const int gi = tm + row;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int gk = k0 + kb + t;
+        As[row][kb + t] = (gi < m && gk < K) ? E[size_t(gi) * lde + gk] : 0.0f;
+      }
+    }
+    {  // B tile: 32 k x 128 cols
+      const int kr = tid >> 3, cb = (tid & 7) * 16;
+      const int gk = k0 + kr;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int gj = tn + cb + t;
+        Bs[kr][cb + t] = (gk < K && gj < nc) ? SM[size_t(gk) * ldsm + gj] : 0.0f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 2) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = As[wm * 64 + i * 32 + (lane & 31)][kk + (lane >> 5)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kk + (lane >> 5)][wn * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int gi = tm + wm * 64 + i * 32 + row;
+        const int gj = tn + wn * 64 + j * 32 + (lane & 31);
+        if (gi < m && gj < nc) {
+          float *p = W + size_t(gi) * ldw + gj;
+          *p = *p - acc[i][j][r];  // W[:, i2:] -= Global_delta   (:545)
+        }
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Tail RTN for truncated columns (:547-553) fused with the unpermute (:556-557).
+// ---------------------------------------------------------------------------
+__global__ void finalize_kernel(const float *__restrict__ Wp, const float *__restrict__ Qp,
+                                const uint8_t *__restrict__ cp, const int32_t *__restrict__ inv,
+                                const int32_t *__restrict__ perm, const float *__restrict__ scale,
+                                const float *__restrict__ zero, int G, int g, int n, int k,
+                                float minq, float maxq, int code_off, float *__restrict__ Wq,
+                                uint8_t *__restrict__ codes) {
+  const int r = blockIdx.y;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int c = inv[j];
+    const size_t o = size_t(r) * n + c;
+    float qv;
+    int code;
+    if (c >= k) {
+      const int gi = j / g;  // perm[c] == j
+      const float s = scale[size_t(r) * G + gi], z = zero[size_t(r) * G + gi];
+      float t = Wp[o] / s;
+      t = t + z;
+      const float qi = clampf(rintf(t), minq, maxq);  // torch.round: half-to-even
+      qv = (qi - z) * s;
+      code = int(qi) + code_off;
+    } else {
+      qv = Qp[o];
+      code = cp[o];
+    }
+    Wq[size_t(r) * n + j] = qv;
+    if (codes) codes[size_t(r) * n + j] = uint8_t(code);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A13: bit-stream packing (value i of a column at bits [i*b, i*b+b)).
+// ---------------------------------------------------------------------------
+__global__ void pack_codes_kernel(const uint8_t *__restrict__ codes, int m, int n, int b,
+                                  int32_t *__restrict__ qw) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;  // output feature
+  const int wi = blockIdx.y;                            // word along in_features
+  if (r >= m) return;
+  const int bit0 = wi * 32;
+  const int i0 = bit0 / b, i1 = min(n - 1, (bit0 + 31) / b);
+  uint64_t acc = 0;
+  for (int i = i0; i <= i1; ++i) {
+    const int64_t sh = int64_t(i) * b - bit0;
+    const uint64_t v = codes[size_t(r) * n + i] & ((1u << b) - 1);
+    if (sh >= 0) acc |= v << sh;
+    else acc |= v >> (-sh);
+  }
+  qw[size_t(wi) * m + r] = int32_t(uint32_t(acc & 0xffffffffu));
+}
+
+__global__ void pack_zeros_kernel(const float *__restrict__ zero, int m, int G, int b, int off,
+                                  int32_t *__restrict__ qz) {
+  const int gi = blockIdx.y;
+  const int wi = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nw = (m * b) / 32;
+  if (wi >= nw) return;
+  const int bit0 = wi * 32;
+  const int i0 = bit0 / b, i1 = min(m - 1, (bit0 + 31) / b);
+  uint64_t acc = 0;
+  for (int i = i0; i <= i1; ++i) {
+    const int64_t sh = int64_t(i) * b - bit0;
+    const uint64_t v = uint64_t(int(rintf(zero[size_t(i) * G + gi])) + off) & ((1u << b) - 1);
+    if (sh >= 0) acc |= v << sh;
+    else acc |= v >> (-sh);
+  }
+  qz[size_t(gi) * nw + wi] = int32_t(uint32_t(acc & 0xffffffffu));
+}
+
+size_t block_smem(int bw) { return sizeof(float) * (size_t(RW) * (bw + 1) + RW * (P + 1) + P * P); }
+
+constexpr int MAX_BLOCK = 2048;
+
+hipError_t ensure_block_smem() {
+  static bool done = false;  // per-process; attribute is per function, device-independent
+  if (done) return hipSuccess;
+  const int bytes = int(block_smem(MAX_BLOCK));
+  hipError_t e = hipFuncSetAttribute((const void *)block_kernel<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void *)block_kernel<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done = e == hipSuccess;
+  return e;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" int tg_group_params(void *stream, const float *W, int m, int n, int ldw, int group,
+                               int w_bits, int sym, float *scale, float *zero) {
+  TG_ARG(W, 2, "null W");
+  TG_ARG(m > 0, 3, "m <= 0");
+  TG_ARG(n > 0, 4, "n <= 0");
+  TG_ARG(ldw >= n, 5, "ldw < n");
+  const int g = group > 0 ? group : n;
+  TG_ARG(n % g == 0, 6, "n % group_size != 0 (gptq_utils.py:253)");
+  TG_ARG(w_bits >= 2 && w_bits <= 8, 7, "w_bits must be in [2, 8]");
+  TG_ARG(scale && zero, 9, "null output");
+  const int G = n / g;
+  const float maxq = sym ? float((1 << (w_bits - 1)) - 1) : float((1 << w_bits) - 1);
+  const int64_t waves = int64_t(m) * G;
+  hipLaunchKernelGGL(group_params_kernel, dim3(tg::cdiv(waves * 64, 256)), dim3(256), 0,
+                     (hipStream_t)stream, W, m, ldw, g, G, maxq, sym, scale, zero);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" int tg_process_block(void *stream, const float *w, int ldw, const float *s, int lds,
+                                const float *z, int ldz, const float *R, int ldr, int m, int B,
+                                int minq, int maxq, float *q, int ldq, float *e, int lde,
+                                void *ws, size_t ws_bytes) {
+  TG_ARG(w && s && z && R, 2, "null input");
+  TG_ARG(m > 0, 10, "m <= 0");
+  TG_ARG(B > 0 && B <= MAX_BLOCK, 11, "block width must be in [1, 2048]");
+  TG_ARG(q && e, 14, "null output");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  float *corr = ar.take<float>(size_t(B) * B);
+  TG_WS(ar);
+  TG_HIP(ensure_block_smem());
+  hipLaunchKernelGGL(prep_block_kernel, dim3(B), dim3(256), 0, st, R, ldr, B, 0, corr, B,
+                     (float *)nullptr, 0);
+  TG_LAUNCHED();
+  BlockArgs a{};
+  a.W = w; a.ldw = ldw; a.Q = q; a.ldq = ldq; a.codes = nullptr; a.ldc = 0; a.E = e; a.lde = lde;
+  a.corr = corr; a.ldcorr = B; a.s = s; a.lds = lds; a.z = z; a.ldz = ldz;
+  a.m = m; a.bw = B; a.minq = float(minq); a.maxq = float(maxq); a.code_off = 0;
+  hipLaunchKernelGGL(block_kernel<false>, dim3(tg::cdiv(m, RW)), dim3(256), block_smem(B), st, a);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" size_t tg_process_block_workspace_size(int B) { return sizeof(float) * size_t(B) * B + 512; }
+
+namespace {
+struct QuantWs {
+  float *Wp, *Qp, *E, *corr, *SM;
+  uint8_t *cp;
+  int32_t *inv, *perm32;
+};
+template <class A>
+void quant_layout(A &ar, int m, int n, int block, QuantWs *p) {
+  const int bp = (block + 31) & ~31;
+  auto t = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  QuantWs d{};
+  QuantWs &q = p ? *p : d;
+  t(q.Wp, size_t(m) * n);
+  t(q.Qp, size_t(m) * n);
+  t(q.E, size_t(m) * bp);
+  t(q.corr, size_t(bp) * bp);
+  t(q.SM, size_t(bp) * n);
+  t(q.cp, size_t(m) * n);
+  t(q.inv, size_t(n));
+  t(q.perm32, size_t(n));
+}
+}  // namespace
+
+extern "C" size_t tg_quantize_workspace_size(int m, int n, int block) {
+  tg::Sizer s;
+  quant_layout(s, m, n, block, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, const float *U, int k,
+                                int ldu, const int64_t *perm, const float *scale,
+                                const float *zero, int group, int w_bits, int sym, int block,
+                                float *Wq, uint8_t *codes, void *ws, size_t ws_bytes) {
+  TG_ARG(W, 2, "null W");
+  TG_ARG(m > 0, 3, "m <= 0");
+  TG_ARG(n > 0, 4, "n <= 0");
+  TG_ARG(U, 5, "null U");
+  TG_ARG(k >= 1 && k <= n, 6, "rank k must be in [1, n]");
+  TG_ARG(ldu >= n, 7, "ldu < n");
+  TG_ARG(perm, 8, "null perm");
+  TG_ARG(scale && zero, 9, "null scale/zero");
+  const int g = group > 0 ? group : n;
+  TG_ARG(n % g == 0, 11, "n % group_size != 0");
+  TG_ARG(w_bits >= 2 && w_bits <= 8, 12, "w_bits must be in [2, 8]");
+  TG_ARG(block >= 1 && block <= MAX_BLOCK, 14, "block_size must be in [1, 2048]");
+  TG_ARG(Wq, 15, "null output");
+  hipStream_t st = (hipStream_t)stream;
+  TG_HIP(ensure_block_smem());
+  tg::Arena ar(ws, ws_bytes);
+  QuantWs q{};
+  quant_layout(ar, m, n, block, &q);
+  TG_WS(ar);
+  const int G = n / g;
+  const float minq = sym ? -float((1 << (w_bits - 1)) - 1) : 0.0f;
+  const float maxq = sym ? float((1 << (w_bits - 1)) - 1) : float((1 << w_bits) - 1);
+  const int code_off = sym ? (1 << (w_bits - 1)) : 0;
+  const int bp = (block + 31) & ~31;
+
+  hipLaunchKernelGGL(invperm_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, perm, n, q.inv,
+                     q.perm32);
+  TG_LAUNCHED();
+  hipLaunchKernelGGL(permute_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, m),
+                     dim3(256), 0, st, W, n, q.perm32, q.Wp);
+  TG_LAUNCHED();
+
+  for (int i1 = 0; i1 < k; i1 += block) {
+    const int i2 = min(i1 + block, k);
+    const int bw = i2 - i1;
+    const int nc = n - i2;
+    hipLaunchKernelGGL(prep_block_kernel, dim3(bw), dim3(256), 0, st, U + size_t(i1) * ldu + i1,
+                       ldu, bw, nc, q.corr, bp, q.SM, n);
+    TG_LAUNCHED();
+    BlockArgs a{};
+    a.W = q.Wp + i1; a.ldw = n; a.Q = q.Qp + i1; a.ldq = n; a.codes = q.cp + i1; a.ldc = n;
+    a.E = q.E; a.lde = bp; a.corr = q.corr; a.ldcorr = bp;
+    a.scale = scale; a.zero = zero; a.perm = q.perm32; a.G = G; a.g = g; a.col0 = i1;
+    a.m = m; a.bw = bw; a.minq = minq; a.maxq = maxq; a.code_off = code_off;
+    hipLaunchKernelGGL(block_kernel<true>, dim3(tg::cdiv(m, RW)), dim3(256), block_smem(bw), st,
+                       a);
+    TG_LAUNCHED();
+    if (nc > 0) {
+      hipLaunchKernelGGL(cross_gemm_kernel, dim3(tg::cdiv(nc, GN), tg::cdiv(m, GM)), dim3(256), 0,
+                         st, q.E, bp, q.SM, n, q.Wp + i2, n, m, nc, bw);
+      TG_LAUNCHED();
+    }
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, m),
+                     dim3(256), 0, st, q.Wp, q.Qp, q.cp, q.inv, q.perm32, scale, zero, G, g, n, k,
+                     minq, maxq, code_off, Wq, codes);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" int tg_pack_codes(void *stream, const uint8_t *codes, int m, int n, int w_bits,
+                             int32_t *qweight) {
+  TG_ARG(codes, 2, "null codes");
+  TG_ARG(m > 0, 3, "m <= 0");
+  TG_ARG(n > 0, 4, "n <= 0");
+  TG_ARG(w_bits >= 2 && w_bits <= 8, 5, "w_bits must be in [2, 8]");
+  TG_ARG((int64_t(n) * w_bits) % 32 == 0, 4, "n * w_bits must be a multiple of 32");
+  TG_ARG(qweight, 6, "null output");
+  const int nw = int((int64_t(n) * w_bits) / 32);
+  hipLaunchKernelGGL(pack_codes_kernel, dim3(tg::cdiv(m, 256), nw), dim3(256), 0,
+                     (hipStream_t)stream, codes, m, n, w_bits, qweight);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" int tg_pack_zeros(void *stream, const float *zero, int m, int G, int w_bits, int sym,
+                             int32_t *qzeros) {
+  TG_ARG(zero, 2, "null zero");
+  TG_ARG(m > 0, 3, "m <= 0");
+  TG_ARG(G > 0, 4, "G <= 0");
+  TG_ARG(w_bits >= 2 && w_bits <= 8, 5, "w_bits must be in [2, 8]");
+  TG_ARG((int64_t(m) * w_bits) % 32 == 0, 3, "m * w_bits must be a multiple of 32");
+  TG_ARG(qzeros, 7, "null output");
+  const int nw = int((int64_t(m) * w_bits) / 32);
+  const int off = sym ? (1 << (w_bits - 1)) : 0;
+  hipLaunchKernelGGL(pack_zeros_kernel, dim3(tg::cdiv(nw, 256), G), dim3(256), 0,
+                     (hipStream_t)stream, zero, m, G, w_bits, off, qzeros);
+  TG_LAUNCHED();
+  return 0;
+}

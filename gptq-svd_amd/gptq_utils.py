@@ -1,0 +1,282 @@
+"""Drop-in counterpart of the reference solver API on MI355X.
+
+Mirrors the names, argument meaning and error behaviour of
+``/root/reference/src/TruncGPTQ/gptq_utils.py`` so the layer-sequential harness
+(``quantize.py:14``) only has to change its import line:
+
+    from gptq_svd_amd.gptq_utils import (gptq_fwrd, Quantizer, process_hessian_alt,
+                                         HessianAccumulator)
+
+Every numerical stage runs in the HIP library (``libtruncgptq.so``, C ABI in
+``include/truncgptq.h``) on the caller's current HIP stream; torch provides
+device memory, streams and the caching allocator only.  There is no CPU
+fallback: CPU tensors raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream, workspace
+
+__all__ = [
+    "HessianAccumulator", "process_hessian_alt", "Quantizer", "gptq_fwrd",
+    "triton_process_block", "log_quantization_error", "next_power_of_2",
+    "truncated_spectral_factor", "pack_quantized",
+]
+
+
+# ---------------------------------------------------------------------------
+# A1  (gptq_utils.py:213-228)
+# ---------------------------------------------------------------------------
+class HessianAccumulator:
+    """H += x^T x in float64 (FP64 MFMA SYRK kernel); get_hessian() = H / N."""
+
+    def __init__(self, in_features, device, dtype=torch.float64):
+        if dtype != torch.float64:
+            raise RuntimeError("HessianAccumulator: only float64 accumulation is supported")
+        self.H = torch.zeros((in_features, in_features), device=device, dtype=dtype)
+        _lib.require_cuda(self.H, "HessianAccumulator device")
+        self.n_samples = 0
+
+    def add_batch(self, x):                                   # gptq_utils.py:218-223
+        if x.dim() == 3:
+            x = x.reshape(-1, x.shape[-1])
+        _lib.require_cuda(x, "add_batch input")
+        if x.dtype not in _lib.DTYPES:
+            x = x.to(torch.float64)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        rows, n = x.shape
+        if n != self.H.shape[0]:
+            raise RuntimeError(f"add_batch: expected {self.H.shape[0]} features, got {n}")
+        if rows:
+            with torch.cuda.device(self.H.device):
+                call("tg_syrk_accum", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
+                     x.stride(0), ptr(self.H), self.H.shape[0])
+        self.n_samples += rows
+
+    def get_hessian(self):                                    # gptq_utils.py:225-228
+        if self.n_samples == 0:
+            return self.H
+        out = torch.empty_like(self.H)
+        with torch.cuda.device(self.H.device):
+            call("tg_scale_f64", stream(), ptr(self.H), self.H.numel(),
+                 -float(self.n_samples), ptr(out))
+        return out
+
+
+# ---------------------------------------------------------------------------
+# A2-A5  (gptq_utils.py:87-126)
+# ---------------------------------------------------------------------------
+def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
+                              threshold_method: str = "mean_trimmed", want_rx: bool = True):
+    """Native pipeline behind process_hessian_alt.  Returns (U, R_x, perm, S, k).
+
+    eigh (Householder tridiagonalisation + bisection + inverse iteration +
+    blocked back-transform) -> rank rule -> greedy-pivoted factor of
+    H_k = S_k^T S_k (the dgeqp3 pivot order and R_x) -> U.
+    """
+    _lib.require_cuda(H, "process_hessian_alt H")
+    n = H.shape[0]
+    if H.dim() != 2 or H.shape[1] != n:
+        raise RuntimeError("process_hessian_alt: H must be square")
+    dev = H.device
+    rule = _lib.RULES.get(threshold_method, 0)
+    with torch.cuda.device(dev):
+        A = H.to(dtype=torch.float64).contiguous().clone()
+        ws = workspace(_lib.lib.tg_eigh_workspace_size(n), dev)
+        w = torch.empty(n, dtype=torch.float64, device=dev)
+        call("tg_eigh_values", stream(), ptr(A), n, n, ptr(w), ptr(ws), ws.numel())
+        S = torch.empty(n, dtype=torch.float64, device=dev)
+        kdev = torch.empty(1, dtype=torch.int32, device=dev)
+        call("tg_truncation_rank", stream(), ptr(w), n, float(threshold), rule, ptr(S), ptr(kdev))
+        k = int(kdev.item())  # the reference syncs here too (gptq_utils.py:100, :106)
+        if k < 1:
+            raise RuntimeError("process_hessian_alt: truncation rank is 0 "
+                               "(threshold keeps no eigenvalue)")
+        del A
+        Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
+        call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
+        del ws
+        perm = torch.empty(n, dtype=torch.int64, device=dev)
+        R_x = torch.empty((k, n), dtype=torch.float64, device=dev) if want_rx else None
+        ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+        call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(R_x),
+             n, ptr(ws), ws.numel())
+        del ws
+        U = torch.empty((k, n), dtype=torch.float64, device=dev)
+        ws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
+        call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n,
+             ptr(ws), ws.numel())
+    return U, R_x, perm, S, k
+
+
+def process_hessian_alt(H: torch.Tensor, threshold: float = 0.0005,
+                        threshold_method: str = "mean_trimmed"
+                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Returns (R, R_x, perm) exactly like gptq_utils.py:87-126:
+    R = U (k x n float64, upper trapezoidal, positive diagonal),
+    R_x (k x n float64), perm (n int64)."""
+    U, R_x, perm, _, _ = truncated_spectral_factor(H, threshold, threshold_method)
+    return U, R_x, perm
+
+
+# ---------------------------------------------------------------------------
+# A7  (gptq_utils.py:230-272)
+# ---------------------------------------------------------------------------
+class Quantizer:
+    """Static-group min/max (asym) or absmax (sym) quantizer; same fields and
+    shapes as the reference (scale/zero: (m, n/g, 1) float32)."""
+
+    def __init__(self, w_bits: int = 4, group_size: int = 128, sym: bool = False):
+        self.w_bits = w_bits
+        self.group_size = group_size
+        self.sym = sym
+        if self.sym:
+            half_range = 2 ** (w_bits - 1) - 1
+            self.max_q = half_range
+            self.min_q = -half_range
+        else:
+            self.max_q = 2 ** w_bits - 1
+            self.min_q = 0
+        self.scale = None
+        self.zero = None
+
+    def find_params(self, weights: torch.Tensor):            # gptq_utils.py:249-266
+        _lib.require_cuda(weights, "Quantizer.find_params weights")
+        m, n = weights.shape
+        g = self.group_size if self.group_size > 0 else n
+        assert n % g == 0
+        W = weights.to(torch.float32).contiguous()
+        G = n // g
+        scale = torch.empty((m, G), dtype=torch.float32, device=W.device)
+        zero = torch.empty((m, G), dtype=torch.float32, device=W.device)
+        with torch.cuda.device(W.device):
+            call("tg_group_params", stream(), ptr(W), m, n, n, self.group_size, self.w_bits,
+                 int(self.sym), ptr(scale), ptr(zero))
+        self.scale = scale.unsqueeze(-1)
+        self.zero = zero.unsqueeze(-1)
+
+    def get_expanded_params(self, m, n):                       # gptq_utils.py:268-272
+        g = self.group_size if self.group_size > 0 else n
+        s_expanded = torch.repeat_interleave(self.scale, g, dim=1)
+        z_expanded = torch.repeat_interleave(self.zero, g, dim=1)
+        return s_expanded[:, :n].squeeze(-1), z_expanded[:, :n].squeeze(-1)
+
+
+# ---------------------------------------------------------------------------
+# A6  (gptq_utils.py:275-291)
+# ---------------------------------------------------------------------------
+def log_quantization_error(W_orig, W_quant, R_x, perm):
+    if R_x is None or perm is None:
+        return None
+    R_mat = R_x.to(device=W_orig.device, dtype=torch.float32)
+    W_o = W_orig[:, perm]
+    W_q = W_quant[:, perm]
+    y_orig_norm = torch.linalg.norm(torch.matmul(W_o, R_mat.T))
+    y_diff_norm = torch.linalg.norm(torch.matmul(W_o - W_q, R_mat.T))
+    relative_error = (y_diff_norm / y_orig_norm).item()
+    logging.info(f"   [Metric] Relative prediction error: {relative_error:.6f}")
+    return relative_error
+
+
+# ---------------------------------------------------------------------------
+# A9  (gptq_utils.py:389-453)
+# ---------------------------------------------------------------------------
+def next_power_of_2(x: int) -> int:
+    return 1 if x == 0 else 2 ** (x - 1).bit_length()
+
+
+def triton_process_block(w_block, s_block, z_block, R_block, quantizer):
+    """Quantize one block with in-block error propagation -> (q, e).
+    The reference pads to a power of two (:404-420); padding never feeds a
+    real column, so the HIP kernel works on the exact width."""
+    for t, nm in ((w_block, "w_block"), (s_block, "s_block"), (z_block, "z_block"),
+                  (R_block, "R_block")):
+        _lib.require_cuda(t, nm)
+    m, B = w_block.shape
+    f = lambda t: t.to(torch.float32).contiguous()
+    w, s, z, R = f(w_block), f(s_block), f(z_block), f(R_block)
+    q = torch.empty_like(w)
+    e = torch.empty_like(w)
+    with torch.cuda.device(w.device):
+        ws = workspace(_lib.lib.tg_process_block_workspace_size(B), w.device)
+        call("tg_process_block", stream(), ptr(w), B, ptr(s), B, ptr(z), B, ptr(R), B, m, B,
+             int(quantizer.min_q), int(quantizer.max_q), ptr(q), B, ptr(e), B, ptr(ws),
+             ws.numel())
+    return q, e
+
+
+# ---------------------------------------------------------------------------
+# A8-A12  (gptq_utils.py:459-565)
+# ---------------------------------------------------------------------------
+def gptq_fwrd(weight_mat: torch.Tensor, H_inv_sqrt: torch.Tensor, quantizer: Quantizer,
+              perm: torch.Tensor, block_size: int = 128, use_triton: bool = True,
+              R_x: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
+    """Column-wise quantize + error propagation driven by U (= H_inv_sqrt).
+
+    Returns (dequantised W in the original column order and dtype, rank).
+    The integer codes of the last call are kept on ``quantizer.codes``
+    (uint8, original order, +2^(b-1) offset when sym) for packing.
+    """
+    if not use_triton:
+        raise NotImplementedError(
+            "gptq_fwrd(use_triton=False) is the reference's GPTQ-comparator loop "
+            "(gptq_utils.py:516-534); it is not part of the TruncGPTQ hot path yet")
+    allow_tf32 = torch.backends.cuda.matmul.allow_tf32       # :474-475, restored :565
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        _lib.require_cuda(weight_mat, "gptq_fwrd weight_mat")
+        out_features, in_features = weight_mat.shape
+        device = weight_mat.device
+        orig_dtype = weight_mat.dtype
+        weight_mat = weight_mat.to(device=device, dtype=torch.float32).contiguous()
+        U = H_inv_sqrt.to(device=device, dtype=torch.float32).contiguous()
+        current_rank = U.shape[0]
+        if current_rank < in_features:
+            logging.info(f"   Rank percent used: {float(current_rank) / in_features:.2%}")
+        quantizer.find_params(weight_mat)
+        perm_d = perm.to(device=device, dtype=torch.int64).contiguous()
+        scale = quantizer.scale.squeeze(-1).contiguous()
+        zero = quantizer.zero.squeeze(-1).contiguous()
+        Wq = torch.empty_like(weight_mat)
+        codes = torch.empty((out_features, in_features), dtype=torch.uint8, device=device)
+        with torch.cuda.device(device):
+            ws = workspace(_lib.lib.tg_quantize_workspace_size(out_features, in_features,
+                                                               block_size), device)
+            call("tg_gptq_quantize", stream(), ptr(weight_mat), out_features, in_features,
+                 ptr(U), current_rank, U.shape[1], ptr(perm_d), ptr(scale), ptr(zero),
+                 quantizer.group_size, quantizer.w_bits, int(quantizer.sym), block_size,
+                 ptr(Wq), ptr(codes), ptr(ws), ws.numel())
+        quantizer.codes = codes
+        if R_x is not None:
+            log_quantization_error(weight_mat, Wq, R_x, perm_d)
+        return Wq.to(dtype=orig_dtype), current_rank
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = allow_tf32
+
+
+# ---------------------------------------------------------------------------
+# A13  packing (new; the reference saves dequantised FP16 only, README.md:133)
+# ---------------------------------------------------------------------------
+def pack_quantized(quantizer: Quantizer, codes: Optional[torch.Tensor] = None):
+    """AutoGPTQ-style tensors from the last gptq_fwrd: qweight int32
+    (n*b/32, m), qzeros int32 (n/g, m*b/32), scales float32 (n/g, m).
+    Static groups in original column order, so no g_idx is needed."""
+    codes = quantizer.codes if codes is None else codes
+    m, n = codes.shape
+    b = quantizer.w_bits
+    zero = quantizer.zero.squeeze(-1).contiguous()
+    G = zero.shape[1]
+    dev = codes.device
+    qweight = torch.empty((n * b // 32, m), dtype=torch.int32, device=dev)
+    qzeros = torch.empty((G, m * b // 32), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        call("tg_pack_codes", stream(), ptr(codes.contiguous()), m, n, b, ptr(qweight))
+        call("tg_pack_zeros", stream(), ptr(zero), m, G, b, int(quantizer.sym), ptr(qzeros))
+    scales = quantizer.scale.squeeze(-1).t().contiguous()
+    return qweight, qzeros, scales

@@ -1,0 +1,117 @@
+/* truncgptq.h -- C ABI of the MI355X-native TruncGPTQ per-layer solver.
+ *
+ * Every entry point takes plain device pointers, explicit sizes / leading
+ * dimensions (row-major, element units) and the caller's hipStream_t
+ * (passed as void* so this header needs no HIP include).  Work is
+ * stream-ordered; nothing here synchronises the device unless the comment
+ * says so.  Scratch memory comes from the caller (`ws`, `ws_bytes`), sized
+ * by the matching *_workspace_size() query; the library allocates nothing.
+ *
+ * Return value: 0 ok; <0 invalid argument (-(1-based argument index));
+ * >0 a hipError_t.  tg_last_error() returns a thread-local message.
+ *
+ * Reference = /root/reference/src/TruncGPTQ (davidtweedle/gptq-svd).
+ */
+#ifndef TRUNCGPTQ_H
+#define TRUNCGPTQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- misc --------------------------------------------------------------- */
+const char *tg_last_error(void);
+int tg_version(void);
+
+enum tg_dtype { TG_F16 = 0, TG_BF16 = 1, TG_F32 = 2, TG_F64 = 3 };
+enum tg_rank_rule { TG_RULE_NONE = 0, TG_RULE_ENERGY = 1, TG_RULE_MEAN_TRIMMED = 2 };
+
+/* ---- A1: Hessian accumulation -------------------------------------------
+ * Replaces HessianAccumulator.add_batch: `self.H.addmm_(x.T, x)` after the
+ * cast to float64 (gptq_utils.py:218-223).  H (n x n, ld ldh) += X^T X where
+ * X is (rows x n, ld ldx) of dtype x_dtype (products formed in float64).
+ * Both triangles of H are written (the reference keeps the full matrix). */
+int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n, int64_t ldx,
+                  double *H, int ldh);
+
+/* Replaces HessianAccumulator.get_hessian `self.H / self.n_samples`
+ * (gptq_utils.py:225-228).  inv_n > 0: out = H * inv_n; inv_n < 0:
+ * out = H / (-inv_n) (exact true division, the reference's semantics).
+ * out may alias H. */
+int tg_scale_f64(void *stream, const double *H, int64_t count, double inv_n, double *out);
+
+/* ---- A2: symmetric eigensolver (torch.linalg.eigh, gptq_utils.py:93) ----
+ * Stage 1: A (n x n symmetric, full storage, destroyed) -> tridiagonal
+ * (Householder, lower) + all eigenvalues ascending in w_asc (n).  The
+ * reflectors stay in ws for stage 2. */
+size_t tg_eigh_workspace_size(int n);
+int tg_eigh_values(void *stream, double *A, int n, int lda, double *w_asc, void *ws,
+                   size_t ws_bytes);
+/* Stage 2: eigenvectors of the `k` LARGEST eigenvalues, in DESCENDING order,
+ * written as ROWS of Vh (k x n, ld ldv) -- i.e. the reference's
+ * `V.T.flip(0)[:k]` (gptq_utils.py:95,110).  Uses the stage-1 workspace. */
+int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, double *Vh, int ldv,
+                    void *ws, size_t ws_bytes);
+
+/* ---- A3: truncation rank (gptq_utils.py:97-108) ---------------------------
+ * From ascending eigenvalues: S = sqrt(max(L, 1e-12)) descending, then the
+ * rank rule.  Writes S_desc (n) and k (int32, device) -- no host sync. */
+int tg_truncation_rank(void *stream, const double *w_asc, int n, double threshold, int rule,
+                       double *S_desc, int32_t *k_dev);
+
+/* ---- A4: pivot order + R_x (jax.scipy.linalg.qr(pivoting=True) on
+ * S_k = diag(S) Vh_k, gptq_utils.py:112-117, 122-123) -----------------------
+ * Computes the dgeqp3 column order `perm` (n, int64) and the sign-normalised
+ * R_x (k x n upper trapezoidal, ld ldr; may be NULL).  Algorithm: greedy
+ * diagonal pivoting on H_k = S_k^T S_k (identical pivot rule to dgeqp3; see
+ * DESIGN.md). */
+size_t tg_pivot_workspace_size(int n, int k);
+int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const double *S, int n, int k,
+                      int64_t *perm, double *Rx, int ldr, void *ws, size_t ws_bytes);
+
+/* ---- A5: U = sign-normalised R of QR(diag(1/S) Vh_k[:, perm])
+ * (gptq_utils.py:111, 118-124).  U (k x n, ld ldu) upper trapezoidal with
+ * positive diagonal; U^T U = P^T H_k^+ P. */
+size_t tg_ufactor_workspace_size(int n, int k);
+int tg_u_factor(void *stream, const double *Vh, int ldv, const double *S, const int64_t *perm,
+                int n, int k, double *U, int ldu, void *ws, size_t ws_bytes);
+
+/* ---- A7: Quantizer.find_params (gptq_utils.py:249-266) --------------------
+ * W (m x n f32, ld ldw) -> scale, zero (m x n/g f32, ld n/g); g = group or n. */
+int tg_group_params(void *stream, const float *W, int m, int n, int ldw, int group, int w_bits,
+                    int sym, float *scale, float *zero);
+
+/* ---- A9: triton_process_block (gptq_utils.py:393-453, kernel :298-386) ----
+ * One block: w, s, z (m x B f32, ld ldw/lds/ldz), R (B x B f32, ld ldr).
+ * Outputs q (dequantised) and e (raw error), m x B, ld ldq / lde. */
+size_t tg_process_block_workspace_size(int B);
+int tg_process_block(void *stream, const float *w, int ldw, const float *s, int lds,
+                     const float *z, int ldz, const float *R, int ldr, int m, int B, int minq,
+                     int maxq, float *q, int ldq, float *e, int lde, void *ws, size_t ws_bytes);
+
+/* ---- A8-A12: gptq_fwrd(use_triton=True) (gptq_utils.py:459-565) ---------
+ * W (m x n f32, original column order), U (k x n f32, ld ldu), perm (n
+ * int64), scale/zero from tg_group_params.  Writes Wq (m x n f32,
+ * dequantised, original order) and codes (m x n uint8, original order,
+ * stored +2^(b-1) when sym).  `block` is the reference's block_size. */
+size_t tg_quantize_workspace_size(int m, int n, int block);
+int tg_gptq_quantize(void *stream, const float *W, int m, int n, const float *U, int k, int ldu,
+                     const int64_t *perm, const float *scale, const float *zero, int group,
+                     int w_bits, int sym, int block, float *Wq, uint8_t *codes, void *ws,
+                     size_t ws_bytes);
+
+/* ---- A13: packing (absent in the reference; README.md:133) ----------------
+ * codes (m x n uint8, offset form) -> qweight (n*b/32 x m int32, bit stream
+ * along in_features; AutoGPTQ layout for b in {2,3,4,8}); zero (m x G f32)
+ * -> qzeros (G x m*b/32 int32, stored zero + 2^(b-1) when sym). */
+int tg_pack_codes(void *stream, const uint8_t *codes, int m, int n, int w_bits, int32_t *qweight);
+int tg_pack_zeros(void *stream, const float *zero, int m, int G, int w_bits, int sym,
+                  int32_t *qzeros);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRUNCGPTQ_H */
