@@ -31,6 +31,7 @@ _SIGS = {
     "tg_version": ([], _i),
     "tg_syrk_accum": ([_vp, _vp, _i, _i64, _i, _i64, _vp, _i], _i),
     "tg_scale_f64": ([_vp, _vp, _i64, _d, _vp], _i),
+    "tg_dgemm": ([_vp, _i, _i, _i, _i, _i, _d, _vp, _i, _vp, _i, _d, _vp, _i], _i),
     "tg_eigh_workspace_size": ([_i], _sz),
     "tg_eigh_values": ([_vp, _vp, _i, _i, _vp, _vp, _sz], _i),
     "tg_eigh_vectors": ([_vp, _i, _vp, _i, _vp, _i, _vp, _sz], _i),

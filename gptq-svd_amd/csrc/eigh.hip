@@ -1,0 +1,713 @@
+// Symmetric eigensolver for the TruncGPTQ spectral factorisation (A2, A3).
+//
+// Replaces `L, V = torch.linalg.eigh(H_double)` + the descending flip and the
+// rank rule of process_hessian_alt
+// (/root/reference/src/TruncGPTQ/gptq_utils.py:92-110), which the reference
+// runs through cuSOLVER syevd.  MI355X-native pipeline:
+//
+//   1. Householder tridiagonalisation A = Q T Q^T, blocked like LAPACK dlatrd
+//      (panels of NB columns).  Per column: one row-parallel kernel computes
+//      the reflector and y = A v (memory-bound, every CU streams rows of the
+//      Infinity-Cache-resident trailing matrix), one kernel finishes the panel
+//      column of W and updates the next column.  Cross-workgroup sums use the
+//      deterministic last-arriver reduction (reduce.h).  Between panels the
+//      trailing matrix takes the rank-2NB update A -= V W^T + W V^T on FP64
+//      MFMA (gemm64.hip).
+//   2. All eigenvalues of T by Sturm-count multisection: 16 lanes per
+//      eigenvalue evaluate 16 shifts per round (interval shrinks 17x/round).
+//   3. Eigenvectors of T for the k largest eigenvalues by inverse iteration
+//      (tridiagonal LU with partial pivoting, 3 solves from a per-index
+//      pseudo-random start); tight clusters are re-orthogonalised (MGS).
+//   4. Back-transformation V = Q Z with compact-WY blocks of BT reflectors
+//      (dlarft T factors, FP64 MFMA GEMMs, split-K for the V^T Z products).
+#include <cfloat>
+#include <cmath>
+#include <type_traits>
+
+#include "../../include/truncgptq.h"
+#include "common.h"
+#include "gemm64.h"
+#include "reduce.h"
+
+namespace {
+
+constexpr int NB = 32;    // tridiagonalisation panel width
+constexpr int NG = 256;   // workgroups of the row-parallel kernels
+constexpr int BT = 64;    // back-transformation block of reflectors
+constexpr int PST = 2 * NB + 2;  // partials stride
+constexpr int ML = 16;    // multisection lanes per eigenvalue
+constexpr int ROUNDS = 16;  // 17^16 > 2^65: interval shrinks below one ulp
+constexpr int SPLITK = 8;
+
+struct Tri {
+  double *V;     // n x n reflectors: V[r*n + j] = v_j[r] (0 above j+1, 1 at r = j+1)
+  double *W;     // n x NB  dlatrd panel W
+  double *tau;   // n
+  double *d;     // n   diagonal of T
+  double *e;     // n   off-diagonal of T (e[i] couples i, i+1)
+  double *acol;  // n   current updated column
+  double *y;     // n   symv result
+  double *part;  // NG x PST partial sums
+  double *red;   // PST reduced sums: [0] = |x|^2, [1..NB] = V^T v, [1+NB..2NB] = W^T v, [1+2NB] = v^T y
+  double *Tf;    // nblk x BT x BT  block-reflector T factors
+  double *Z;     // n x n  eigenvectors of T (column j), later of A
+  double *lu;    // 4 x n x n  inverse-iteration LU factors ([i][thread] layout)
+  double *X1;    // BT x n
+  double *X2;    // BT x n
+  double *skp;   // split-K scratch
+  double *scal;  // small scalars (norm of T)
+  unsigned *cnt; // reduction tickets
+  int8_t *piv;   // n x n pivot flags
+};
+
+template <class A>
+void tri_layout(A &ar, int n, Tri *t) {
+  Tri d{};
+  Tri &q = t ? *t : d;
+  const size_t nn = size_t(n) * n;
+  const int nblk = tg::cdiv(n, BT);
+  auto take = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  take(q.V, nn);
+  take(q.W, size_t(n) * NB);
+  take(q.tau, n);
+  take(q.d, n);
+  take(q.e, n);
+  take(q.acol, n);
+  take(q.y, n);
+  take(q.part, size_t(NG) * PST);
+  take(q.red, PST);
+  take(q.Tf, size_t(nblk) * BT * BT);
+  take(q.Z, nn);
+  take(q.lu, 4 * nn);
+  take(q.X1, size_t(BT) * n);
+  take(q.X2, size_t(BT) * n);
+  take(q.skp, size_t(SPLITK) * BT * n);
+  take(q.scal, 16);
+  take(q.cnt, 16);
+  take(q.piv, nn);
+}
+
+// ---------------------------------------------------------------------------
+// 1. tridiagonalisation kernels
+// ---------------------------------------------------------------------------
+
+// Panel start at column i (no pending panel corrections): acol = A[i:, i]
+// (= row i by symmetry), d[i], and |x|^2 of A[i+2:, i].
+__global__ __launch_bounds__(256) void tri_start_kernel(const double *__restrict__ A, int lda,
+                                                        int n, int i, Tri w) {
+  __shared__ double scratch[8];
+  __shared__ double vals[1];
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  double s = 0.0;
+  for (int r = i + gtid; r < n; r += gridDim.x * blockDim.x) {
+    const double a = A[size_t(i) * lda + r];
+    w.acol[r] = a;
+    if (r == i) w.d[i] = a;
+    if (r >= i + 2) s += a * a;
+  }
+  s = tg::block_sum(s, scratch);
+  if (threadIdx.x == 0) vals[0] = s;
+  __syncthreads();
+  if (tg::publish_partials(vals, 1, w.part, PST, w.cnt)) tg::sum_partials(w.part, PST, 1, w.red, w.cnt);
+}
+
+// Reflector for column i + y = A[i+1:, i+1:] v + partial V^T v, W^T v, v^T y.
+// VLDS: v staged in LDS (n <= 16384); otherwise v_c = acol[c] * scal on the fly.
+template <bool VLDS>
+__global__ __launch_bounds__(256) void tri_symv_kernel(const double *__restrict__ A, int lda, int n,
+                                                       int i, int p, Tri w) {
+  extern __shared__ double vsh[];  // n - i - 1 entries of v
+  __shared__ double wpart[4][PST];
+  __shared__ double vals[PST];
+  const int t = i - p;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int len = n - i - 1;
+  // dlarfg (LAPACK): beta = -sign(alpha) * hypot(alpha, |x|), tau = (beta-alpha)/beta,
+  // v = [1, x / (alpha - beta)]
+  const double xn2 = w.red[0];
+  const double alpha = w.acol[i + 1];
+  double tau = 0.0, beta = alpha, scal = 0.0;
+  if (xn2 > 0.0) {
+    beta = -copysign(hypot(alpha, sqrt(xn2)), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  if (VLDS)
+    for (int c = tid; c < len; c += blockDim.x) vsh[c] = c == 0 ? 1.0 : w.acol[i + 1 + c] * scal;
+  const double *ac = w.acol + i + 1;
+  auto vget = [&](int c) -> double {
+    if (VLDS) return vsh[c];
+    return c == 0 ? 1.0 : ac[c] * scal;
+  };
+  if (blockIdx.x == 0 && tid == 0) {
+    w.tau[i] = tau;
+    w.e[i] = beta;
+  }
+  for (int j = tid; j < 4 * PST; j += blockDim.x) (&wpart[0][0])[j] = 0.0;
+  __syncthreads();
+
+  double q1 = 0.0, q2 = 0.0, sv = 0.0;  // per-lane partials (lane l -> panel column l)
+  const int gw = blockIdx.x * 4 + wid;
+  for (int r = i + 1 + gw; r < n; r += NG * 4) {
+    const double *row = A + size_t(r) * lda + (i + 1);
+    double dot = 0.0;
+    for (int c = lane; c < len; c += 64) dot += row[c] * vget(c);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+    const double vr = vget(r - i - 1);
+    if (lane == 0) {
+      w.y[r] = dot;
+      w.V[size_t(r) * n + i] = vr;
+      sv += vr * dot;
+    }
+    if (lane < t) {
+      q1 += w.V[size_t(r) * n + p + lane] * vr;
+      q2 += w.W[size_t(r) * NB + lane] * vr;
+    }
+  }
+  if (lane < NB) {
+    wpart[wid][lane] = q1;
+    wpart[wid][NB + lane] = q2;
+  }
+  if (lane == 0) wpart[wid][2 * NB] = sv;
+  __syncthreads();
+  constexpr int NV = 2 * NB + 1;
+  for (int j = tid; j < NV; j += blockDim.x)
+    vals[j] = wpart[0][j] + wpart[1][j] + wpart[2][j] + wpart[3][j];
+  __syncthreads();
+  if (tg::publish_partials(vals, NV, w.part, PST, w.cnt))
+    tg::sum_partials(w.part, PST, NV, w.red + 1, w.cnt);
+}
+
+// W[:, t] = tau (y - V (W^T v) - W (V^T v)) + alpha2 v, then (do_next) update
+// column i+1 with the panel's t+1 reflectors and reduce its |x|^2.
+__global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__ A, int lda, int n,
+                                                      int i, int p, int do_next, Tri w) {
+  __shared__ double q1[NB], q2[NB], vrow[NB], wrow[NB];
+  __shared__ double scratch[8];
+  __shared__ double vals[1];
+  const int t = i - p, j = i + 1;
+  const int tid = threadIdx.x;
+  const double tau = w.tau[i];
+  if (tid < NB) {
+    q1[tid] = tid < t ? w.red[1 + tid] : 0.0;
+    q2[tid] = tid < t ? w.red[1 + NB + tid] : 0.0;
+  }
+  __syncthreads();
+  double dq = 0.0;
+  for (int l = 0; l < t; ++l) dq += q1[l] * q2[l];
+  const double wtv = tau * (w.red[1 + 2 * NB] - 2.0 * dq);
+  const double alpha2 = -0.5 * tau * wtv;
+  // row j of V (panel columns 0..t) and of W (0..t-1, then w_j recomputed here)
+  if (tid <= t && tid < NB) vrow[tid] = w.V[size_t(j) * n + p + tid];
+  if (tid < t) wrow[tid] = w.W[size_t(j) * NB + tid];
+  __syncthreads();
+  if (tid == 0) {
+    double acc = w.y[j];
+    for (int l = 0; l < t; ++l) acc -= vrow[l] * q2[l];
+    for (int l = 0; l < t; ++l) acc -= wrow[l] * q1[l];
+    wrow[t] = tau * acc + alpha2 * vrow[t];
+  }
+  __syncthreads();
+  double s = 0.0;
+  for (int r = j + blockIdx.x * blockDim.x + tid; r < n; r += gridDim.x * blockDim.x) {
+    const double *vr_ = w.V + size_t(r) * n + p;
+    double *wr_ = w.W + size_t(r) * NB;
+    double acc = w.y[r];
+    for (int l = 0; l < t; ++l) acc -= vr_[l] * q2[l];
+    for (int l = 0; l < t; ++l) acc -= wr_[l] * q1[l];
+    const double wr = tau * acc + alpha2 * vr_[t];
+    wr_[t] = wr;
+    if (do_next) {
+      double a = A[size_t(j) * lda + r];
+      for (int l = 0; l <= t; ++l) a -= vr_[l] * wrow[l];
+      for (int l = 0; l < t; ++l) a -= wr_[l] * vrow[l];
+      a -= wr * vrow[t];
+      w.acol[r] = a;
+      if (r == j) w.d[j] = a;
+      if (r >= j + 2) s += a * a;
+    }
+  }
+  if (!do_next) return;
+  s = tg::block_sum(s, scratch);
+  if (tid == 0) vals[0] = s;
+  __syncthreads();
+  if (tg::publish_partials(vals, 1, w.part, PST, w.cnt)) tg::sum_partials(w.part, PST, 1, w.red, w.cnt);
+}
+
+// ---------------------------------------------------------------------------
+// 2. eigenvalues of T: Sturm-count multisection
+// ---------------------------------------------------------------------------
+__device__ inline int sturm_count(const double *__restrict__ d, const double *__restrict__ e2, int n,
+                                  double x, double pivmin) {
+  double q = d[0] - x;
+  if (fabs(q) <= pivmin) q = -pivmin;
+  int c = q < 0.0;
+  for (int k = 1; k < n; ++k) {
+    q = (d[k] - x) - e2[k - 1] / q;
+    if (fabs(q) <= pivmin) q = -pivmin;
+    c += q < 0.0;
+  }
+  return c;
+}
+
+// Gershgorin bounds, ||T||_1 and pivmin: one workgroup.
+__global__ void tri_bounds_kernel(const double *__restrict__ d, const double *__restrict__ e, int n,
+                                  double *__restrict__ out /* gl gu tnorm pivmin */) {
+  __shared__ double s_lo[256], s_hi[256], s_e2[256];
+  double lo = INFINITY, hi = -INFINITY, me2 = 0.0;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const double el = k > 0 ? fabs(e[k - 1]) : 0.0;
+    const double er = k < n - 1 ? fabs(e[k]) : 0.0;
+    lo = fmin(lo, d[k] - el - er);
+    hi = fmax(hi, d[k] + el + er);
+    if (k < n - 1) me2 = fmax(me2, e[k] * e[k]);
+  }
+  s_lo[threadIdx.x] = lo;
+  s_hi[threadIdx.x] = hi;
+  s_e2[threadIdx.x] = me2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (int(threadIdx.x) < off) {
+      s_lo[threadIdx.x] = fmin(s_lo[threadIdx.x], s_lo[threadIdx.x + off]);
+      s_hi[threadIdx.x] = fmax(s_hi[threadIdx.x], s_hi[threadIdx.x + off]);
+      s_e2[threadIdx.x] = fmax(s_e2[threadIdx.x], s_e2[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double tnorm = fmax(fabs(s_lo[0]), fabs(s_hi[0]));
+    const double pad = 2.0 * DBL_EPSILON * tnorm * n + 1e-300;
+    out[0] = s_lo[0] - pad;
+    out[1] = s_hi[0] + pad;
+    out[2] = tnorm;
+    out[3] = DBL_MIN * fmax(1.0, s_e2[0]);
+  }
+}
+
+// LDS: d and e^2 staged in LDS (n <= 10240); otherwise e2 holds e^2 in global memory.
+template <bool LDS>
+__global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ d,
+                                                     const double *__restrict__ e2g, int n,
+                                                     const double *__restrict__ bnd,
+                                                     double *__restrict__ w_asc) {
+  extern __shared__ double sh[];
+  const double *dd = d, *ee2 = e2g;
+  if (LDS) {
+    double *sd = sh, *se2 = sh + n;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      sd[k] = d[k];
+      se2[k] = e2g[k];
+    }
+    __syncthreads();
+    dd = sd;
+    ee2 = se2;
+  }
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (ML - 1);
+  const int grp_base = lane & ~(ML - 1);
+  const int j = (blockIdx.x * blockDim.x + threadIdx.x) / ML;  // eigenvalue index (ascending)
+  const double pivmin = bnd[3];
+  double lo = bnd[0], hi = bnd[1];
+  for (int round = 0; round < ROUNDS; ++round) {
+    const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
+    int c = 0;
+    if (j < n) c = sturm_count(dd, ee2, n, x, pivmin);
+    // lanes with count(x) <= j have x <= lambda_j
+    const unsigned long long m = __ballot(j < n && c <= j);
+    const int a = __popcll((m >> grp_base) & ((1ull << ML) - 1));
+    const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
+    const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
+    const double nlo = a > 0 ? xa1 : lo;
+    const double nhi = a < ML ? xa : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (j < n && sub == 0) w_asc[j] = 0.5 * (lo + hi);
+}
+
+// e^2 (e[n-1] = 0 padding)
+__global__ void square_kernel(const double *__restrict__ e, int n, double *__restrict__ e2) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) e2[k] = k < n - 1 ? e[k] * e[k] : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// A3: truncation rank (gptq_utils.py:94, 97-108), one thread (sequential sums,
+// deterministic).
+// ---------------------------------------------------------------------------
+__global__ void rank_kernel(const double *__restrict__ w_asc, int n, double thr, int rule,
+                            double *__restrict__ S, int32_t *__restrict__ kout) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) S[i] = sqrt(fmax(w_asc[n - 1 - i], 1e-12));
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int k = n;
+  if (rule == TG_RULE_ENERGY) {
+    double total = 0.0;
+    for (int i = 0; i < n; ++i) total += S[i] * S[i];
+    const double target = (1.0 - thr) * total;
+    double cs = 0.0;
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+      cs += S[i] * S[i];
+      cnt += cs <= target;
+    }
+    k = cnt < n ? cnt + 1 : cnt;
+  } else if (rule == TG_RULE_MEAN_TRIMMED) {
+    const int ref_k = n < 33 ? n : 33;
+    double ref = S[0];
+    if (n > 1) {
+      double s = 0.0;
+      for (int i = 1; i < ref_k; ++i) s += S[i];
+      ref = s / double(ref_k - 1);
+    }
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) cnt += S[i] > thr * ref;
+    k = cnt;
+  }
+  *kout = k;
+}
+
+// ---------------------------------------------------------------------------
+// 3. inverse iteration: one thread per wanted eigenvector (column jj of Z,
+// eigenvalue w_asc[n-1-jj]).  LU with partial pivoting of T - lambda I
+// (dgttrf pattern), tiny pivots replaced by +-eps*||T|| (dlagts).
+// ---------------------------------------------------------------------------
+__device__ inline double hash_unit(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return (double(h) + 0.5) / 4294967296.0 - 0.5;
+}
+
+__global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
+                                                   const double *__restrict__ e, int n, int k,
+                                                   const double *__restrict__ w_asc,
+                                                   const double *__restrict__ bnd, Tri w) {
+  const int jj = blockIdx.x * blockDim.x + threadIdx.x;
+  if (jj >= k) return;
+  const double lam = w_asc[n - 1 - jj];
+  const double tol = fmax(DBL_EPSILON * bnd[2], 1e-300);
+  const size_t K = size_t(k);
+  double *dl = w.lu, *dd = w.lu + size_t(n) * n, *du = w.lu + 2 * size_t(n) * n,
+         *du2 = w.lu + 3 * size_t(n) * n;
+  int8_t *pv = w.piv;
+  double *x = w.Z;
+  auto at = [&](int i) { return size_t(i) * K + jj; };
+  // factor
+  double cur_d = d[0] - lam;
+  double cur_u = n > 1 ? e[0] : 0.0;
+  for (int i = 0; i < n - 1; ++i) {
+    const double sub = e[i];
+    const double nd = d[i + 1] - lam;
+    const double nu = i + 1 < n - 1 ? e[i + 1] : 0.0;
+    if (fabs(cur_d) >= fabs(sub)) {
+      double piv = cur_d;
+      if (fabs(piv) < tol) piv = piv < 0.0 ? -tol : tol;
+      const double f = sub / piv;
+      dd[at(i)] = piv;
+      du[at(i)] = cur_u;
+      du2[at(i)] = 0.0;
+      dl[at(i)] = f;
+      pv[at(i)] = 0;
+      cur_d = nd - f * cur_u;
+      cur_u = nu;
+    } else {
+      const double f = cur_d / sub;
+      dd[at(i)] = sub;
+      du[at(i)] = nd;
+      du2[at(i)] = nu;
+      dl[at(i)] = f;
+      pv[at(i)] = 1;
+      cur_d = cur_u - f * nd;
+      cur_u = -f * nu;
+    }
+  }
+  {
+    double piv = cur_d;
+    if (fabs(piv) < tol) piv = piv < 0.0 ? -tol : tol;
+    dd[at(n - 1)] = piv;
+  }
+  // start vector
+  for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(i), uint32_t(jj)) + 0.25;
+  for (int it = 0; it < 3; ++it) {
+    // forward: apply L^-1 with interchanges
+    for (int i = 0; i < n - 1; ++i) {
+      const double f = dl[at(i)];
+      if (pv[at(i)] == 0) {
+        x[at(i + 1)] -= f * x[at(i)];
+      } else {
+        const double tmp = x[at(i)];
+        x[at(i)] = x[at(i + 1)];
+        x[at(i + 1)] = tmp - f * x[at(i)];
+      }
+    }
+    // backward: U^-1
+    double xn1 = 0.0, xn2 = 0.0, amax = 0.0;
+    for (int i = n - 1; i >= 0; --i) {
+      double v = x[at(i)];
+      if (i < n - 1) v -= du[at(i)] * xn1;
+      if (i < n - 2) v -= du2[at(i)] * xn2;
+      v /= dd[at(i)];
+      x[at(i)] = v;
+      xn2 = xn1;
+      xn1 = v;
+      amax = fmax(amax, fabs(v));
+    }
+    // rescale to avoid overflow on the next solve
+    const double s = amax > 0.0 ? 1.0 / amax : 1.0;
+    double nrm = 0.0;
+    for (int i = 0; i < n; ++i) {
+      const double v = x[at(i)] * s;
+      x[at(i)] = v;
+      nrm += v * v;
+    }
+    if (it == 2) {
+      const double inv = 1.0 / sqrt(nrm);
+      for (int i = 0; i < n; ++i) x[at(i)] *= inv;
+    }
+  }
+}
+
+// Re-orthogonalise clusters of (near-)equal eigenvalues (gap <= reltol*||T||)
+// by modified Gram-Schmidt, one workgroup walking the k columns.
+__global__ __launch_bounds__(256) void cluster_mgs_kernel(const double *__restrict__ w_asc, int n,
+                                                          int k, const double *__restrict__ bnd,
+                                                          double reltol, double *__restrict__ Z) {
+  __shared__ double scratch[8];
+  const double gap = reltol * bnd[2];
+  int start = 0;
+  while (start < k) {
+    int end = start + 1;
+    while (end < k && fabs(w_asc[n - 1 - (end - 1)] - w_asc[n - 1 - end]) <= gap) ++end;
+    for (int c = start + 1; c < end; ++c) {
+      for (int b = start; b < c; ++b) {
+        double dot = 0.0;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) dot += Z[size_t(i) * k + b] * Z[size_t(i) * k + c];
+        dot = tg::block_sum(dot, scratch);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] -= dot * Z[size_t(i) * k + b];
+        __syncthreads();
+      }
+      double nrm = 0.0;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) nrm += Z[size_t(i) * k + c] * Z[size_t(i) * k + c];
+      nrm = tg::block_sum(nrm, scratch);
+      const double inv = 1.0 / sqrt(nrm);
+      for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] *= inv;
+      __syncthreads();
+    }
+    start = end;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 4. back-transformation helpers
+// ---------------------------------------------------------------------------
+// T factor of block b (dlarft forward/columnwise): reflectors p..p+bw-1.
+__global__ __launch_bounds__(256) void tfactor_kernel(const double *__restrict__ V, int n, int nref,
+                                                      const double *__restrict__ tau,
+                                                      double *__restrict__ Tf) {
+  __shared__ double G[BT][BT + 1];
+  __shared__ double rows[16][BT];
+  __shared__ double Ts[BT][BT + 1];
+  const int b = blockIdx.x;
+  const int p = b * BT;
+  const int bw = min(BT, nref - p);
+  const int tid = threadIdx.x;
+  double acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+  // entries (a, c) for idx = tid + 256*q, a = idx / BT, c = idx % BT
+  for (int r0 = p + 1; r0 < n; r0 += 16) {
+    for (int idx = tid; idx < 16 * BT; idx += blockDim.x) {
+      const int rr = idx / BT, c = idx % BT;
+      const int r = r0 + rr;
+      rows[rr][c] = (r < n && c < bw) ? V[size_t(r) * n + p + c] : 0.0;
+    }
+    __syncthreads();
+    for (int rr = 0; rr < 16; ++rr) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int idx = tid + 256 * q;
+        acc[q] += rows[rr][idx / BT] * rows[rr][idx % BT];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = tid + 256 * q;
+    G[idx / BT][idx % BT] = acc[q];
+  }
+  for (int idx = tid; idx < BT * BT; idx += blockDim.x) Ts[idx / BT][idx % BT] = 0.0;
+  __syncthreads();
+  for (int a = 0; a < bw; ++a) {
+    const double ta = tau[p + a];
+    // z[r] = -tau_a G[r][a], r < a ; T[r][a] = sum_{c=r}^{a-1} T[r][c] z[c]
+    if (tid < a) {
+      double s = 0.0;
+      for (int c = tid; c < a; ++c) s += Ts[tid][c] * (-ta * G[c][a]);
+      Ts[tid][a] = s;
+    }
+    if (tid == 0) Ts[a][a] = ta;
+    __syncthreads();
+  }
+  for (int idx = tid; idx < BT * BT; idx += blockDim.x)
+    Tf[size_t(b) * BT * BT + idx] = Ts[idx / BT][idx % BT];
+}
+
+// Vh[jj][c] = Z[c][jj]  (n x k -> k x n)
+__global__ void transpose_kernel(const double *__restrict__ Z, int n, int k, double *__restrict__ Vh,
+                                 int ldv) {
+  __shared__ double tile[32][33];
+  const int c0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  for (int r = threadIdx.y; r < 32; r += blockDim.y) {
+    const int c = c0 + r, jj = j0 + threadIdx.x;
+    tile[r][threadIdx.x] = (c < n && jj < k) ? Z[size_t(c) * k + jj] : 0.0;
+  }
+  __syncthreads();
+  for (int r = threadIdx.y; r < 32; r += blockDim.y) {
+    const int jj = j0 + r, c = c0 + threadIdx.x;
+    if (jj < k && c < n) Vh[size_t(jj) * ldv + c] = tile[threadIdx.x][r];
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" size_t tg_eigh_workspace_size(int n) {
+  tg::Sizer s;
+  tri_layout(s, n, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w_asc, void *ws,
+                              size_t ws_bytes) {
+  TG_ARG(A, 2, "null A");
+  TG_ARG(n >= 1, 3, "n < 1");
+  TG_ARG(lda >= n, 4, "lda < n");
+  TG_ARG(w_asc, 5, "null w");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  Tri w{};
+  tri_layout(ar, n, &w);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(w.V, 0, sizeof(double) * size_t(n) * n, st));
+  TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
+  TG_HIP(hipMemsetAsync(w.e, 0, sizeof(double) * n, st));
+  TG_HIP(hipMemsetAsync(w.tau, 0, sizeof(double) * n, st));
+  const bool vlds = n <= 16384;
+  const size_t vsh_bytes = vlds ? sizeof(double) * size_t(n) : 0;
+  if (vsh_bytes > 64 * 1024)
+    TG_HIP(hipFuncSetAttribute((const void *)tri_symv_kernel<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(vsh_bytes)));
+  for (int p = 0; p < n; p += NB) {
+    hipLaunchKernelGGL(tri_start_kernel, dim3(NG), dim3(256), 0, st, A, lda, n, p, w);
+    TG_LAUNCHED();
+    if (p >= n - 1) break;  // last column: only d[n-1]
+    const int pe = min(p + NB, n - 1);
+    for (int i = p; i < pe; ++i) {
+      if (vlds)
+        hipLaunchKernelGGL(tri_symv_kernel<true>, dim3(NG), dim3(256), vsh_bytes, st, A, lda, n,
+                           i, p, w);
+      else
+        hipLaunchKernelGGL(tri_symv_kernel<false>, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, w);
+      TG_LAUNCHED();
+      const int do_next = (i + 1 < p + NB) ? 1 : 0;
+      hipLaunchKernelGGL(tri_fin_kernel, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, do_next, w);
+      TG_LAUNCHED();
+    }
+    const int q = p + NB;
+    if (q <= n - 1) {  // trailing rank-2NB update of A[q:, q:]
+      const int mt = n - q;
+      double *C = A + size_t(q) * lda + q;
+      const double *Vb = w.V + size_t(q) * n + p;
+      const double *Wb = w.W + size_t(q) * NB;
+      TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Vb, n, Wb, NB, 1.0, C, lda));
+      TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Wb, NB, Vb, n, 1.0, C, lda));
+    }
+  }
+  // eigenvalues of T
+  double *bnd = w.scal;
+  hipLaunchKernelGGL(tri_bounds_kernel, dim3(1), dim3(256), 0, st, w.d, w.e, n, bnd);
+  TG_LAUNCHED();
+  const int blocks = tg::cdiv(int64_t(n) * ML, 256);
+  const size_t lds = 2 * sizeof(double) * size_t(n);
+  hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.e, n, w.acol);
+  TG_LAUNCHED();
+  if (lds <= 160 * 1024) {
+    if (lds > 64 * 1024)
+      TG_HIP(hipFuncSetAttribute((const void *)bisect_kernel<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    hipLaunchKernelGGL(bisect_kernel<true>, dim3(blocks), dim3(256), lds, st, w.d, w.acol, n, bnd,
+                       w_asc);
+  } else {
+    hipLaunchKernelGGL(bisect_kernel<false>, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
+                       w_asc);
+  }
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" int tg_truncation_rank(void *stream, const double *w_asc, int n, double threshold,
+                                  int rule, double *S_desc, int32_t *k_dev) {
+  TG_ARG(w_asc, 2, "null w");
+  TG_ARG(n >= 1, 3, "n < 1");
+  TG_ARG(S_desc && k_dev, 6, "null output");
+  hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, w_asc, n, threshold,
+                     rule, S_desc, k_dev);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, double *Vh, int ldv,
+                               void *ws, size_t ws_bytes) {
+  TG_ARG(n >= 1, 2, "n < 1");
+  TG_ARG(w_asc, 3, "null w");
+  TG_ARG(k >= 1 && k <= n, 4, "k must be in [1, n]");
+  TG_ARG(Vh, 5, "null Vh");
+  TG_ARG(ldv >= n, 6, "ldv < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  Tri w{};
+  tri_layout(ar, n, &w);
+  TG_WS(ar);
+  const double *bnd = w.scal;
+  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.e, n, k, w_asc,
+                     bnd, w);
+  TG_LAUNCHED();
+  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-10, w.Z);
+  TG_LAUNCHED();
+  // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
+  const int nref = n - 1;
+  if (nref > 0) {
+    const int nblk = tg::cdiv(nref, BT);
+    hipLaunchKernelGGL(tfactor_kernel, dim3(nblk), dim3(256), 0, st, w.V, n, nref, w.tau, w.Tf);
+    TG_LAUNCHED();
+    for (int b = nblk - 1; b >= 0; --b) {
+      const int p = b * BT, bw = min(BT, nref - p), r0 = p + 1;
+      const double *Vb = w.V + size_t(r0) * n + p;
+      // X1 = Vb^T Z[r0:, :]   (bw x k)
+      TG_HIP(tg::dgemm_splitk(st, true, false, bw, k, n - r0, 1.0, Vb, n, w.Z + size_t(r0) * k, k,
+                              0.0, w.X1, k, SPLITK, w.skp));
+      // X2 = T_b X1
+      TG_HIP(tg::dgemm(st, false, false, bw, k, bw, 1.0, w.Tf + size_t(b) * BT * BT, BT, w.X1, k,
+                       0.0, w.X2, k));
+      // Z[r0:, :] -= Vb X2
+      TG_HIP(tg::dgemm(st, false, false, n - r0, k, bw, -1.0, Vb, n, w.X2, k, 1.0,
+                       w.Z + size_t(r0) * k, k));
+    }
+  }
+  hipLaunchKernelGGL(transpose_kernel, dim3(tg::cdiv(k, 32), tg::cdiv(n, 32)), dim3(32, 8), 0, st,
+                     w.Z, n, k, Vh, ldv);
+  TG_LAUNCHED();
+  return 0;
+}

@@ -1,0 +1,351 @@
+// Pivot order, R_x and U of the truncated spectral factorisation (A4, A5).
+//
+// Replaces, in /root/reference/src/TruncGPTQ/gptq_utils.py:
+//   H_sqrt = S[:, None] * Vh; jax.scipy.linalg.qr(H_sqrt, pivoting=True)  :112-117
+//       (XLA -> MAGMA dgeqp3)                      -> tg_pivoted_factor
+//   torch.linalg.qr(H_inv_partial[:, perm]) + sign normalisation        :118-124
+//       (cuSOLVER geqrf)                           -> tg_u_factor
+//
+// Pivot order.  dgeqp3 picks, at step i, the remaining column of largest
+// residual norm (first index on ties) and swaps it into position i.  The
+// residual column norms of S_k after i Householder steps equal the diagonal
+// of the Schur complement of H_k = S_k^T S_k after i pivoted Cholesky steps,
+// and the R factor equals the pivoted Cholesky factor (both with positive
+// diagonal).  So the pivot sequence (identical swap bookkeeping) and R_x come
+// from a greedy diagonal-pivoted Cholesky of H_k (SYRK on FP64 MFMA), one
+// launch per pivot; the panel's rank-32 Schur update runs on FP64 MFMA.
+//
+// U.  U (k x n, upper trapezoidal, positive diagonal) is the R factor of
+// A = diag(1/S_k) Vh_k[:, perm].  U^T U = A^T A, so U is the first k rows of
+// the upper Cholesky factor of G = A^T A: form G[:k, :] = A[:, :k]^T A on
+// FP64 MFMA, then a right-looking blocked Cholesky over those k rows (panel
+// factor in LDS, triangular solve across all n columns, MFMA trailing update).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <type_traits>
+
+#include "../../include/truncgptq.h"
+#include "common.h"
+#include "gemm64.h"
+#include "reduce.h"
+
+namespace {
+
+constexpr int PB = 32;    // pivoted-Cholesky panel (steps between Schur updates)
+constexpr int CB = 32;    // Cholesky row panel for U
+constexpr int PGMAX = 64; // max workgroups of the per-pivot kernel
+
+struct PivWs {
+  double *B;     // k x n  S_k-scaled eigenvectors (H_sqrt)
+  double *Hk;    // n x n  H_k, then its Schur complements
+  double *dsc;   // n      Schur diagonal (by original index)
+  double *L;     // n x k  L[r][i] (original row index r, pivot step i)
+  double *part;  // PGMAX x 2
+  int32_t *perm; // n      position -> original index
+  unsigned *cnt;
+};
+
+template <class A>
+void piv_layout(A &ar, int n, int k, PivWs *p) {
+  PivWs d{};
+  PivWs &q = p ? *p : d;
+  auto take = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  take(q.B, size_t(k) * n);
+  take(q.Hk, size_t(n) * n);
+  take(q.dsc, n);
+  take(q.L, size_t(n) * k);
+  take(q.part, PGMAX * 2);
+  take(q.perm, n);
+  take(q.cnt, 16);
+}
+
+// B[t][c] = S[t] * Vh[t][c]    (gptq_utils.py:112)
+__global__ void scale_rows_kernel(const double *__restrict__ Vh, int ldv, const double *__restrict__ S,
+                                  int n, int k, double *__restrict__ B) {
+  const int t = blockIdx.y;
+  const double s = S[t];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+    B[size_t(t) * n + c] = s * Vh[size_t(t) * ldv + c];
+}
+
+// (value, position) argmax with first-position tie break, published for the
+// last workgroup, which then swaps perm[i] <-> perm[q].
+__device__ inline void argmax_publish(double bv, int bp, int i, int n, PivWs w) {
+  __shared__ double sv[256];
+  __shared__ int sp[256];
+  __shared__ double vals[2];
+  const int tid = threadIdx.x;
+  sv[tid] = bv;
+  sp[tid] = bp;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      const double ov = sv[tid + off];
+      const int op = sp[tid + off];
+      if (ov > sv[tid] || (ov == sv[tid] && op < sp[tid])) {
+        sv[tid] = ov;
+        sp[tid] = op;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    vals[0] = sv[0];
+    vals[1] = double(sp[0]);
+  }
+  __syncthreads();
+  if (tg::publish_partials(vals, 2, w.part, 2, w.cnt)) {
+    if (tid == 0) {
+      double best = -INFINITY;
+      int q = n;
+      for (int g = 0; g < int(gridDim.x); ++g) {
+        const double v = w.part[2 * g];
+        const int p = int(w.part[2 * g + 1]);
+        if (v > best || (v == best && p < q)) {
+          best = v;
+          q = p;
+        }
+      }
+      if (q < n && q != i) {
+        const int a = w.perm[i];
+        w.perm[i] = w.perm[q];
+        w.perm[q] = a;
+      }
+      *w.cnt = 0u;
+    }
+  }
+}
+
+// dsc = diag(Hk), perm = identity, first pivot swapped into position 0.
+__global__ __launch_bounds__(256) void piv_init_kernel(int n, PivWs w) {
+  double bv = -INFINITY;
+  int bp = n;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const double v = w.Hk[size_t(j) * n + j];
+    w.dsc[j] = v;
+    w.perm[j] = j;
+    if (v > bv || (v == bv && j < bp)) {
+      bv = v;
+      bp = j;
+    }
+  }
+  argmax_publish(bv, bp, 0, n, w);
+}
+
+// One pivot step i (pivot already swapped into position i).
+__global__ __launch_bounds__(256) void piv_step_kernel(int n, int k, int i, int ps, PivWs w) {
+  __shared__ double lp[PB];
+  const int t = i - ps;
+  const int piv = w.perm[i];
+  const double dpiv = w.dsc[piv];
+  const double ljj = sqrt(fmax(dpiv, 0.0));
+  if (threadIdx.x < t) lp[threadIdx.x] = w.L[size_t(piv) * k + ps + threadIdx.x];
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.L[size_t(piv) * k + i] = ljj;
+  const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
+  double bv = -INFINITY;
+  int bp = n;
+  for (int j = i + 1 + blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int r = w.perm[j];
+    double v = w.Hk[size_t(piv) * n + r];
+    const double *lr = w.L + size_t(r) * k + ps;
+    for (int l = 0; l < t; ++l) v -= lr[l] * lp[l];
+    const double lv = v * inv;
+    w.L[size_t(r) * k + i] = lv;
+    const double dn = w.dsc[r] - lv * lv;
+    w.dsc[r] = dn;
+    if (dn > bv || (dn == bv && j < bp)) {
+      bv = dn;
+      bp = j;
+    }
+  }
+  if (i + 1 < n) argmax_publish(bv, bp, i + 1, n, w);
+}
+
+// Rx[t][j] = L[perm[j]][t] for j >= t (upper trapezoidal), perm64 = perm.
+__global__ void rx_gather_kernel(int n, int k, PivWs w, double *__restrict__ Rx, int ldr,
+                                 int64_t *__restrict__ perm64) {
+  const int t = blockIdx.y;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int r = w.perm[j];
+    if (t == 0) perm64[j] = r;
+    if (Rx) Rx[size_t(t) * ldr + j] = j >= t ? w.L[size_t(r) * k + t] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// U
+// ---------------------------------------------------------------------------
+// A[t][j] = (1/S[t]) * Vh[t][perm[j]]     (gptq_utils.py:111, 118-119)
+__global__ void gather_scale_kernel(const double *__restrict__ Vh, int ldv, const double *__restrict__ S,
+                                    const int64_t *__restrict__ perm, int n, double *__restrict__ A) {
+  const int t = blockIdx.y;
+  const double sinv = 1.0 / S[t];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    A[size_t(t) * n + j] = sinv * Vh[size_t(t) * ldv + perm[j]];
+}
+
+// Upper Cholesky of the pb x pb diagonal block at U[p][p] (in place), LDS.
+__global__ __launch_bounds__(256) void potf2_kernel(double *__restrict__ U, int ldu, int p, int pb,
+                                                    int *__restrict__ info) {
+  __shared__ double a[CB][CB + 1];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < CB * CB; idx += blockDim.x) {
+    const int r = idx / CB, c = idx % CB;
+    a[r][c] = (r < pb && c < pb) ? U[size_t(p + r) * ldu + p + c] : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  for (int j = 0; j < CB; ++j) {
+    const double djj = a[j][j];
+    const double piv = sqrt(djj);
+    if (tid == 0 && !(djj > 0.0) && j < pb) atomicAdd(info, 1);
+    __syncthreads();
+    for (int c = j + 1 + tid; c < CB; c += blockDim.x) a[j][c] /= piv;
+    __syncthreads();
+    if (tid == 0) a[j][j] = piv;
+    // trailing: a[r][c] -= a[j][r] * a[j][c], j < r <= c
+    const int m = CB - j - 1;
+    for (int idx = tid; idx < m * m; idx += blockDim.x) {
+      const int r = j + 1 + idx / m, c = j + 1 + idx % m;
+      if (c >= r) a[r][c] -= a[j][r] * a[j][c];
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < pb * pb; idx += blockDim.x) {
+    const int r = idx / pb, c = idx % pb;
+    U[size_t(p + r) * ldu + p + c] = c >= r ? a[r][c] : 0.0;
+  }
+}
+
+// Row-panel triangular solve: X = Ubb^{-T} G[p:p+pb, c] for c in [c0, n).
+// One thread per column; the column's pb unknowns live in LDS (xs[j][tid]).
+__global__ __launch_bounds__(256) void trsm_rows_kernel(double *__restrict__ U, int ldu, int p, int pb,
+                                                        int c0, int n) {
+  __shared__ double ub[CB][CB + 1];
+  __shared__ double xs[CB][256];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < CB * CB; idx += blockDim.x) {
+    const int r = idx / CB, c = idx % CB;
+    ub[r][c] = (r < pb && c < pb) ? U[size_t(p + r) * ldu + p + c] : (r == c ? 1.0 : 0.0);
+  }
+  const int c = c0 + blockIdx.x * blockDim.x + tid;
+  const bool act = c < n;
+  for (int j = 0; j < pb; ++j) xs[j][tid] = act ? U[size_t(p + j) * ldu + c] : 0.0;
+  __syncthreads();
+  for (int j = 0; j < pb; ++j) {
+    double v = xs[j][tid];
+    for (int l = 0; l < j; ++l) v -= ub[l][j] * xs[l][tid];
+    xs[j][tid] = v / ub[j][j];
+  }
+  if (act)
+    for (int j = 0; j < pb; ++j) U[size_t(p + j) * ldu + c] = xs[j][tid];
+}
+
+__global__ void zero_lower_kernel(double *__restrict__ U, int ldu, int k) {
+  const int r = blockIdx.y;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < r && c < k; c += gridDim.x * blockDim.x)
+    U[size_t(r) * ldu + c] = 0.0;
+}
+
+}  // namespace
+
+extern "C" size_t tg_pivot_workspace_size(int n, int k) {
+  tg::Sizer s;
+  piv_layout(s, n, k, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const double *S, int n,
+                                 int k, int64_t *perm, double *Rx, int ldr, void *ws,
+                                 size_t ws_bytes) {
+  TG_ARG(Vh, 2, "null Vh");
+  TG_ARG(ldv >= n, 3, "ldv < n");
+  TG_ARG(S, 4, "null S");
+  TG_ARG(n >= 1, 5, "n < 1");
+  TG_ARG(k >= 1 && k <= n, 6, "k must be in [1, n]");
+  TG_ARG(perm, 7, "null perm");
+  TG_ARG(!Rx || ldr >= n, 9, "ldr < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  PivWs w{};
+  piv_layout(ar, n, k, &w);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
+                     dim3(256), 0, st, Vh, ldv, S, n, k, w.B);
+  TG_LAUNCHED();
+  TG_HIP(tg::dsyrk_tn(st, n, k, 1.0, w.B, n, 0.0, w.Hk, n));  // H_k = H_sqrt^T H_sqrt
+  const int g0 = std::min(PGMAX, tg::cdiv(n, 256));
+  hipLaunchKernelGGL(piv_init_kernel, dim3(g0), dim3(256), 0, st, n, w);
+  TG_LAUNCHED();
+  for (int ps = 0; ps < k; ps += PB) {
+    const int pe = std::min(ps + PB, k);
+    for (int i = ps; i < pe; ++i) {
+      const int g = std::max(1, std::min(PGMAX, tg::cdiv(n - i - 1, 256)));
+      hipLaunchKernelGGL(piv_step_kernel, dim3(g), dim3(256), 0, st, n, k, i, ps, w);
+      TG_LAUNCHED();
+    }
+    if (pe < k)  // Schur update with this panel's columns (all rows, original order)
+      TG_HIP(tg::dsyrk_nt(st, n, pe - ps, -1.0, w.L + ps, k, 1.0, w.Hk, n));
+  }
+  hipLaunchKernelGGL(rx_gather_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
+                     dim3(256), 0, st, n, k, w, Rx, ldr, perm);
+  TG_LAUNCHED();
+  return 0;
+}
+
+extern "C" size_t tg_ufactor_workspace_size(int n, int k) {
+  tg::Sizer s;
+  s.take<double>(size_t(k) * n);
+  s.take<int>(16);
+  return s.off + 256;
+}
+
+extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double *S,
+                           const int64_t *perm, int n, int k, double *U, int ldu, void *ws,
+                           size_t ws_bytes) {
+  TG_ARG(Vh, 2, "null Vh");
+  TG_ARG(ldv >= n, 3, "ldv < n");
+  TG_ARG(S, 4, "null S");
+  TG_ARG(perm, 5, "null perm");
+  TG_ARG(n >= 1, 6, "n < 1");
+  TG_ARG(k >= 1 && k <= n, 7, "k must be in [1, n]");
+  TG_ARG(U, 8, "null U");
+  TG_ARG(ldu >= n, 9, "ldu < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  double *A = ar.take<double>(size_t(k) * n);
+  int *info = ar.take<int>(16);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  hipLaunchKernelGGL(gather_scale_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
+                     dim3(256), 0, st, Vh, ldv, S, perm, n, A);
+  TG_LAUNCHED();
+  // G[:k, :] = A[:, :k]^T A   (k x n) into U
+  TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));
+  for (int p = 0; p < k; p += CB) {
+    const int pb = std::min(CB, k - p);
+    hipLaunchKernelGGL(potf2_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, info);
+    TG_LAUNCHED();
+    const int c0 = p + pb;
+    if (c0 < n) {
+      hipLaunchKernelGGL(trsm_rows_kernel, dim3(tg::cdiv(n - c0, 256)), dim3(256), 0, st, U, ldu,
+                         p, pb, c0, n);
+      TG_LAUNCHED();
+    }
+    if (c0 < k) {
+      const double *P = U + size_t(p) * ldu + c0;
+      TG_HIP(tg::dgemm(st, true, false, k - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
+                       U + size_t(c0) * ldu + c0, ldu));
+    }
+  }
+  hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
+                     dim3(256), 0, st, U, ldu, k);
+  TG_LAUNCHED();
+  return 0;
+}

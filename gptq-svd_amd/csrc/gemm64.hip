@@ -1,0 +1,281 @@
+// FP64 MFMA GEMM for gfx950 (v_mfma_f64_16x16x4_f64) and the Hessian SYRK.
+//
+//   C = alpha * op(A) * op(B) + beta * C     (row-major everything)
+//
+// Used by: Hessian accumulation (A1, gptq_utils.py:222 `H.addmm_(x.T, x)`,
+// SYRK mode: lower tiles only, mirrored), the tridiagonalisation's trailing
+// rank-2k updates, the eigenvector back-transformation and the factor stages.
+//
+// Tile BM x BN per 256-thread workgroup, 4 waves as 2x2, each wave a
+// (BM/2) x (BN/2) grid of 16x16 MFMA tiles; K staged through LDS in chunks of
+// 16 (k-major images so fragment reads are 16 consecutive doubles).
+// f64 MFMA C/D layout (differs from f32!): col = lane & 15,
+// row = (lane >> 4) + 4 * reg  (MI355X guide §3).
+#include <algorithm>
+
+#include "../../include/truncgptq.h"
+#include "common.h"
+#include "gemm64.h"
+
+namespace {
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+template <class T>
+__device__ inline double to_f64(T v) { return double(v); }
+template <>
+__device__ inline double to_f64<__half>(__half v) { return double(__half2float(v)); }
+template <>
+__device__ inline double to_f64<__hip_bfloat16>(__hip_bfloat16 v) { return double(__bfloat162float(v)); }
+
+constexpr int KC = 16;
+constexpr int PAD = 4;
+
+// Stage op(X) tile into a k-major LDS image S[KC][W + PAD] covering
+// rows r0..r0+W of op(X) (op(X) is R x K) and k0..k0+KC.
+//  TRANS == false: X stored R x K (ld), element (r, k) at X[r*ld + k]
+//  TRANS == true : X stored K x R (ld), element (r, k) at X[k*ld + r]
+template <class T, int W, bool TRANS>
+__device__ inline void stage(const T *__restrict__ X, int64_t ld, int R, int K, int r0, int k0,
+                             double (*S)[W + PAD]) {
+  const int tid = threadIdx.x;
+  constexpr int PER = W * KC / 256;  // elements per thread
+  if (!TRANS) {
+    // each thread: one row, PER consecutive k
+    constexpr int TPR = KC / PER;  // threads per row
+    const int r = tid / TPR, kb = (tid % TPR) * PER;
+    const int gr = r0 + r;
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int gk = k0 + kb + t;
+      S[kb + t][r] = (gr < R && gk < K) ? to_f64(X[int64_t(gr) * ld + gk]) : 0.0;
+    }
+  } else {
+    // each thread: one k, PER consecutive rows
+    constexpr int TPK = W / PER;
+    const int k = tid / TPK, rb = (tid % TPK) * PER;
+    const int gk = k0 + k;
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int gr = r0 + rb + t;
+      S[k][rb + t] = (gr < R && gk < K) ? to_f64(X[int64_t(gk) * ld + gr]) : 0.0;
+    }
+  }
+}
+
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK>
+__global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha,
+                                                    const TA_ *__restrict__ A, int64_t lda,
+                                                    const TB_ *__restrict__ B, int64_t ldb,
+                                                    double beta, double *__restrict__ C,
+                                                    int64_t ldc, int kchunk, int64_t zstride) {
+  __shared__ double As[KC][BM + PAD];
+  __shared__ double Bs[KC][BN + PAD];
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int tm, tn;
+  if (SYRK) {  // blockIdx.x enumerates lower-triangle tiles (I >= J)
+    const int b = blockIdx.x;
+    int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= b) ++I;
+    while (I * (I + 1) / 2 > b) --I;
+    const int J = b - I * (I + 1) / 2;
+    tm = I * BM;
+    tn = J * BN;
+  } else {
+    tm = blockIdx.y * BM;
+    tn = blockIdx.x * BN;
+  }
+  doublex4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+
+  // split-K: workgroup z covers k in [kb, ke) and writes C + z * zstride
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  C += int64_t(blockIdx.z) * zstride;
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+    stage<TA_, BM, TA>(A, lda, M, ke, tm, k0, As);
+    // op(B) is K x N; stage it as op(B)^T (N x K) with the transposed flag
+    stage<TB_, BN, !TB>(B, ldb, N, ke, tn, k0, Bs);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      double af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
+        const int gj = tn + wn * WN + j * 16 + (lane & 15);
+        if (gi < M && gj < N) {
+          double *p = C + int64_t(gi) * ldc + gj;
+          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *p;
+          *p = v;
+          if (SYRK && tm != tn) C[int64_t(gj) * ldc + gi] = v;
+        }
+      }
+}
+
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>
+hipError_t launch(hipStream_t st, int M, int N, int K, double alpha, const TA_ *A, int64_t lda,
+                  const TB_ *B, int64_t ldb, double beta, double *C, int64_t ldc, int splits,
+                  int64_t zstride) {
+  const int kchunk = splits > 1 ? ((tg::cdiv(K, splits) + KC - 1) / KC) * KC : (K > 0 ? K : 1);
+  const int nz = splits > 1 ? tg::cdiv(K, kchunk) : 1;
+  dim3 grid(tg::cdiv(N, BN), tg::cdiv(M, BM), nz);
+  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, TA, TB, false>), grid, dim3(256), 0, st, M,
+                     N, K, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, zstride);
+  return hipGetLastError();
+}
+
+template <class TA_, class TB_, int BM, int BN>
+hipError_t dispatch_t(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
+                      const TA_ *A, int64_t lda, const TB_ *B, int64_t ldb, double beta,
+                      double *C, int64_t ldc, int splits = 1, int64_t zs = 0) {
+  if (!ta && !tb) return launch<TA_, TB_, BM, BN, false, false>(st, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits, zs);
+  if (!ta && tb) return launch<TA_, TB_, BM, BN, false, true>(st, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits, zs);
+  if (ta && !tb) return launch<TA_, TB_, BM, BN, true, false>(st, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits, zs);
+  return launch<TA_, TB_, BM, BN, true, true>(st, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits, zs);
+}
+
+// C = alpha * sum_z P_z + beta * C
+__global__ void splitk_reduce_kernel(const double *__restrict__ P, int nz, int64_t zstride, int M,
+                                     int N, double alpha, double beta, double *__restrict__ C,
+                                     int64_t ldc) {
+  const int64_t total = int64_t(M) * N;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int r = int(idx / N), c = int(idx % N);
+    double s = 0.0;
+    for (int z = 0; z < nz; ++z) s += P[z * zstride + idx];
+    double *p = C + int64_t(r) * ldc + c;
+    *p = beta == 0.0 ? alpha * s : alpha * s + beta * *p;
+  }
+}
+
+template <class T>
+hipError_t syrk_t(hipStream_t st, const T *X, int64_t rows, int n, int64_t ldx, double *H,
+                  int64_t ldh) {
+  constexpr int BT = 64;
+  const int nt = tg::cdiv(n, BT);
+  const int tiles = nt * (nt + 1) / 2;
+  // H += X^T X : op(A) = X^T (A = X stored rows x n -> TA), op(B) = X (K x N, no trans)
+  hipLaunchKernelGGL((dgemm_kernel<T, T, BT, BT, true, false, true>), dim3(tiles), dim3(256), 0,
+                     st, n, n, int(rows), 1.0, X, ldx, X, ldx, 1.0, H, ldh, int(rows), int64_t(0));
+  return hipGetLastError();
+}
+
+}  // namespace
+
+namespace tg {
+hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
+                 const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                 double *C, int64_t ldc) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0) {
+    // C = beta * C (alpha * 0): run with K = 0 -> the kernel writes beta*C
+  }
+  const int64_t tiles128 = int64_t(cdiv(M, 128)) * cdiv(N, 128);
+  if (tiles128 >= 256)
+    return dispatch_t<double, double, 128, 128>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
+                                                C, ldc);
+  return dispatch_t<double, double, 64, 64>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C,
+                                            ldc);
+}
+size_t dgemm_splitk_scratch(int M, int N, int splits) {
+  return sizeof(double) * size_t(M) * size_t(N) * size_t(splits);
+}
+
+hipError_t dgemm_splitk(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
+                        const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                        double *C, int64_t ldc, int splits, double *scratch) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (splits <= 1 || K < 2 * KC * splits)
+    return dgemm(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  const int64_t zs = int64_t(M) * N;
+  const int kchunk = ((cdiv(K, splits) + KC - 1) / KC) * KC;
+  const int nz = cdiv(K, kchunk);
+  hipError_t e = dispatch_t<double, double, 64, 64>(st, ta, tb, M, N, K, 1.0, A, lda, B, ldb, 0.0,
+                                                    scratch, N, splits, zs);
+  if (e != hipSuccess) return e;
+  const int blocks = int(std::min<int64_t>(4096, (zs + 255) / 256));
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, scratch, nz, zs, M, N,
+                     alpha, beta, C, ldc);
+  return hipGetLastError();
+}
+
+// C = alpha * X^T X + beta * C on lower tiles, mirrored (X is K x n, ld ldx).
+hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
+                    double beta, double *C, int64_t ldc) {
+  if (n <= 0) return hipSuccess;
+  constexpr int BT = 64;
+  const int nt = cdiv(n, BT);
+  hipLaunchKernelGGL((dgemm_kernel<double, double, BT, BT, true, false, true>),
+                     dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X, ldx,
+                     beta, C, ldc, K > 0 ? K : 1, int64_t(0));
+  return hipGetLastError();
+}
+
+// C = alpha * X X^T + beta * C on lower tiles, mirrored (X is n x K, ld ldx).
+hipError_t dsyrk_nt(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
+                    double beta, double *C, int64_t ldc) {
+  if (n <= 0) return hipSuccess;
+  constexpr int BT = 64;
+  const int nt = cdiv(n, BT);
+  hipLaunchKernelGGL((dgemm_kernel<double, double, BT, BT, false, true, true>),
+                     dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X, ldx,
+                     beta, C, ldc, K > 0 ? K : 1, int64_t(0));
+  return hipGetLastError();
+}
+}  // namespace tg
+
+extern "C" int tg_dgemm(void *stream, int transA, int transB, int M, int N, int K, double alpha,
+                        const double *A, int lda, const double *B, int ldb, double beta,
+                        double *C, int ldc) {
+  TG_ARG(M >= 0 && N >= 0 && K >= 0, 4, "negative size");
+  TG_ARG(A && B && C, 8, "null pointer");
+  TG_HIP(tg::dgemm((hipStream_t)stream, transA != 0, transB != 0, M, N, K, alpha, A, lda, B, ldb,
+                   beta, C, ldc));
+  return 0;
+}
+
+extern "C" int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n,
+                             int64_t ldx, double *H, int ldh) {
+  TG_ARG(X, 2, "null X");
+  TG_ARG(x_dtype >= TG_F16 && x_dtype <= TG_F64, 3, "unsupported dtype");
+  TG_ARG(rows >= 0 && rows <= INT32_MAX, 4, "rows out of range");
+  TG_ARG(n > 0, 5, "n <= 0");
+  TG_ARG(ldx >= n, 6, "ldx < n");
+  TG_ARG(H, 7, "null H");
+  TG_ARG(ldh >= n, 8, "ldh < n");
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  switch (x_dtype) {
+    case TG_F16: e = syrk_t(st, (const __half *)X, rows, n, ldx, H, ldh); break;
+    case TG_BF16: e = syrk_t(st, (const __hip_bfloat16 *)X, rows, n, ldx, H, ldh); break;
+    case TG_F32: e = syrk_t(st, (const float *)X, rows, n, ldx, H, ldh); break;
+    default: e = syrk_t(st, (const double *)X, rows, n, ldx, H, ldh); break;
+  }
+  TG_HIP(e);
+  return 0;
+}

@@ -43,6 +43,11 @@ int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n,
  * out may alias H. */
 int tg_scale_f64(void *stream, const double *H, int64_t count, double inv_n, double *out);
 
+/* FP64 MFMA GEMM used by every dense stage (exported for tests / reuse):
+ * C = alpha op(A) op(B) + beta C, row-major, op(A) M x K, op(B) K x N. */
+int tg_dgemm(void *stream, int transA, int transB, int M, int N, int K, double alpha,
+             const double *A, int lda, const double *B, int ldb, double beta, double *C, int ldc);
+
 /* ---- A2: symmetric eigensolver (torch.linalg.eigh, gptq_utils.py:93) ----
  * Stage 1: A (n x n symmetric, full storage, destroyed) -> tridiagonal
  * (Householder, lower) + all eigenvalues ascending in w_asc (n).  The
