@@ -1,0 +1,311 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X-native TruncGPTQ per-layer solver.
+
+BASELINE.json metric: "weight-cols quantized/sec at d_in=4096".  One step =
+one full solve of an independent synthetic layer per rank, with the Hessian
+already resident in HBM:
+
+    process_hessian_alt(H, 1e-4, "energy")     eigh, rank rule, pivot order, R_x, U
+    gptq_fwrd(W, U, Quantizer(4, 128), perm, block_size=1024)
+    pack_quantized(...)                        AutoGPTQ-style int32 packing
+    [N > 1] RCCL all_gather of the packed weights (the only collective)
+
+Workload (BASELINE.json configs[1]): X = randn(3072, 4096)
+fp32 -> fp16 (seed = rank), H = X^T X / 3072 in float64 (FP64 SYRK on the GPU,
+outside the timed region, reported separately), W = randn(4096, 4096) f32,
+4-bit asym g128, eps = 1e-4 energy (k ~ 3058), block 1024.
+
+Launch (driver contract):
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAKS = {  # MI355X_MICROARCH.md chip table (spec / dense)
+    "hbm": ("GB/s", 8000.0),
+    "fp32_mfma": ("TFLOP/s", 157.3),
+    "fp64_mfma": ("TFLOP/s", 78.6),
+}
+# kernel class -> roofline it is bound by
+BOUND = {
+    "tri_symv": ("hbm", "bytes"),
+    "cross_gemm": ("fp32_mfma", "flops"),
+    "quant_block": ("hbm", "bytes"),
+    "tri_syr2k": ("fp64_mfma", "flops"),
+    "pivot_step": ("hbm", "bytes"),
+    "bisect": ("hbm", "bytes"),
+    "inverse_iteration": ("hbm", "bytes"),
+    "back_transform": ("fp64_mfma", "flops"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--n", type=int, default=4096, help="in_features (d_in)")
+    p.add_argument("--m", type=int, default=4096, help="out_features")
+    p.add_argument("--tokens", type=int, default=3072, help="calibration rows of X")
+    p.add_argument("--bits", type=int, default=4)
+    p.add_argument("--group", type=int, default=128)
+    p.add_argument("--sym", action="store_true")
+    p.add_argument("--eps", type=float, default=1e-4)
+    p.add_argument("--block", type=int, default=1024)
+    p.add_argument("--prof-every", type=int, default=8,
+                   help="sample every k-th launch of each kernel class with HIP events")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-syrk", action="store_true")
+    return p.parse_args()
+
+
+def make_problem(args, rank, device):
+    torch.manual_seed(rank)
+    X = torch.randn(args.tokens, args.n).half()
+    W = torch.randn(args.m, args.n)
+    return X, W
+
+
+def solve(g, H, W, args, gather=None):
+    R, R_x, perm = g.process_hessian_alt(H, args.eps, "energy")
+    q = g.Quantizer(args.bits, args.group, args.sym)
+    Wq, k = g.gptq_fwrd(W, R, q, perm, block_size=args.block, use_triton=True)
+    qweight, qzeros, scales = g.pack_quantized(q)
+    if gather is not None:
+        gather(qweight)
+    return k, qweight
+
+
+def phases(g, H, W, args):
+    """One instrumented solve: wall ms per stage (device-synchronised)."""
+    from gptq_svd_amd import _lib
+    from gptq_svd_amd._lib import call, ptr, stream, workspace
+    dev = H.device
+    n = H.shape[0]
+    sync = torch.cuda.synchronize
+    out = {}
+
+    def tick(name, t0):
+        sync()
+        out[name] = round((time.perf_counter() - t0) * 1e3, 3)
+        return time.perf_counter()
+
+    sync()
+    t = time.perf_counter()
+    A = H.contiguous().clone()
+    ws = workspace(_lib.lib.tg_eigh_workspace_size(n), dev)
+    w = torch.empty(n, dtype=torch.float64, device=dev)
+    call("tg_eigh_values", stream(), ptr(A), n, n, ptr(w), ptr(ws), ws.numel())
+    t = tick("eigh_values", t)
+    S = torch.empty(n, dtype=torch.float64, device=dev)
+    kd = torch.empty(1, dtype=torch.int32, device=dev)
+    call("tg_truncation_rank", stream(), ptr(w), n, args.eps, 1, ptr(S), ptr(kd))
+    k = int(kd.item())
+    t = tick("rank", t)
+    Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
+    call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
+    t = tick("eigh_vectors", t)
+    del ws, A
+    perm = torch.empty(n, dtype=torch.int64, device=dev)
+    Rx = torch.empty((k, n), dtype=torch.float64, device=dev)
+    ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+    call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(Rx), n, ptr(ws),
+         ws.numel())
+    t = tick("pivot_order_Rx", t)
+    U = torch.empty((k, n), dtype=torch.float64, device=dev)
+    ws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
+    call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n, ptr(ws),
+         ws.numel())
+    t = tick("u_factor", t)
+    q = g.Quantizer(args.bits, args.group, args.sym)
+    g.gptq_fwrd(W, U, q, perm, block_size=args.block)
+    t = tick("quantize", t)
+    g.pack_quantized(q)
+    tick("pack", t)
+    return out, k
+
+
+def syrk_bench(g, args, device):
+    """Hessian accumulation (A1), reported separately."""
+    res = {}
+    n = args.n
+    for rows, reps in ((args.tokens, 1), (65536, 4)):
+        X = torch.randn(rows, n, device=device).half()
+        acc = g.HessianAccumulator(n, device)
+        acc.add_batch(X)  # warm
+        torch.cuda.synchronize()
+        acc = g.HessianAccumulator(n, device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            acc.add_batch(X)
+        acc.get_hessian()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        N = rows * reps
+        res[f"N{N}"] = dict(ms=round(dt * 1e3, 3),
+                            tflops_algorithmic=round(2.0 * N * n * n / dt / 1e12, 2))
+        del X
+    return res
+
+
+def cpu_baseline(H, W, args):
+    """The oracle's CPU restatement of the reference path (numpy eigh, LAPACK
+    dgeqp3, numpy QR, exact C block loop + torch SGEMM), timed on this host."""
+    import numpy as np
+    from oracle import oracle as o
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    Hn = H.cpu().numpy()
+    Wn = W.cpu().numpy()
+    t0 = time.perf_counter()
+    f = o.process_hessian_alt(Hn, args.eps, "energy")
+    t1 = time.perf_counter()
+    _, k, codes = o.gptq_fwrd(Wn, f.U, f.perm, args.bits, args.group, args.sym, args.block,
+                              gemm="torch", impl="c", return_codes=True, nthreads=cores)
+    s, z = o.find_params(Wn, args.bits, args.group, args.sym)
+    o.pack_weights(codes, s, z, args.bits, args.sym)
+    t2 = time.perf_counter()
+    dt = t2 - t0
+    return dict(value=round(args.n / dt, 2), unit="cols/s", cores=cores, kind="port",
+                sample=(f"one full {args.m}x{args.n} solve (k={f.k}) of the same synthetic layer: "
+                        f"factorisation {t1 - t0:.2f}s + quantize/pack {t2 - t1:.2f}s"))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import gptq_svd_amd.gptq_utils as g
+    from gptq_svd_amd import _lib
+
+    X, W_cpu = make_problem(args, rank, device)
+    acc = g.HessianAccumulator(args.n, device)
+    acc.add_batch(X.to(device))
+    H = acc.get_hessian()
+    W = W_cpu.to(device)
+    del acc
+
+    gather = None
+    if world > 1:
+        def gather(qw):
+            out = torch.empty((world,) + tuple(qw.shape), dtype=qw.dtype, device=qw.device)
+            dist.all_gather_into_tensor(out, qw.contiguous())
+            return out
+
+    for _ in range(args.warmup):
+        solve(g, H, W, args, gather)
+    torch.cuda.synchronize()
+
+    _lib.profile_reset()
+    _lib.profile_enable(True, args.prof_every)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        k, _ = solve(g, H, W, args, gather)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    prof = _lib.profile_query()
+    if world > 1:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    value = world * args.n * args.steps / dt
+
+    # roofline of the dominant kernel class (largest estimated share of step time)
+    best = None
+    for name, p in prof.items():
+        if p["sampled"] == 0:
+            continue
+        est_total = p["ms"] * p["launches"] / p["sampled"]
+        if best is None or est_total > best[1]:
+            best = (name, est_total, p)
+    roof = None
+    shares = {}
+    for name, p in prof.items():
+        if p["sampled"]:
+            shares[name] = round(p["ms"] * p["launches"] / p["sampled"] / args.steps, 3)
+    if best is not None:
+        name, _, p = best
+        kind, field = BOUND[name]
+        unit, peak = PEAKS[kind]
+        avg_ms = p["ms"] / p["sampled"]
+        per_launch = p[field] / p["sampled"]
+        if field == "bytes":
+            achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        else:
+            achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        roof = dict(kernel=name, bound="hbm" if kind == "hbm" else "mfma",
+                    achieved=round(achieved, 3), peak=peak, unit=unit,
+                    frac=round(achieved / peak, 4), traffic=None,
+                    avg_launch_ms=round(avg_ms, 5), launches_per_step=p["launches"] // args.steps)
+
+    extra = {}
+    if rank == 0:
+        ph, _ = phases(g, H, W, args)
+        extra["phases_ms"] = ph
+        extra["kernel_ms_per_step"] = shares
+        if not args.no_syrk:
+            extra["syrk"] = syrk_bench(g, args, device)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(H, W, args)
+
+    if rank == 0:
+        line = {
+            "metric": "weight-cols quantized/sec at d_in=4096",
+            "value": round(value, 2),
+            "unit": "cols/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64+f32",
+            "data": "synthetic (X randn fp16 3072x4096 -> H=X^T X/N f64; W randn f32)",
+            "config": {
+                "workload": (f"single synthetic {args.n}x{args.n} Hessian per rank, full solver "
+                             f"(eigh, rank rule, pivot order, U, {args.bits}-bit "
+                             f"{'sym' if args.sym else 'asym'} g{args.group} quantize, pack)"),
+                "n": args.n, "m": args.m, "calib_rows": args.tokens, "rank_k": k,
+                "eps": args.eps, "threshold_method": "energy", "block_size": args.block,
+                "parallelism": (f"independent layer per rank x{world}"
+                                + (", RCCL all_gather of packed weights" if world > 1 else "")),
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            **extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

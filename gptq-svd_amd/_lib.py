@@ -31,6 +31,10 @@ _SIGS = {
     "tg_version": ([], _i),
     "tg_syrk_accum": ([_vp, _vp, _i, _i64, _i, _i64, _vp, _i], _i),
     "tg_scale_f64": ([_vp, _vp, _i64, _d, _vp], _i),
+    "tg_profile_enable": ([_i, _i], _i),
+    "tg_profile_reset": ([], _i),
+    "tg_profile_query": ([_i, ctypes.POINTER(_d), ctypes.POINTER(_i64), ctypes.POINTER(_d),
+                          ctypes.POINTER(_d), ctypes.POINTER(_i64)], _i),
     "tg_dgemm": ([_vp, _i, _i, _i, _i, _i, _d, _vp, _i, _vp, _i, _d, _vp, _i], _i),
     "tg_eigh_workspace_size": ([_i], _sz),
     "tg_eigh_values": ([_vp, _vp, _i, _i, _vp, _vp, _sz], _i),
@@ -64,6 +68,31 @@ TG_F16, TG_BF16, TG_F32, TG_F64 = 0, 1, 2, 3
 RULES = {"none": 0, "energy": 1, "mean_trimmed": 2}
 DTYPES = {torch.float16: TG_F16, torch.bfloat16: TG_BF16, torch.float32: TG_F32,
           torch.float64: TG_F64}
+
+
+PROF_CLASSES = ["tri_symv", "cross_gemm", "quant_block", "tri_syr2k", "pivot_step", "bisect",
+                "inverse_iteration", "back_transform"]
+
+
+def profile_enable(on: bool = True, every: int = 1) -> None:
+    lib.tg_profile_enable(int(on), int(every))
+
+
+def profile_reset() -> None:
+    lib.tg_profile_reset()
+
+
+def profile_query() -> dict:
+    """{class: dict(ms, sampled, launches, bytes, flops)} over sampled launches."""
+    out = {}
+    for i, name in enumerate(PROF_CLASSES):
+        ms, b, f = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        s, tot = ctypes.c_int64(), ctypes.c_int64()
+        lib.tg_profile_query(i, ctypes.byref(ms), ctypes.byref(s), ctypes.byref(b), ctypes.byref(f),
+                             ctypes.byref(tot))
+        out[name] = dict(ms=ms.value, sampled=s.value, launches=tot.value, bytes=b.value,
+                         flops=f.value)
+    return out
 
 
 def last_error() -> str:

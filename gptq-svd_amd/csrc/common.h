@@ -36,6 +36,19 @@ struct Sizer {
 
 inline int cdiv(int64_t a, int64_t b) { return int((a + b - 1) / b); }
 
+// Sampled HIP-event timing of tagged kernel classes (tg_profile_* in the C ABI).
+// A launch site calls prof_begin/prof_end around the launch on its stream; when
+// profiling is on, every `every`-th launch of the class is bracketed by events
+// and its algorithmic bytes / flops are recorded for roofline reporting.
+enum ProfId { PROF_TRI_SYMV = 0, PROF_CROSS_GEMM = 1, PROF_QBLOCK = 2, PROF_SYR2K = 3,
+              PROF_PIVSTEP = 4, PROF_BISECT = 5, PROF_INVIT = 6, PROF_BACKTR = 7, PROF_N = 8 };
+struct ProfTok {
+  int id = -1;
+  int slot = -1;
+};
+ProfTok prof_begin(hipStream_t st, int id, double bytes, double flops);
+void prof_end(hipStream_t st, ProfTok tok);
+
 }  // namespace tg
 
 #define TG_ARG(cond, idx, msg)                                   \

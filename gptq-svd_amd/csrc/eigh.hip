@@ -487,7 +487,8 @@ __global__ __launch_bounds__(256) void cluster_mgs_kernel(const double *__restri
   while (start < k) {
     int end = start + 1;
     while (end < k && fabs(w_asc[n - 1 - (end - 1)] - w_asc[n - 1 - end]) <= gap) ++end;
-    for (int c = start + 1; c < end; ++c) {
+    for (int c = start; c < end && end - start > 1; ++c) {
+      for (int pass = 0; pass < 2; ++pass)  // MGS twice ("twice is enough")
       for (int b = start; b < c; ++b) {
         double dot = 0.0;
         for (int i = threadIdx.x; i < n; i += blockDim.x) dot += Z[size_t(i) * k + b] * Z[size_t(i) * k + c];
@@ -615,11 +616,14 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
     if (p >= n - 1) break;  // last column: only d[n-1]
     const int pe = min(p + NB, n - 1);
     for (int i = p; i < pe; ++i) {
+      const double len = double(n - i - 1);
+      auto tok = tg::prof_begin(st, tg::PROF_TRI_SYMV, 8.0 * len * len, 2.0 * len * len);
       if (vlds)
         hipLaunchKernelGGL(tri_symv_kernel<true>, dim3(NG), dim3(256), vsh_bytes, st, A, lda, n,
                            i, p, w);
       else
         hipLaunchKernelGGL(tri_symv_kernel<false>, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, w);
+      tg::prof_end(st, tok);
       TG_LAUNCHED();
       const int do_next = (i + 1 < p + NB) ? 1 : 0;
       hipLaunchKernelGGL(tri_fin_kernel, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, do_next, w);
@@ -631,8 +635,11 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
       double *C = A + size_t(q) * lda + q;
       const double *Vb = w.V + size_t(q) * n + p;
       const double *Wb = w.W + size_t(q) * NB;
+      auto tok = tg::prof_begin(st, tg::PROF_SYR2K, 8.0 * 3.0 * double(mt) * mt,
+                                4.0 * double(mt) * mt * NB);
       TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Vb, n, Wb, NB, 1.0, C, lda));
       TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Wb, NB, Vb, n, 1.0, C, lda));
+      tg::prof_end(st, tok);
     }
   }
   // eigenvalues of T
@@ -643,6 +650,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   const size_t lds = 2 * sizeof(double) * size_t(n);
   hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.e, n, w.acol);
   TG_LAUNCHED();
+  auto btok = tg::prof_begin(st, tg::PROF_BISECT, 16.0 * n, 0.0);
   if (lds <= 160 * 1024) {
     if (lds > 64 * 1024)
       TG_HIP(hipFuncSetAttribute((const void *)bisect_kernel<true>,
@@ -653,6 +661,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
     hipLaunchKernelGGL(bisect_kernel<false>, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
                        w_asc);
   }
+  tg::prof_end(st, btok);
   TG_LAUNCHED();
   return 0;
 }
@@ -681,10 +690,12 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   tri_layout(ar, n, &w);
   TG_WS(ar);
   const double *bnd = w.scal;
+  auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
   hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.e, n, k, w_asc,
                      bnd, w);
+  tg::prof_end(st, itok);
   TG_LAUNCHED();
-  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-10, w.Z);
+  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-9, w.Z);
   TG_LAUNCHED();
   // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
   const int nref = n - 1;
@@ -692,6 +703,7 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
     const int nblk = tg::cdiv(nref, BT);
     hipLaunchKernelGGL(tfactor_kernel, dim3(nblk), dim3(256), 0, st, w.V, n, nref, w.tau, w.Tf);
     TG_LAUNCHED();
+    auto btok2 = tg::prof_begin(st, tg::PROF_BACKTR, 0.0, 2.0 * double(n) * n * k);
     for (int b = nblk - 1; b >= 0; --b) {
       const int p = b * BT, bw = min(BT, nref - p), r0 = p + 1;
       const double *Vb = w.V + size_t(r0) * n + p;
@@ -705,6 +717,7 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
       TG_HIP(tg::dgemm(st, false, false, n - r0, k, bw, -1.0, Vb, n, w.X2, k, 1.0,
                        w.Z + size_t(r0) * k, k));
     }
+    tg::prof_end(st, btok2);
   }
   hipLaunchKernelGGL(transpose_kernel, dim3(tg::cdiv(k, 32), tg::cdiv(n, 32)), dim3(32, 8), 0, st,
                      w.Z, n, k, Vh, ldv);

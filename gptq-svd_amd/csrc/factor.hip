@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void piv_step_kernel(int n, int k, int i, int 
       bp = j;
     }
   }
-  if (i + 1 < n) argmax_publish(bv, bp, i + 1, n, w);
+  // dgeqp3 stops after min(k, n) steps: no swap into position k.
+  if (i + 1 < k) argmax_publish(bv, bp, i + 1, n, w);
 }
 
 // Rx[t][j] = L[perm[j]][t] for j >= t (upper trapezoidal), perm64 = perm.
@@ -287,7 +288,9 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
     const int pe = std::min(ps + PB, k);
     for (int i = ps; i < pe; ++i) {
       const int g = std::max(1, std::min(PGMAX, tg::cdiv(n - i - 1, 256)));
+      auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n - i) * (i - ps + 3), 0.0);
       hipLaunchKernelGGL(piv_step_kernel, dim3(g), dim3(256), 0, st, n, k, i, ps, w);
+      tg::prof_end(st, tok);
       TG_LAUNCHED();
     }
     if (pe < k)  // Schur update with this panel's columns (all rows, original order)

@@ -543,12 +543,19 @@ extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, cons
     a.E = q.E; a.lde = bp; a.corr = q.corr; a.ldcorr = bp;
     a.scale = scale; a.zero = zero; a.perm = q.perm32; a.G = G; a.g = g; a.col0 = i1;
     a.m = m; a.bw = bw; a.minq = minq; a.maxq = maxq; a.code_off = code_off;
+    auto qtok = tg::prof_begin(st, tg::PROF_QBLOCK, 4.0 * 4.0 * double(m) * bw,
+                               double(m) * bw * (bw - 1));
     hipLaunchKernelGGL(block_kernel<true>, dim3(tg::cdiv(m, RW)), dim3(256), block_smem(bw), st,
                        a);
+    tg::prof_end(st, qtok);
     TG_LAUNCHED();
     if (nc > 0) {
+      auto gtok = tg::prof_begin(st, tg::PROF_CROSS_GEMM,
+                                 4.0 * (double(m) * bw + double(bw) * nc + 2.0 * double(m) * nc),
+                                 2.0 * double(m) * bw * nc);
       hipLaunchKernelGGL(cross_gemm_kernel, dim3(tg::cdiv(nc, GN), tg::cdiv(m, GM)), dim3(256), 0,
                          st, q.E, bp, q.SM, n, q.Wp + i2, n, m, nc, bw);
+      tg::prof_end(st, gtok);
       TG_LAUNCHED();
     }
   }

