@@ -206,10 +206,8 @@ def main():
 
     gather = None
     if world > 1:
-        def gather(qw):
-            out = torch.empty((world,) + tuple(qw.shape), dtype=qw.dtype, device=qw.device)
-            dist.all_gather_into_tensor(out, qw.contiguous())
-            return out
+        from gptq_svd_amd.dist import gather_packed
+        gather = gather_packed
 
     for _ in range(args.warmup):
         solve(g, H, W, args, gather)

@@ -20,6 +20,7 @@
 //      pseudo-random start); tight clusters are re-orthogonalised (MGS).
 //   4. Back-transformation V = Q Z with compact-WY blocks of BT reflectors
 //      (dlarft T factors, FP64 MFMA GEMMs, split-K for the V^T Z products).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <type_traits>
@@ -32,7 +33,8 @@
 namespace {
 
 constexpr int NB = 32;    // tridiagonalisation panel width
-constexpr int NG = 256;   // workgroups of the row-parallel kernels
+constexpr int NG = 256;   // workgroups of the symv kernel (16 waves each)
+constexpr int SYT = 1024; // symv threads per workgroup
 constexpr int BT = 64;    // back-transformation block of reflectors
 constexpr int PST = 2 * NB + 2;  // partials stride
 constexpr int ML = 16;    // multisection lanes per eigenvalue
@@ -41,23 +43,27 @@ constexpr int SPLITK = 8;
 
 struct Tri {
   double *V;     // n x n reflectors: V[r*n + j] = v_j[r] (0 above j+1, 1 at r = j+1)
-  double *W;     // n x NB  dlatrd panel W
+  double *PT;    // 3 x NB x n  column-major panel [V^T; W^T; V^T] (coalesced, one K=2NB update)
   double *tau;   // n
   double *d;     // n   diagonal of T
   double *e;     // n   off-diagonal of T (e[i] couples i, i+1)
   double *acol;  // n   current updated column
   double *y;     // n   symv result
-  double *part;  // NG x PST partial sums
+  double *part;  // PST x NG partial sums (transposed)
   double *red;   // PST reduced sums: [0] = |x|^2, [1..NB] = V^T v, [1+NB..2NB] = W^T v, [1+2NB] = v^T y
   double *Tf;    // nblk x BT x BT  block-reflector T factors
   double *Z;     // n x n  eigenvectors of T (column j), later of A
-  double *lu;    // 4 x n x n  inverse-iteration LU factors ([i][thread] layout)
+  double *lu;    // 3 x n x n  inverse-iteration U factors ([i][thread] layout)
   double *X1;    // BT x n
   double *X2;    // BT x n
   double *skp;   // split-K scratch
   double *scal;  // small scalars (norm of T)
+  double *es;    // n   off-diagonal with negligible entries zeroed (block splits)
+  double *wraw;  // n   eigenvalue of slot j (block-local order)
+  int32_t *bs;   // n   start of the unreduced block containing position j
+  int32_t *be;   // n   end (exclusive) of that block
+  int32_t *slot; // n   slot of the j-th smallest eigenvalue
   unsigned *cnt; // reduction tickets
-  int8_t *piv;   // n x n pivot flags
 };
 
 template <class A>
@@ -72,7 +78,7 @@ void tri_layout(A &ar, int n, Tri *t) {
     else ar.template take<T>(cnt);
   };
   take(q.V, nn);
-  take(q.W, size_t(n) * NB);
+  take(q.PT, size_t(3) * NB * n);
   take(q.tau, n);
   take(q.d, n);
   take(q.e, n);
@@ -82,13 +88,17 @@ void tri_layout(A &ar, int n, Tri *t) {
   take(q.red, PST);
   take(q.Tf, size_t(nblk) * BT * BT);
   take(q.Z, nn);
-  take(q.lu, 4 * nn);
+  take(q.lu, 3 * nn);
   take(q.X1, size_t(BT) * n);
   take(q.X2, size_t(BT) * n);
   take(q.skp, size_t(SPLITK) * BT * n);
   take(q.scal, 16);
   take(q.cnt, 16);
-  take(q.piv, nn);
+  take(q.es, n);
+  take(q.wraw, n);
+  take(q.bs, n);
+  take(q.be, n);
+  take(q.slot, n);
 }
 
 // ---------------------------------------------------------------------------
@@ -112,20 +122,22 @@ __global__ __launch_bounds__(256) void tri_start_kernel(const double *__restrict
   s = tg::block_sum(s, scratch);
   if (threadIdx.x == 0) vals[0] = s;
   __syncthreads();
-  if (tg::publish_partials(vals, 1, w.part, PST, w.cnt)) tg::sum_partials(w.part, PST, 1, w.red, w.cnt);
+  if (tg::publish_partials(vals, 1, w.part, w.cnt)) tg::sum_partials(w.part, 1, w.red, w.cnt);
 }
 
 // Reflector for column i + y = A[i+1:, i+1:] v + partial V^T v, W^T v, v^T y.
-// VLDS: v staged in LDS (n <= 16384); otherwise v_c = acol[c] * scal on the fly.
+// One wave per row; lanes stream the row as 16-byte double2 loads, 8 in flight
+// per lane.  v lives in LDS (n <= 16384) indexed by absolute column, zero
+// below i+1; otherwise v_c = acol[c] * scal is formed on the fly.
 template <bool VLDS>
-__global__ __launch_bounds__(256) void tri_symv_kernel(const double *__restrict__ A, int lda, int n,
+__global__ __launch_bounds__(SYT) void tri_symv_kernel(const double *__restrict__ A, int lda, int n,
                                                        int i, int p, Tri w) {
-  extern __shared__ double vsh[];  // n - i - 1 entries of v
-  __shared__ double wpart[4][PST];
+  extern __shared__ double vsh[];
+  __shared__ double wpart[SYT / 64][PST];
   __shared__ double vals[PST];
   const int t = i - p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int len = n - i - 1;
+  const double *VT = w.PT, *WT = w.PT + size_t(NB) * n;
   // dlarfg (LAPACK): beta = -sign(alpha) * hypot(alpha, |x|), tau = (beta-alpha)/beta,
   // v = [1, x / (alpha - beta)]
   const double xn2 = w.red[0];
@@ -136,55 +148,90 @@ __global__ __launch_bounds__(256) void tri_symv_kernel(const double *__restrict_
     tau = (beta - alpha) / beta;
     scal = 1.0 / (alpha - beta);
   }
-  if (VLDS)
-    for (int c = tid; c < len; c += blockDim.x) vsh[c] = c == 0 ? 1.0 : w.acol[i + 1 + c] * scal;
-  const double *ac = w.acol + i + 1;
-  auto vget = [&](int c) -> double {
-    if (VLDS) return vsh[c];
-    return c == 0 ? 1.0 : ac[c] * scal;
+  const int c_lo = (i + 1) & ~1;
+  auto vval = [&](int c) -> double {
+    return c < i + 1 ? 0.0 : (c == i + 1 ? 1.0 : w.acol[c] * scal);
   };
+  if (VLDS)
+    for (int c = c_lo + tid; c < n; c += blockDim.x) vsh[c] = vval(c);
   if (blockIdx.x == 0 && tid == 0) {
     w.tau[i] = tau;
     w.e[i] = beta;
   }
-  for (int j = tid; j < 4 * PST; j += blockDim.x) (&wpart[0][0])[j] = 0.0;
+  for (int j = tid; j < (SYT / 64) * PST; j += blockDim.x) (&wpart[0][0])[j] = 0.0;
   __syncthreads();
 
+  const bool vec = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const int len2 = (n - c_lo) >> 1;  // double2 count
+  const int tail = (n - c_lo) & 1;
   double q1 = 0.0, q2 = 0.0, sv = 0.0;  // per-lane partials (lane l -> panel column l)
-  const int gw = blockIdx.x * 4 + wid;
-  for (int r = i + 1 + gw; r < n; r += NG * 4) {
-    const double *row = A + size_t(r) * lda + (i + 1);
-    double dot = 0.0;
-    for (int c = lane; c < len; c += 64) dot += row[c] * vget(c);
+  const int TW = gridDim.x * (SYT / 64);
+  for (int r = i + 1 + blockIdx.x * (SYT / 64) + wid; r < n; r += TW) {
+    const double *row = A + size_t(r) * lda + c_lo;
+    double a0 = 0.0, a1 = 0.0;
+    if (VLDS && vec) {
+      const double2 *r2 = reinterpret_cast<const double2 *>(row);
+      const double2 *v2 = reinterpret_cast<const double2 *>(vsh + c_lo);
+      int c = lane;
+      for (; c + 7 * 64 < len2; c += 8 * 64) {
+        double2 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = r2[c + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double2 vv = v2[c + u * 64];
+          a0 += x[u].x * vv.x;
+          a1 += x[u].y * vv.y;
+        }
+      }
+      for (; c < len2; c += 64) {
+        const double2 x = r2[c], vv = v2[c];
+        a0 += x.x * vv.x;
+        a1 += x.y * vv.y;
+      }
+      if (tail && lane == 0) a0 += row[2 * len2] * vsh[c_lo + 2 * len2];
+    } else {
+      for (int c = lane; c < n - c_lo; c += 64) {
+        const double vc = VLDS ? vsh[c_lo + c] : vval(c_lo + c);
+        a0 += row[c] * vc;
+      }
+    }
+    double dot = a0 + a1;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
-    const double vr = vget(r - i - 1);
+    const double vr = VLDS ? vsh[r] : vval(r);
     if (lane == 0) {
       w.y[r] = dot;
       w.V[size_t(r) * n + i] = vr;
       sv += vr * dot;
     }
+    if (lane == 1) w.PT[size_t(t) * n + r] = vr;                   // V^T panel row t
+    if (lane == 2) w.PT[size_t(2 * NB + t) * n + r] = vr;          // second copy
     if (lane < t) {
-      q1 += w.V[size_t(r) * n + p + lane] * vr;
-      q2 += w.W[size_t(r) * NB + lane] * vr;
+      q1 += VT[size_t(lane) * n + r] * vr;
+      q2 += WT[size_t(lane) * n + r] * vr;
     }
   }
-  if (lane < NB) {
+  // live values only: [q1 (t) | q2 (t) | v^T y]
+  if (lane < t) {
     wpart[wid][lane] = q1;
-    wpart[wid][NB + lane] = q2;
+    wpart[wid][t + lane] = q2;
   }
-  if (lane == 0) wpart[wid][2 * NB] = sv;
+  if (lane == 0) wpart[wid][2 * t] = sv;
   __syncthreads();
-  constexpr int NV = 2 * NB + 1;
-  for (int j = tid; j < NV; j += blockDim.x)
-    vals[j] = wpart[0][j] + wpart[1][j] + wpart[2][j] + wpart[3][j];
+  const int nv = 2 * t + 1;
+  for (int j = tid; j < nv; j += blockDim.x) {
+    double s = 0.0;
+    for (int ww = 0; ww < SYT / 64; ++ww) s += wpart[ww][j];
+    vals[j] = s;
+  }
   __syncthreads();
-  if (tg::publish_partials(vals, NV, w.part, PST, w.cnt))
-    tg::sum_partials(w.part, PST, NV, w.red + 1, w.cnt);
+  if (tg::publish_partials(vals, nv, w.part, w.cnt)) tg::sum_partials(w.part, nv, w.red + 1, w.cnt);
 }
 
 // W[:, t] = tau (y - V (W^T v) - W (V^T v)) + alpha2 v, then (do_next) update
-// column i+1 with the panel's t+1 reflectors and reduce its |x|^2.
+// column i+1 with the panel's t+1 reflectors and reduce its |x|^2.  One thread
+// per row; the column-major panel makes every load coalesced.
 __global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__ A, int lda, int n,
                                                       int i, int p, int do_next, Tri w) {
   __shared__ double q1[NB], q2[NB], vrow[NB], wrow[NB];
@@ -192,20 +239,20 @@ __global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__
   __shared__ double vals[1];
   const int t = i - p, j = i + 1;
   const int tid = threadIdx.x;
+  const double *VT = w.PT;
+  double *WT = w.PT + size_t(NB) * n;
   const double tau = w.tau[i];
   if (tid < NB) {
     q1[tid] = tid < t ? w.red[1 + tid] : 0.0;
-    q2[tid] = tid < t ? w.red[1 + NB + tid] : 0.0;
+    q2[tid] = tid < t ? w.red[1 + t + tid] : 0.0;
+    vrow[tid] = tid <= t ? VT[size_t(tid) * n + j] : 0.0;
+    wrow[tid] = tid < t ? WT[size_t(tid) * n + j] : 0.0;
   }
   __syncthreads();
   double dq = 0.0;
   for (int l = 0; l < t; ++l) dq += q1[l] * q2[l];
-  const double wtv = tau * (w.red[1 + 2 * NB] - 2.0 * dq);
+  const double wtv = tau * (w.red[1 + 2 * t] - 2.0 * dq);
   const double alpha2 = -0.5 * tau * wtv;
-  // row j of V (panel columns 0..t) and of W (0..t-1, then w_j recomputed here)
-  if (tid <= t && tid < NB) vrow[tid] = w.V[size_t(j) * n + p + tid];
-  if (tid < t) wrow[tid] = w.W[size_t(j) * NB + tid];
-  __syncthreads();
   if (tid == 0) {
     double acc = w.y[j];
     for (int l = 0; l < t; ++l) acc -= vrow[l] * q2[l];
@@ -215,17 +262,28 @@ __global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__
   __syncthreads();
   double s = 0.0;
   for (int r = j + blockIdx.x * blockDim.x + tid; r < n; r += gridDim.x * blockDim.x) {
-    const double *vr_ = w.V + size_t(r) * n + p;
-    double *wr_ = w.W + size_t(r) * NB;
+    double vr_[NB], wr_[NB];
+#pragma unroll
+    for (int l = 0; l < NB; ++l) {
+      vr_[l] = VT[size_t(l) * n + r];
+      wr_[l] = WT[size_t(l) * n + r];
+    }
     double acc = w.y[r];
-    for (int l = 0; l < t; ++l) acc -= vr_[l] * q2[l];
-    for (int l = 0; l < t; ++l) acc -= wr_[l] * q1[l];
-    const double wr = tau * acc + alpha2 * vr_[t];
-    wr_[t] = wr;
+#pragma unroll
+    for (int l = 0; l < NB; ++l) acc -= l < t ? vr_[l] * q2[l] : 0.0;
+#pragma unroll
+    for (int l = 0; l < NB; ++l) acc -= l < t ? wr_[l] * q1[l] : 0.0;
+    double vt = 0.0;
+#pragma unroll
+    for (int l = 0; l < NB; ++l) vt = l == t ? vr_[l] : vt;
+    const double wr = tau * acc + alpha2 * vt;
+    WT[size_t(t) * n + r] = wr;
     if (do_next) {
       double a = A[size_t(j) * lda + r];
-      for (int l = 0; l <= t; ++l) a -= vr_[l] * wrow[l];
-      for (int l = 0; l < t; ++l) a -= wr_[l] * vrow[l];
+#pragma unroll
+      for (int l = 0; l < NB; ++l) a -= l <= t ? vr_[l] * wrow[l] : 0.0;
+#pragma unroll
+      for (int l = 0; l < NB; ++l) a -= l < t ? wr_[l] * vrow[l] : 0.0;
       a -= wr * vrow[t];
       w.acol[r] = a;
       if (r == j) w.d[j] = a;
@@ -236,7 +294,7 @@ __global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__
   s = tg::block_sum(s, scratch);
   if (tid == 0) vals[0] = s;
   __syncthreads();
-  if (tg::publish_partials(vals, 1, w.part, PST, w.cnt)) tg::sum_partials(w.part, PST, 1, w.red, w.cnt);
+  if (tg::publish_partials(vals, 1, w.part, w.cnt)) tg::sum_partials(w.part, 1, w.red, w.cnt);
 }
 
 // ---------------------------------------------------------------------------
@@ -289,12 +347,61 @@ __global__ void tri_bounds_kernel(const double *__restrict__ d, const double *__
   }
 }
 
+// Split T into unreduced blocks at |e_i| <= eps * ||T|| (LAPACK dstebz does the
+// same with a relative test); one thread scans (n is small).  es = e with the
+// split entries zeroed; bs/be = block of each position.
+__global__ void tri_split_kernel(const double *__restrict__ e, int n, const double *__restrict__ bnd,
+                                 double *__restrict__ es, int32_t *__restrict__ bs,
+                                 int32_t *__restrict__ be) {
+  if (threadIdx.x != 0) return;
+  const double tol = DBL_EPSILON * bnd[2];
+  int start = 0;
+  for (int i = 0; i < n; ++i) {
+    const bool split = i == n - 1 || fabs(e[i]) <= tol;
+    es[i] = (i == n - 1 || split) ? 0.0 : e[i];
+    if (split) {
+      for (int j = start; j <= i; ++j) {
+        bs[j] = start;
+        be[j] = i + 1;
+      }
+      start = i + 1;
+    }
+  }
+}
+
+// Global ascending order of the block eigenvalues: rank(j) = #{i: v_i < v_j or
+// (v_i == v_j and i < j)} -- deterministic, O(n^2) compares spread over n threads.
+__global__ void rank_sort_kernel(const double *__restrict__ v, int n, double *__restrict__ w_asc,
+                                 int32_t *__restrict__ slot) {
+  extern __shared__ double sv[];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const double vj = j < n ? v[j] : 0.0;
+  int r = 0;
+  for (int c0 = 0; c0 < n; c0 += 2048) {
+    const int cn = min(2048, n - c0);
+    __syncthreads();
+    for (int c = threadIdx.x; c < cn; c += blockDim.x) sv[c] = v[c0 + c];
+    __syncthreads();
+    if (j < n)
+      for (int c = 0; c < cn; ++c) {
+        const double vi = sv[c];
+        r += (vi < vj) || (vi == vj && c0 + c < j);
+      }
+  }
+  if (j < n) {
+    w_asc[r] = vj;
+    slot[r] = j;
+  }
+}
+
 // LDS: d and e^2 staged in LDS (n <= 10240); otherwise e2 holds e^2 in global memory.
 template <bool LDS>
 __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ d,
                                                      const double *__restrict__ e2g, int n,
                                                      const double *__restrict__ bnd,
-                                                     double *__restrict__ w_asc) {
+                                                     const int32_t *__restrict__ bsv,
+                                                     const int32_t *__restrict__ bev,
+                                                     double *__restrict__ w_out) {
   extern __shared__ double sh[];
   const double *dd = d, *ee2 = e2g;
   if (LDS) {
@@ -310,15 +417,18 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
   const int lane = threadIdx.x & 63;
   const int sub = lane & (ML - 1);
   const int grp_base = lane & ~(ML - 1);
-  const int j = (blockIdx.x * blockDim.x + threadIdx.x) / ML;  // eigenvalue index (ascending)
+  // slot j = local eigenvalue (j - bs) of the unreduced block [bs, be) holding position j
+  const int j = (blockIdx.x * blockDim.x + threadIdx.x) / ML;
+  const int b0 = j < n ? bsv[j] : 0, b1 = j < n ? bev[j] : 1;
+  const int jl = j - b0;
   const double pivmin = bnd[3];
   double lo = bnd[0], hi = bnd[1];
   for (int round = 0; round < ROUNDS; ++round) {
     const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
     int c = 0;
-    if (j < n) c = sturm_count(dd, ee2, n, x, pivmin);
-    // lanes with count(x) <= j have x <= lambda_j
-    const unsigned long long m = __ballot(j < n && c <= j);
+    if (j < n) c = sturm_count(dd + b0, ee2 + b0, b1 - b0, x, pivmin);
+    // lanes with count(x) <= jl have x <= lambda_jl
+    const unsigned long long m = __ballot(j < n && c <= jl);
     const int a = __popcll((m >> grp_base) & ((1ull << ML) - 1));
     const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
     const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
@@ -327,7 +437,7 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
     lo = nlo;
     hi = nhi;
   }
-  if (j < n && sub == 0) w_asc[j] = 0.5 * (lo + hi);
+  if (j < n && sub == 0) w_out[j] = 0.5 * (lo + hi);
 }
 
 // e^2 (e[n-1] = 0 padding)
@@ -387,6 +497,9 @@ __device__ inline double hash_unit(uint32_t a, uint32_t b) {
   return (double(h) + 0.5) / 4294967296.0 - 0.5;
 }
 
+constexpr int FCH = 32;  // forward-sweep chunk (elements staged in registers)
+constexpr int BCH = 16;  // backward-sweep chunk
+
 __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
                                                    const double *__restrict__ e, int n, int k,
                                                    const double *__restrict__ w_asc,
@@ -394,84 +507,125 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
   const int jj = blockIdx.x * blockDim.x + threadIdx.x;
   if (jj >= k) return;
   const double lam = w_asc[n - 1 - jj];
+  const int sl = w.slot[n - 1 - jj];
+  const int b0 = w.bs[sl], b1 = w.be[sl];
   const double tol = fmax(DBL_EPSILON * bnd[2], 1e-300);
   const size_t K = size_t(k);
-  double *dl = w.lu, *dd = w.lu + size_t(n) * n, *du = w.lu + 2 * size_t(n) * n,
-         *du2 = w.lu + 3 * size_t(n) * n;
-  int8_t *pv = w.piv;
-  double *x = w.Z;
+  const size_t nn = size_t(n) * n;
+  // the solve runs on the unreduced block [b0, b1) only; x is zero elsewhere
+  double *dd = w.lu + b0 * K, *du = w.lu + nn + b0 * K, *du2 = w.lu + 2 * nn + b0 * K;
+  double *x = w.Z + b0 * K;
+  d += b0;
+  e += b0;
+  for (int i = 0; i < b0; ++i) w.Z[size_t(i) * K + jj] = 0.0;
+  for (int i = b1; i < n; ++i) w.Z[size_t(i) * K + jj] = 0.0;
+  n = b1 - b0;
   auto at = [&](int i) { return size_t(i) * K + jj; };
-  // factor
-  double cur_d = d[0] - lam;
-  double cur_u = n > 1 ? e[0] : 0.0;
-  for (int i = 0; i < n - 1; ++i) {
-    const double sub = e[i];
-    const double nd = d[i + 1] - lam;
-    const double nu = i + 1 < n - 1 ? e[i + 1] : 0.0;
-    if (fabs(cur_d) >= fabs(sub)) {
-      double piv = cur_d;
-      if (fabs(piv) < tol) piv = piv < 0.0 ? -tol : tol;
-      const double f = sub / piv;
-      dd[at(i)] = piv;
-      du[at(i)] = cur_u;
-      du2[at(i)] = 0.0;
-      dl[at(i)] = f;
-      pv[at(i)] = 0;
-      cur_d = nd - f * cur_u;
-      cur_u = nu;
-    } else {
-      const double f = cur_d / sub;
-      dd[at(i)] = sub;
-      du[at(i)] = nd;
-      du2[at(i)] = nu;
-      dl[at(i)] = f;
-      pv[at(i)] = 1;
-      cur_d = cur_u - f * nd;
-      cur_u = -f * nu;
-    }
-  }
-  {
-    double piv = cur_d;
-    if (fabs(piv) < tol) piv = piv < 0.0 ? -tol : tol;
-    dd[at(n - 1)] = piv;
-  }
-  // start vector
-  for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(i), uint32_t(jj)) + 0.25;
+  auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
+  for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(b0 + i), uint32_t(jj)) + 0.25;
   for (int it = 0; it < 3; ++it) {
-    // forward: apply L^-1 with interchanges
-    for (int i = 0; i < n - 1; ++i) {
-      const double f = dl[at(i)];
-      if (pv[at(i)] == 0) {
-        x[at(i + 1)] -= f * x[at(i)];
-      } else {
-        const double tmp = x[at(i)];
-        x[at(i)] = x[at(i + 1)];
-        x[at(i + 1)] = tmp - f * x[at(i)];
+    // fused LU (dgttrf pattern) + forward substitution with the row interchanges
+    double cur_d = d[0] - lam, cur_u = n > 1 ? e[0] : 0.0, xi = x[at(0)];
+    for (int i0 = 0; i0 < n - 1; i0 += FCH) {
+      const int cnt = min(FCH, n - 1 - i0);
+      double xn[FCH], dn[FCH], en[FCH], enn[FCH];
+#pragma unroll
+      for (int u = 0; u < FCH; ++u) {
+        if (u < cnt) {
+          const int i = i0 + u;
+          xn[u] = x[at(i + 1)];
+          dn[u] = d[i + 1];
+          en[u] = e[i];
+          enn[u] = i + 1 < n - 1 ? e[i + 1] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < FCH; ++u) {
+        if (u < cnt) {
+          const int i = i0 + u;
+          const double sub = en[u], nd = dn[u] - lam, nu = enn[u], xnext = xn[u];
+          double xi_next;
+          if (fabs(cur_d) >= fabs(sub)) {
+            const double piv = clampp(cur_d);
+            const double f = sub / piv;
+            dd[at(i)] = piv;
+            du[at(i)] = cur_u;
+            du2[at(i)] = 0.0;
+            x[at(i)] = xi;
+            xi_next = xnext - f * xi;
+            cur_d = nd - f * cur_u;
+            cur_u = nu;
+          } else {
+            const double f = cur_d / sub;
+            dd[at(i)] = sub;
+            du[at(i)] = nd;
+            du2[at(i)] = nu;
+            x[at(i)] = xnext;
+            xi_next = xi - f * xnext;
+            cur_d = cur_u - f * nd;
+            cur_u = -f * nu;
+          }
+          xi = xi_next;
+        }
       }
     }
-    // backward: U^-1
+    dd[at(n - 1)] = clampp(cur_d);
+    x[at(n - 1)] = xi;
+    // backward substitution with U, in chunks from the end
     double xn1 = 0.0, xn2 = 0.0, amax = 0.0;
-    for (int i = n - 1; i >= 0; --i) {
-      double v = x[at(i)];
-      if (i < n - 1) v -= du[at(i)] * xn1;
-      if (i < n - 2) v -= du2[at(i)] * xn2;
-      v /= dd[at(i)];
-      x[at(i)] = v;
-      xn2 = xn1;
-      xn1 = v;
-      amax = fmax(amax, fabs(v));
+    for (int i1 = n; i1 > 0; i1 -= BCH) {
+      const int i0 = max(0, i1 - BCH), cnt = i1 - i0;
+      double xv[BCH], dv[BCH], uv[BCH], u2v[BCH];
+#pragma unroll
+      for (int u = 0; u < BCH; ++u) {
+        if (u < cnt) {
+          const int i = i0 + u;
+          xv[u] = x[at(i)];
+          dv[u] = dd[at(i)];
+          uv[u] = i < n - 1 ? du[at(i)] : 0.0;
+          u2v[u] = i < n - 2 ? du2[at(i)] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = BCH - 1; u >= 0; --u) {
+        if (u < cnt) {
+          const double v = (xv[u] - uv[u] * xn1 - u2v[u] * xn2) / dv[u];
+          xv[u] = v;
+          xn2 = xn1;
+          xn1 = v;
+          amax = fmax(amax, fabs(v));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < BCH; ++u)
+        if (u < cnt) x[at(i0 + u)] = xv[u];
     }
-    // rescale to avoid overflow on the next solve
-    const double s = amax > 0.0 ? 1.0 / amax : 1.0;
+    // rescale (and normalise on the last iteration)
+    const double sc = amax > 0.0 ? 1.0 / amax : 1.0;
     double nrm = 0.0;
-    for (int i = 0; i < n; ++i) {
-      const double v = x[at(i)] * s;
-      x[at(i)] = v;
-      nrm += v * v;
+    for (int i0 = 0; i0 < n; i0 += BCH) {
+      double xv[BCH];
+#pragma unroll
+      for (int u = 0; u < BCH; ++u)
+        if (i0 + u < n) xv[u] = x[at(i0 + u)] * sc;
+#pragma unroll
+      for (int u = 0; u < BCH; ++u)
+        if (i0 + u < n) {
+          nrm += xv[u] * xv[u];
+          x[at(i0 + u)] = xv[u];
+        }
     }
     if (it == 2) {
       const double inv = 1.0 / sqrt(nrm);
-      for (int i = 0; i < n; ++i) x[at(i)] *= inv;
+      for (int i0 = 0; i0 < n; i0 += BCH) {
+        double xv[BCH];
+#pragma unroll
+        for (int u = 0; u < BCH; ++u)
+          if (i0 + u < n) xv[u] = x[at(i0 + u)];
+#pragma unroll
+        for (int u = 0; u < BCH; ++u)
+          if (i0 + u < n) x[at(i0 + u)] = xv[u] * inv;
+      }
     }
   }
 }
@@ -611,34 +765,36 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
     TG_HIP(hipFuncSetAttribute((const void *)tri_symv_kernel<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(vsh_bytes)));
   for (int p = 0; p < n; p += NB) {
-    hipLaunchKernelGGL(tri_start_kernel, dim3(NG), dim3(256), 0, st, A, lda, n, p, w);
+    hipLaunchKernelGGL(tri_start_kernel, dim3(std::max(1, tg::cdiv(n - p, 256))), dim3(256), 0, st,
+                       A, lda, n, p, w);
     TG_LAUNCHED();
     if (p >= n - 1) break;  // last column: only d[n-1]
     const int pe = min(p + NB, n - 1);
     for (int i = p; i < pe; ++i) {
       const double len = double(n - i - 1);
       auto tok = tg::prof_begin(st, tg::PROF_TRI_SYMV, 8.0 * len * len, 2.0 * len * len);
+      const int gs = std::max(1, std::min(NG, tg::cdiv(n - i - 1, SYT / 64)));
       if (vlds)
-        hipLaunchKernelGGL(tri_symv_kernel<true>, dim3(NG), dim3(256), vsh_bytes, st, A, lda, n,
+        hipLaunchKernelGGL(tri_symv_kernel<true>, dim3(gs), dim3(SYT), vsh_bytes, st, A, lda, n,
                            i, p, w);
       else
-        hipLaunchKernelGGL(tri_symv_kernel<false>, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, w);
+        hipLaunchKernelGGL(tri_symv_kernel<false>, dim3(gs), dim3(SYT), 0, st, A, lda, n, i, p, w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
       const int do_next = (i + 1 < p + NB) ? 1 : 0;
-      hipLaunchKernelGGL(tri_fin_kernel, dim3(NG), dim3(256), 0, st, A, lda, n, i, p, do_next, w);
+      hipLaunchKernelGGL(tri_fin_kernel, dim3(std::max(1, tg::cdiv(n - i - 1, 256))), dim3(256), 0,
+                         st, A, lda, n, i, p, do_next, w);
       TG_LAUNCHED();
     }
     const int q = p + NB;
     if (q <= n - 1) {  // trailing rank-2NB update of A[q:, q:]
       const int mt = n - q;
       double *C = A + size_t(q) * lda + q;
-      const double *Vb = w.V + size_t(q) * n + p;
-      const double *Wb = w.W + size_t(q) * NB;
-      auto tok = tg::prof_begin(st, tg::PROF_SYR2K, 8.0 * 3.0 * double(mt) * mt,
+      // C -= [V W] [W V]^T : op(A) = ([V^T; W^T])^T, op(B) = [W^T; V^T]
+      auto tok = tg::prof_begin(st, tg::PROF_SYR2K, 8.0 * 2.0 * double(mt) * mt,
                                 4.0 * double(mt) * mt * NB);
-      TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Vb, n, Wb, NB, 1.0, C, lda));
-      TG_HIP(tg::dgemm(st, false, true, mt, mt, NB, -1.0, Wb, NB, Vb, n, 1.0, C, lda));
+      TG_HIP(tg::dgemm(st, true, false, mt, mt, 2 * NB, -1.0, w.PT + q, n,
+                       w.PT + size_t(NB) * n + q, n, 1.0, C, lda));
       tg::prof_end(st, tok);
     }
   }
@@ -648,7 +804,9 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   TG_LAUNCHED();
   const int blocks = tg::cdiv(int64_t(n) * ML, 256);
   const size_t lds = 2 * sizeof(double) * size_t(n);
-  hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.e, n, w.acol);
+  hipLaunchKernelGGL(tri_split_kernel, dim3(1), dim3(64), 0, st, w.e, n, bnd, w.es, w.bs, w.be);
+  TG_LAUNCHED();
+  hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.es, n, w.acol);
   TG_LAUNCHED();
   auto btok = tg::prof_begin(st, tg::PROF_BISECT, 16.0 * n, 0.0);
   if (lds <= 160 * 1024) {
@@ -656,12 +814,15 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
       TG_HIP(hipFuncSetAttribute((const void *)bisect_kernel<true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(bisect_kernel<true>, dim3(blocks), dim3(256), lds, st, w.d, w.acol, n, bnd,
-                       w_asc);
+                       w.bs, w.be, w.wraw);
   } else {
     hipLaunchKernelGGL(bisect_kernel<false>, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
-                       w_asc);
+                       w.bs, w.be, w.wraw);
   }
   tg::prof_end(st, btok);
+  TG_LAUNCHED();
+  hipLaunchKernelGGL(rank_sort_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 2048 * sizeof(double), st,
+                     w.wraw, n, w_asc, w.slot);
   TG_LAUNCHED();
   return 0;
 }
@@ -691,7 +852,7 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   TG_WS(ar);
   const double *bnd = w.scal;
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
-  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.e, n, k, w_asc,
+  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k, w_asc,
                      bnd, w);
   tg::prof_end(st, itok);
   TG_LAUNCHED();

@@ -99,24 +99,36 @@ __device__ inline void argmax_publish(double bv, int bp, int i, int n, PivWs w) 
     vals[1] = double(sp[0]);
   }
   __syncthreads();
-  if (tg::publish_partials(vals, 2, w.part, 2, w.cnt)) {
-    if (tid == 0) {
+  if (tg::publish_partials(vals, 2, w.part, w.cnt)) {
+    if (tid < 64) {  // one wave: lanes cover the partials, fixed butterfly argmax
+      const int G = int(gridDim.x);
       double best = -INFINITY;
       int q = n;
-      for (int g = 0; g < int(gridDim.x); ++g) {
-        const double v = w.part[2 * g];
-        const int p = int(w.part[2 * g + 1]);
+      for (int g = tid; g < G; g += 64) {
+        const double v = w.part[g];
+        const int p = int(w.part[G + g]);
         if (v > best || (v == best && p < q)) {
           best = v;
           q = p;
         }
       }
-      if (q < n && q != i) {
-        const int a = w.perm[i];
-        w.perm[i] = w.perm[q];
-        w.perm[q] = a;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(best, off);
+        const int op = __shfl_xor(q, off);
+        if (ov > best || (ov == best && op < q)) {
+          best = ov;
+          q = op;
+        }
       }
-      *w.cnt = 0u;
+      if (tid == 0) {
+        if (q < n && q != i) {
+          const int a = w.perm[i];
+          w.perm[i] = w.perm[q];
+          w.perm[q] = a;
+        }
+        *w.cnt = 0u;
+      }
     }
   }
 }

@@ -13,11 +13,13 @@
 
 namespace tg {
 
-__device__ inline bool publish_partials(const double *vals, int cnt, double *part, int stride,
+// Partials are stored transposed: part[j * gridDim.x + blockIdx.x].
+__device__ inline bool publish_partials(const double *vals, int cnt, double *part,
                                         unsigned *counter) {
   __shared__ int s_last;
   const int tid = threadIdx.x;
-  for (int j = tid; j < cnt; j += blockDim.x) part[size_t(blockIdx.x) * stride + j] = vals[j];
+  const int G = int(gridDim.x);
+  for (int j = tid; j < cnt; j += blockDim.x) part[size_t(j) * G + blockIdx.x] = vals[j];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -35,16 +37,44 @@ __device__ inline bool publish_partials(const double *vals, int cnt, double *par
   return s_last != 0;
 }
 
-// Sum the published partials (call only in the last workgroup).
-__device__ inline void sum_partials(const double *part, int stride, int cnt, double *out,
-                                    unsigned *counter) {
-  const int tid = threadIdx.x;
-  for (int j = tid; j < cnt; j += blockDim.x) {
-    double s = 0.0;
-    for (int g = 0; g < int(gridDim.x); ++g) s += part[size_t(g) * stride + j];
-    out[j] = s;
+// Sum the published partials (call only in the last workgroup).  Wave w owns
+// values j = w + nw*u (u < 5); its lanes cover partials g = lane + 64*s
+// (s < 4) -- all loads of one batch are issued before any is used.  Each value
+// is summed in a fixed order (per-lane in s, then a fixed butterfly), so the
+// result is bit-reproducible.
+__device__ inline void sum_partials(const double *part, int cnt, double *out, unsigned *counter) {
+  constexpr int MJ = 5, MG = 4;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = int(blockDim.x >> 6);
+  const int G = int(gridDim.x);
+  for (int jb = 0; jb < cnt; jb += nw * MJ) {
+    double acc[MJ];
+#pragma unroll
+    for (int u = 0; u < MJ; ++u) acc[u] = 0.0;
+    for (int gb = 0; gb < G; gb += 64 * MG) {
+      double v[MJ][MG];
+#pragma unroll
+      for (int u = 0; u < MJ; ++u)
+#pragma unroll
+        for (int s = 0; s < MG; ++s) {
+          const int j = jb + wid + nw * u, g = gb + lane + 64 * s;
+          v[u][s] = (j < cnt && g < G) ? part[size_t(j) * G + g] : 0.0;
+        }
+#pragma unroll
+      for (int u = 0; u < MJ; ++u)
+#pragma unroll
+        for (int s = 0; s < MG; ++s) acc[u] += v[u][s];
+    }
+#pragma unroll
+    for (int u = 0; u < MJ; ++u) {
+      double a = acc[u];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+      const int j = jb + wid + nw * u;
+      if (lane == 0 && j < cnt) out[j] = a;
+    }
   }
-  if (tid == 0) *counter = 0u;
+  if (threadIdx.x == 0) *counter = 0u;
 }
 
 // Block-wide sum of one double per thread into LDS slot (all threads get it).
