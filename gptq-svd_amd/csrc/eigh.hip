@@ -232,7 +232,7 @@ __global__ __launch_bounds__(SYT) void tri_symv_kernel(const double *__restrict_
 // W[:, t] = tau (y - V (W^T v) - W (V^T v)) + alpha2 v, then (do_next) update
 // column i+1 with the panel's t+1 reflectors and reduce its |x|^2.  One thread
 // per row; the column-major panel makes every load coalesced.
-__global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__ A, int lda, int n,
+__global__ __launch_bounds__(64) void tri_fin_kernel(const double *__restrict__ A, int lda, int n,
                                                       int i, int p, int do_next, Tri w) {
   __shared__ double q1[NB], q2[NB], vrow[NB], wrow[NB];
   __shared__ double scratch[8];
@@ -300,13 +300,23 @@ __global__ __launch_bounds__(256) void tri_fin_kernel(const double *__restrict__
 // ---------------------------------------------------------------------------
 // 2. eigenvalues of T: Sturm-count multisection
 // ---------------------------------------------------------------------------
+// a / b with v_rcp_f64 + two Newton steps + one residual correction (the
+// sweeps only need a backward-stable quotient, not IEEE rounding)
+__device__ inline double fdiv(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  r = fma(fma(-b, r, 1.0), r, r);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
+
 __device__ inline int sturm_count(const double *__restrict__ d, const double *__restrict__ e2, int n,
                                   double x, double pivmin) {
   double q = d[0] - x;
   if (fabs(q) <= pivmin) q = -pivmin;
   int c = q < 0.0;
   for (int k = 1; k < n; ++k) {
-    q = (d[k] - x) - e2[k - 1] / q;
+    q = (d[k] - x) - fdiv(e2[k - 1], q);
     if (fabs(q) <= pivmin) q = -pivmin;
     c += q < 0.0;
   }
@@ -500,6 +510,8 @@ __device__ inline double hash_unit(uint32_t a, uint32_t b) {
 constexpr int FCH = 32;  // forward-sweep chunk (elements staged in registers)
 constexpr int BCH = 16;  // backward-sweep chunk
 
+
+
 __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
                                                    const double *__restrict__ e, int n, int k,
                                                    const double *__restrict__ w_asc,
@@ -530,14 +542,13 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
       const int cnt = min(FCH, n - 1 - i0);
       double xn[FCH], dn[FCH], en[FCH], enn[FCH];
 #pragma unroll
-      for (int u = 0; u < FCH; ++u) {
-        if (u < cnt) {
-          const int i = i0 + u;
-          xn[u] = x[at(i + 1)];
-          dn[u] = d[i + 1];
-          en[u] = e[i];
-          enn[u] = i + 1 < n - 1 ? e[i + 1] : 0.0;
-        }
+      for (int u = 0; u < FCH; ++u) {  // unconditional (clamped) loads: one batch in flight
+        const int i = min(i0 + u, n - 2);
+        xn[u] = x[at(i + 1)];
+        dn[u] = d[i + 1];
+        en[u] = e[i];
+        enn[u] = e[min(i + 1, n - 1)];
+        if (i + 1 >= n - 1) enn[u] = 0.0;
       }
 #pragma unroll
       for (int u = 0; u < FCH; ++u) {
@@ -547,7 +558,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
           double xi_next;
           if (fabs(cur_d) >= fabs(sub)) {
             const double piv = clampp(cur_d);
-            const double f = sub / piv;
+            const double f = fdiv(sub, piv);
             dd[at(i)] = piv;
             du[at(i)] = cur_u;
             du2[at(i)] = 0.0;
@@ -556,7 +567,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
             cur_d = nd - f * cur_u;
             cur_u = nu;
           } else {
-            const double f = cur_d / sub;
+            const double f = fdiv(cur_d, sub);
             dd[at(i)] = sub;
             du[at(i)] = nd;
             du2[at(i)] = nu;
@@ -577,19 +588,19 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
       const int i0 = max(0, i1 - BCH), cnt = i1 - i0;
       double xv[BCH], dv[BCH], uv[BCH], u2v[BCH];
 #pragma unroll
-      for (int u = 0; u < BCH; ++u) {
-        if (u < cnt) {
-          const int i = i0 + u;
-          xv[u] = x[at(i)];
-          dv[u] = dd[at(i)];
-          uv[u] = i < n - 1 ? du[at(i)] : 0.0;
-          u2v[u] = i < n - 2 ? du2[at(i)] : 0.0;
-        }
+      for (int u = 0; u < BCH; ++u) {  // unconditional (clamped) loads: one batch in flight
+        const int i = min(i0 + u, n - 1);
+        xv[u] = x[at(i)];
+        dv[u] = dd[at(i)];
+        uv[u] = du[at(i)];
+        u2v[u] = du2[at(i)];
+        if (i >= n - 1) uv[u] = 0.0;
+        if (i >= n - 2) u2v[u] = 0.0;
       }
 #pragma unroll
       for (int u = BCH - 1; u >= 0; --u) {
         if (u < cnt) {
-          const double v = (xv[u] - uv[u] * xn1 - u2v[u] * xn2) / dv[u];
+          const double v = fdiv(xv[u] - uv[u] * xn1 - u2v[u] * xn2, dv[u]);
           xv[u] = v;
           xn2 = xn1;
           xn1 = v;
@@ -606,8 +617,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
     for (int i0 = 0; i0 < n; i0 += BCH) {
       double xv[BCH];
 #pragma unroll
-      for (int u = 0; u < BCH; ++u)
-        if (i0 + u < n) xv[u] = x[at(i0 + u)] * sc;
+      for (int u = 0; u < BCH; ++u) xv[u] = x[at(min(i0 + u, n - 1))] * sc;
 #pragma unroll
       for (int u = 0; u < BCH; ++u)
         if (i0 + u < n) {
@@ -620,8 +630,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
       for (int i0 = 0; i0 < n; i0 += BCH) {
         double xv[BCH];
 #pragma unroll
-        for (int u = 0; u < BCH; ++u)
-          if (i0 + u < n) xv[u] = x[at(i0 + u)];
+        for (int u = 0; u < BCH; ++u) xv[u] = x[at(min(i0 + u, n - 1))];
 #pragma unroll
         for (int u = 0; u < BCH; ++u)
           if (i0 + u < n) x[at(i0 + u)] = xv[u] * inv;
@@ -782,7 +791,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
       tg::prof_end(st, tok);
       TG_LAUNCHED();
       const int do_next = (i + 1 < p + NB) ? 1 : 0;
-      hipLaunchKernelGGL(tri_fin_kernel, dim3(std::max(1, tg::cdiv(n - i - 1, 256))), dim3(256), 0,
+      hipLaunchKernelGGL(tri_fin_kernel, dim3(std::max(1, tg::cdiv(n - i - 1, 64))), dim3(64), 0,
                          st, A, lda, n, i, p, do_next, w);
       TG_LAUNCHED();
     }

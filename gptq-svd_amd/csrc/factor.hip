@@ -41,8 +41,10 @@ struct PivWs {
   double *Hk;    // n x n  H_k, then its Schur complements
   double *dsc;   // n      Schur diagonal (by original index)
   double *L;     // n x k  L[r][i] (original row index r, pivot step i)
-  double *part;  // PGMAX x 2
+  double *LT;    // PB x n current panel of L, column-major (coalesced per step)
+  double *part;  // 2 x PGMAX
   int32_t *perm; // n      position -> original index
+  int32_t *pos;  // n      original index -> position
   unsigned *cnt;
 };
 
@@ -59,8 +61,10 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.Hk, size_t(n) * n);
   take(q.dsc, n);
   take(q.L, size_t(n) * k);
+  take(q.LT, size_t(PB) * n);
   take(q.part, PGMAX * 2);
   take(q.perm, n);
+  take(q.pos, n);
   take(q.cnt, 16);
 }
 
@@ -123,9 +127,11 @@ __device__ inline void argmax_publish(double bv, int bp, int i, int n, PivWs w) 
       }
       if (tid == 0) {
         if (q < n && q != i) {
-          const int a = w.perm[i];
-          w.perm[i] = w.perm[q];
+          const int a = w.perm[i], b = w.perm[q];
+          w.perm[i] = b;
           w.perm[q] = a;
+          w.pos[b] = i;
+          w.pos[a] = q;
         }
         *w.cnt = 0u;
       }
@@ -141,6 +147,7 @@ __global__ __launch_bounds__(256) void piv_init_kernel(int n, PivWs w) {
     const double v = w.Hk[size_t(j) * n + j];
     w.dsc[j] = v;
     w.perm[j] = j;
+    w.pos[j] = j;
     if (v > bv || (v == bv && j < bp)) {
       bv = v;
       bp = j;
@@ -149,31 +156,43 @@ __global__ __launch_bounds__(256) void piv_init_kernel(int n, PivWs w) {
   argmax_publish(bv, bp, 0, n, w);
 }
 
-// One pivot step i (pivot already swapped into position i).
+// One pivot step i (pivot already swapped into position i).  Threads walk the
+// rows in ORIGINAL order (coalesced row of H_k, panel of L^T, Schur diagonal);
+// rows already pivoted (pos <= i) are skipped; the argmax breaks ties on the
+// dgeqp3 position.
 __global__ __launch_bounds__(256) void piv_step_kernel(int n, int k, int i, int ps, PivWs w) {
   __shared__ double lp[PB];
   const int t = i - ps;
   const int piv = w.perm[i];
   const double dpiv = w.dsc[piv];
   const double ljj = sqrt(fmax(dpiv, 0.0));
-  if (threadIdx.x < t) lp[threadIdx.x] = w.L[size_t(piv) * k + ps + threadIdx.x];
+  if (threadIdx.x < t) lp[threadIdx.x] = w.LT[size_t(threadIdx.x) * n + piv];
   __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.L[size_t(piv) * k + i] = ljj;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.L[size_t(piv) * k + i] = ljj;
+    w.LT[size_t(t) * n + piv] = ljj;
+  }
   const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
   double bv = -INFINITY;
   int bp = n;
-  for (int j = i + 1 + blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const int r = w.perm[j];
-    double v = w.Hk[size_t(piv) * n + r];
-    const double *lr = w.L + size_t(r) * k + ps;
-    for (int l = 0; l < t; ++l) v -= lr[l] * lp[l];
+  const double *hrow = w.Hk + size_t(piv) * n;
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const int pr = w.pos[r];
+    double v = hrow[r];
+    double lr[PB];
+#pragma unroll
+    for (int l = 0; l < PB; ++l) lr[l] = l < t ? w.LT[size_t(l) * n + r] : 0.0;
+#pragma unroll
+    for (int l = 0; l < PB; ++l) v -= l < t ? lr[l] * lp[l] : 0.0;
+    if (pr <= i) continue;
     const double lv = v * inv;
     w.L[size_t(r) * k + i] = lv;
+    w.LT[size_t(t) * n + r] = lv;
     const double dn = w.dsc[r] - lv * lv;
     w.dsc[r] = dn;
-    if (dn > bv || (dn == bv && j < bp)) {
+    if (dn > bv || (dn == bv && pr < bp)) {
       bv = dn;
-      bp = j;
+      bp = pr;
     }
   }
   // dgeqp3 stops after min(k, n) steps: no swap into position k.
@@ -289,6 +308,7 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
   piv_layout(ar, n, k, &w);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
+  TG_HIP(hipMemsetAsync(w.LT, 0, sizeof(double) * PB * size_t(n), st));
   hipLaunchKernelGGL(scale_rows_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
                      dim3(256), 0, st, Vh, ldv, S, n, k, w.B);
   TG_LAUNCHED();
@@ -299,14 +319,14 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
   for (int ps = 0; ps < k; ps += PB) {
     const int pe = std::min(ps + PB, k);
     for (int i = ps; i < pe; ++i) {
-      const int g = std::max(1, std::min(PGMAX, tg::cdiv(n - i - 1, 256)));
+      const int g = std::max(1, std::min(PGMAX, tg::cdiv(n, 256)));
       auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n - i) * (i - ps + 3), 0.0);
       hipLaunchKernelGGL(piv_step_kernel, dim3(g), dim3(256), 0, st, n, k, i, ps, w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
     }
     if (pe < k)  // Schur update with this panel's columns (all rows, original order)
-      TG_HIP(tg::dsyrk_nt(st, n, pe - ps, -1.0, w.L + ps, k, 1.0, w.Hk, n));
+      TG_HIP(tg::dsyrk_tn(st, n, pe - ps, -1.0, w.LT, n, 1.0, w.Hk, n));
   }
   hipLaunchKernelGGL(rx_gather_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
                      dim3(256), 0, st, n, k, w, Rx, ldr, perm);
