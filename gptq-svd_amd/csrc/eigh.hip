@@ -138,6 +138,22 @@ __global__ __launch_bounds__(SYT) void tri_symv_kernel(const double *__restrict_
   const int t = i - p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const double *VT = w.PT, *WT = w.PT + size_t(NB) * n;
+  const int c_lo = (i + 1) & ~1;
+  const bool vec = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const int len2 = (n - c_lo) >> 1;  // double2 count
+  const int TW = gridDim.x * (SYT / 64);
+  const int r_first = i + 1 + blockIdx.x * (SYT / 64) + wid;
+  // row data does not depend on the reflector: put the first batch in flight now
+  double2 pre[8];
+  const bool have_pre = VLDS && vec && r_first < n;
+  if (have_pre) {
+    const double2 *r2 = reinterpret_cast<const double2 *>(A + size_t(r_first) * lda + c_lo);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = lane + u * 64;
+      pre[u] = r2[c < len2 ? c : 0];
+    }
+  }
   // dlarfg (LAPACK): beta = -sign(alpha) * hypot(alpha, |x|), tau = (beta-alpha)/beta,
   // v = [1, x / (alpha - beta)]
   const double xn2 = w.red[0];
@@ -148,7 +164,6 @@ __global__ __launch_bounds__(SYT) void tri_symv_kernel(const double *__restrict_
     tau = (beta - alpha) / beta;
     scal = 1.0 / (alpha - beta);
   }
-  const int c_lo = (i + 1) & ~1;
   auto vval = [&](int c) -> double {
     return c < i + 1 ? 0.0 : (c == i + 1 ? 1.0 : w.acol[c] * scal);
   };
@@ -161,18 +176,27 @@ __global__ __launch_bounds__(SYT) void tri_symv_kernel(const double *__restrict_
   for (int j = tid; j < (SYT / 64) * PST; j += blockDim.x) (&wpart[0][0])[j] = 0.0;
   __syncthreads();
 
-  const bool vec = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-  const int len2 = (n - c_lo) >> 1;  // double2 count
   const int tail = (n - c_lo) & 1;
   double q1 = 0.0, q2 = 0.0, sv = 0.0;  // per-lane partials (lane l -> panel column l)
-  const int TW = gridDim.x * (SYT / 64);
-  for (int r = i + 1 + blockIdx.x * (SYT / 64) + wid; r < n; r += TW) {
+  for (int r = r_first; r < n; r += TW) {
     const double *row = A + size_t(r) * lda + c_lo;
     double a0 = 0.0, a1 = 0.0;
     if (VLDS && vec) {
       const double2 *r2 = reinterpret_cast<const double2 *>(row);
       const double2 *v2 = reinterpret_cast<const double2 *>(vsh + c_lo);
       int c = lane;
+      if (r == r_first) {  // consume the prefetched batch
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int cc = lane + u * 64;
+          if (cc < len2) {
+            const double2 vv = v2[cc];
+            a0 += pre[u].x * vv.x;
+            a1 += pre[u].y * vv.y;
+          }
+        }
+        c = lane + 8 * 64;
+      }
       for (; c + 7 * 64 < len2; c += 8 * 64) {
         double2 x[8];
 #pragma unroll
@@ -241,6 +265,17 @@ __global__ __launch_bounds__(64) void tri_fin_kernel(const double *__restrict__ 
   const int tid = threadIdx.x;
   const double *VT = w.PT;
   double *WT = w.PT + size_t(NB) * n;
+  // the thread's first row: its panel rows do not depend on the reductions
+  const int r_first = j + blockIdx.x * blockDim.x + tid;
+  double vr_[NB], wr_[NB];
+  {
+    const int rr = r_first < n ? r_first : n - 1;
+#pragma unroll
+    for (int l = 0; l < NB; ++l) {
+      vr_[l] = VT[size_t(l) * n + rr];
+      wr_[l] = WT[size_t(l) * n + rr];
+    }
+  }
   const double tau = w.tau[i];
   if (tid < NB) {
     q1[tid] = tid < t ? w.red[1 + tid] : 0.0;
@@ -261,12 +296,13 @@ __global__ __launch_bounds__(64) void tri_fin_kernel(const double *__restrict__ 
   }
   __syncthreads();
   double s = 0.0;
-  for (int r = j + blockIdx.x * blockDim.x + tid; r < n; r += gridDim.x * blockDim.x) {
-    double vr_[NB], wr_[NB];
+  for (int r = r_first; r < n; r += gridDim.x * blockDim.x) {
+    if (r != r_first) {
 #pragma unroll
-    for (int l = 0; l < NB; ++l) {
-      vr_[l] = VT[size_t(l) * n + r];
-      wr_[l] = WT[size_t(l) * n + r];
+      for (int l = 0; l < NB; ++l) {
+        vr_[l] = VT[size_t(l) * n + r];
+        wr_[l] = WT[size_t(l) * n + r];
+      }
     }
     double acc = w.y[r];
 #pragma unroll

@@ -109,8 +109,8 @@ __device__ inline void argmax_publish(double bv, int bp, int i, int n, PivWs w) 
       double best = -INFINITY;
       int q = n;
       for (int g = tid; g < G; g += 64) {
-        const double v = w.part[g];
-        const int p = int(w.part[G + g]);
+        const double v = tg::load_partial(&w.part[g]);
+        const int p = int(tg::load_partial(&w.part[G + g]));
         if (v > best || (v == best && p < q)) {
           best = v;
           q = p;

@@ -21,4 +21,17 @@ hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X,
                     double beta, double *C, int64_t ldc);  // C = a X^T X + b C, X: K x n
 hipError_t dsyrk_nt(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc);  // C = a X X^T + b C, X: n x K
+// Chunked (grouped) GEMM over z = 0..nc-1.  Chunk z covers rows
+// [kb, ke) of a length-m axis: kb = z*c, ke = (z == nc-1) ? m : kb + c.
+// Per z:  C_z = alpha * op(A_z) op(B_z) + beta * C_z  with
+//   X_z = X + kb * x_kb + z * x_z  (X in {A, B, C}),
+//   M/N/K = fixed value, or (when < 0) the chunk length ke - kb.
+struct ChunkSpec {
+  int c, nc, m;
+  int64_t a_kb, a_z, b_kb, b_z, c_kb, c_z;
+  int M, N, K;
+};
+hipError_t dgemm_chunked(hipStream_t st, bool transA, bool transB, const ChunkSpec &cs,
+                         double alpha, const double *A, int64_t lda, const double *B,
+                         int64_t ldb, double beta, double *C, int64_t ldc);
 }  // namespace tg

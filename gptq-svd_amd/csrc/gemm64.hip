@@ -135,6 +135,70 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
       }
 }
 
+// Chunked variant: blockIdx.z = chunk; offsets/dims from ChunkSpec.
+template <int BM, int BN, bool TA, bool TB>
+__global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, double alpha,
+                                                            const double *__restrict__ A,
+                                                            int64_t lda,
+                                                            const double *__restrict__ B,
+                                                            int64_t ldb, double beta,
+                                                            double *__restrict__ C,
+                                                            int64_t ldc) {
+  __shared__ double As[KC][BM + PAD];
+  __shared__ double Bs[KC][BN + PAD];
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  const int z = blockIdx.z;
+  const int kb = z * cs.c;
+  const int ke = (z == cs.nc - 1) ? cs.m : kb + cs.c;
+  const int h = ke - kb;
+  const int M = cs.M < 0 ? h : cs.M, N = cs.N < 0 ? h : cs.N, K = cs.K < 0 ? h : cs.K;
+  const int tm = blockIdx.y * BM, tn = blockIdx.x * BN;
+  if (tm >= M || tn >= N) return;
+  A += int64_t(kb) * cs.a_kb + int64_t(z) * cs.a_z;
+  B += int64_t(kb) * cs.b_kb + int64_t(z) * cs.b_z;
+  C += int64_t(kb) * cs.c_kb + int64_t(z) * cs.c_z;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  doublex4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    stage<double, BM, TA>(A, lda, M, K, tm, k0, As);
+    stage<double, BN, !TB>(B, ldb, N, K, tn, k0, Bs);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      double af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
+        const int gj = tn + wn * WN + j * 16 + (lane & 15);
+        if (gi < M && gj < N) {
+          double *p = C + int64_t(gi) * ldc + gj;
+          *p = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *p;
+        }
+      }
+}
+
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>
 hipError_t launch(hipStream_t st, int M, int N, int K, double alpha, const TA_ *A, int64_t lda,
                   const TB_ *B, int64_t ldb, double beta, double *C, int64_t ldc, int splits,
@@ -201,6 +265,33 @@ hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double a
   return dispatch_t<double, double, 64, 64>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C,
                                             ldc);
 }
+hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, double alpha,
+                         const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                         double *C, int64_t ldc) {
+  if (cs.nc <= 0) return hipSuccess;
+  const int hmax = std::max(cs.c, cs.m - (cs.nc - 1) * cs.c);
+  const int M = cs.M < 0 ? hmax : cs.M, N = cs.N < 0 ? hmax : cs.N;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const bool big = int64_t(cdiv(M, 128)) * cdiv(N, 128) * cs.nc >= 256;
+#define TG_CH(BM_, TA_, TB_)                                                                   \
+  hipLaunchKernelGGL((dgemm_chunked_kernel<BM_, BM_, TA_, TB_>),                              \
+                     dim3(cdiv(N, BM_), cdiv(M, BM_), cs.nc), dim3(256), 0, st, cs, alpha, A, \
+                     lda, B, ldb, beta, C, ldc)
+  if (big) {
+    if (!ta && !tb) TG_CH(128, false, false);
+    else if (!ta && tb) TG_CH(128, false, true);
+    else if (ta && !tb) TG_CH(128, true, false);
+    else TG_CH(128, true, true);
+  } else {
+    if (!ta && !tb) TG_CH(64, false, false);
+    else if (!ta && tb) TG_CH(64, false, true);
+    else if (ta && !tb) TG_CH(64, true, false);
+    else TG_CH(64, true, true);
+  }
+#undef TG_CH
+  return hipGetLastError();
+}
+
 size_t dgemm_splitk_scratch(int M, int N, int splits) {
   return sizeof(double) * size_t(M) * size_t(N) * size_t(splits);
 }
