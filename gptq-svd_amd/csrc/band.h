@@ -1,0 +1,74 @@
+// Stage 1 of the two-stage symmetric eigensolver: full -> band reduction
+// (sy2sb) with TSQR panel factorisations, and its back-transformation.
+#pragma once
+#include <type_traits>
+#include <vector>
+
+#include "common.h"
+
+namespace tg {
+
+constexpr int SB_B = 32;    // half-bandwidth of the band matrix (= panel width)
+constexpr int SB_C = 256;   // TSQR leaf height (last leaf of a level absorbs < SB_C rows)
+constexpr int SB_LV = 6;    // max TSQR levels
+
+// One TSQR level of one panel: `rows` stacked rows split in `nc` chunks.
+struct SbLevel {
+  int rows, nc;
+  size_t yoff, toff;  // offsets of this level's Y (rows x 32) and T (nc x 32 x 32)
+};
+struct SbPanel {
+  int p, r0, m, nl;
+  SbLevel L[SB_LV];
+};
+
+struct SbPlan {
+  std::vector<SbPanel> panels;
+  size_t ytotal = 0, ttotal = 0;
+  int ncmax = 1;
+  explicit SbPlan(int n);
+};
+
+// Device buffers (carved by the caller from the eigensolver workspace).
+struct SbBufs {
+  double *Y, *T;          // reflector storage for all panels (persist until back-transform)
+  double *YT, *X, *G, *M; // per-panel temporaries
+  double *R[2];           // TSQR R stacks (ping-pong between levels)
+  double *Gr, *U;         // gathered rows / symmetric update (ncmax*32 x n)
+  double *Xs;             // gathered rows of X (ncmax*32 x ncmax*32)
+  double *Zg, *P, *Mz;    // back-transformation temporaries (ncmax*32 x k)
+};
+
+template <class A>
+void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
+  SbBufs d{};
+  SbBufs &b = bp ? *bp : d;
+  const size_t w = size_t(pl.ncmax) * SB_B;
+  auto take = [&](double *&dst, size_t cnt) {
+    if constexpr (std::is_same_v<A, Arena>) dst = ar.template take<double>(cnt);
+    else ar.template take<double>(cnt);
+  };
+  take(b.Y, pl.ytotal + 1);
+  take(b.T, pl.ttotal + 1);
+  take(b.YT, size_t(n) * SB_B);
+  take(b.X, size_t(n) * w);
+  take(b.G, w * w);
+  take(b.M, w * w);
+  take(b.R[0], w * SB_B);
+  take(b.R[1], w * SB_B);
+  take(b.Gr, w * n);
+  take(b.U, w * n);
+  take(b.Xs, w * w);
+  take(b.Zg, w * kmax);
+  take(b.P, w * kmax);
+  take(b.Mz, w * kmax);
+}
+
+// A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth
+// SB_B in place (full storage, zeros outside the band); reflectors in bufs.
+hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b);
+// Z (n x k row-major) <- Q1 Z.
+hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
+                       const SbBufs &b);
+
+}  // namespace tg

@@ -1,0 +1,684 @@
+// Stage 1 of the two-stage eigensolver: dense symmetric -> band (sy2sb).
+//
+// Replaces the first half of the reduction inside `torch.linalg.eigh`
+// (/root/reference/src/TruncGPTQ/gptq_utils.py:92).  The one-stage dlatrd
+// reduction (eigh.hip) streams the trailing matrix once per column with two
+// grid-wide reductions each; here every panel of SB_B = 32 columns is
+// factorised once and applied with GEMM-shaped FP64 MFMA work:
+//
+//   panel P = A[r0:, p:p+32]  (m = n - r0 rows)
+//   TSQR:  level 0 = Householder QR of each leaf of SB_C rows (one workgroup
+//          per leaf, the leaf in LDS), level l+1 = QR of the stacked R factors
+//          of level l, until one R remains.  Q = D_0 E_1 E_2 ... with D_0
+//          block-diagonal over the leaves and E_l embedded on the rows that
+//          carry level l's stacked R's.
+//   A22 <- Q^T A22 Q, one level at a time, each as the compact-WY two-sided
+//          update  X = A22 Y T,  W = X - 1/2 Y T^T Y^T X,  A22 -= Y W^T + W Y^T
+//          with Y block-diagonal (chunked grouped GEMMs, gemm64.hip) and the
+//          rank-64-per-tile symmetric update on lower tiles, mirrored, so A22
+//          stays bitwise symmetric.
+//   A[r0:, p:p+32] <- [R; 0]  (and its transpose).
+//
+// The reflectors (Y, T of every level of every panel) stay in the workspace
+// for the back-transformation Z <- Q1 Z of the eigenvectors.
+#include <algorithm>
+#include <cmath>
+#include <utility>
+
+#include "band.h"
+#include "gemm64.h"
+#include "reduce.h"
+
+namespace tg {
+
+SbPlan::SbPlan(int n) {
+  ncmax = std::max(1, n / SB_C);
+  int p = 0;
+  while (p + SB_B < n - 1) {
+    SbPanel P{};
+    P.p = p;
+    P.r0 = p + SB_B;
+    P.m = n - P.r0;
+    int rows = P.m, l = 0;
+    while (true) {
+      SbLevel &L = P.L[l];
+      L.rows = rows;
+      L.nc = std::max(1, rows / SB_C);
+      L.yoff = ytotal;
+      L.toff = ttotal;
+      ytotal += size_t(rows) * SB_B;
+      ttotal += size_t(L.nc) * SB_B * SB_B;
+      ++l;
+      if (L.nc == 1) break;
+      rows = L.nc * SB_B;
+    }
+    P.nl = l;
+    panels.push_back(P);
+    p += SB_B;
+  }
+}
+
+}  // namespace tg
+
+namespace {
+
+using tg::SB_B;
+using tg::SB_C;
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+// Row map of TSQR level lv: stacked row s of level lv -> row of level 0.
+struct RowMap {
+  int lv;
+  int nc[tg::SB_LV];  // chunks of each level
+  __device__ int fwd(int s) const {
+    for (int l = lv; l >= 1; --l) s = (s / SB_B) * SB_C + s % SB_B;
+    return s;
+  }
+  __device__ int inv(int r) const {  // -1 if level-0 row r is not in the level's set
+    for (int l = 1; l <= lv; ++l) {
+      const int I = r / SB_C, o = r % SB_C;
+      if (o >= SB_B || I >= nc[l - 1]) return -1;
+      r = I * SB_B + o;
+    }
+    return r;
+  }
+};
+
+// Cross-lane exchange without the LDS crossbar: partner value of `x` for
+// the pairings lane^32, lane^16 (v_permlane{32,16}_swap), lane^15 (DPP
+// row_mirror), lane^7 (row_half_mirror), lane^3, lane^1 (quad_perm).
+// Each pairing flips a new bit (32, 16, 8 via 15, 4 via 7, 2 via 3, 1), so a
+// butterfly over them in this order is a full reduction / reduce-scatter.
+__device__ inline double xchg32(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = (threadIdx.x & 32) != 0;
+  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+}
+__device__ inline double xchg16(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool up = (threadIdx.x & 16) != 0;
+  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+}
+template <int CTRL>
+__device__ inline double xdpp(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int DPP_MIRROR = 0x140, DPP_HALF_MIRROR = 0x141, DPP_XOR3 = 0x1B, DPP_XOR1 = 0xB1;
+
+__device__ inline double wave_allsum(double s) {
+  s += xchg32(s);
+  s += xchg16(s);
+  s += xdpp<DPP_MIRROR>(s);
+  s += xdpp<DPP_HALF_MIRROR>(s);
+  s += xdpp<DPP_XOR3>(s);
+  s += xdpp<DPP_XOR1>(s);
+  return s;
+}
+
+// Reduce-scatter of the 32 products v * r[l] over the wave: lane ends with
+// the sum of column rs_col(lane) (bits 5..1 of the lane id pick the half kept
+// at each step).
+__device__ inline int rs_col(int lane) {
+  return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
+         ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
+}
+// q_l = v0 r0[l] + v1 r1[l] (0 for l == J), formed inside the first step.
+template <int J>
+__device__ inline double reduce_scatter32(const double (&r0)[32], const double (&r1)[32],
+                                          double v0, double v1, int lane) {
+  auto qf = [&](int l) { return l == J ? 0.0 : v0 * r0[l] + v1 * r1[l]; };
+  double p[16];
+  {
+    const bool up = (lane & 32) != 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const double recv = xchg32(up ? qf(k) : qf(k + 16));
+      p[k] = (up ? qf(k + 16) : qf(k)) + recv;
+    }
+  }
+  {
+    const bool up = (lane & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double recv = xchg16(up ? p[k] : p[k + 8]);
+      p[k] = (up ? p[k + 8] : p[k]) + recv;
+    }
+  }
+  {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double recv = xdpp<DPP_MIRROR>(up ? p[k] : p[k + 4]);
+      p[k] = (up ? p[k + 4] : p[k]) + recv;
+    }
+  }
+  {
+    const bool up = (lane & 4) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const double recv = xdpp<DPP_HALF_MIRROR>(up ? p[k] : p[k + 2]);
+      p[k] = (up ? p[k + 2] : p[k]) + recv;
+    }
+  }
+  {
+    const bool up = (lane & 2) != 0;
+    const double recv = xdpp<DPP_XOR3>(up ? p[0] : p[1]);
+    p[0] = (up ? p[1] : p[0]) + recv;
+  }
+  return p[0] + xdpp<DPP_XOR1>(p[0]);
+}
+
+// Householder QR of one leaf (chunk z of `m` rows, rows kb..ke of src, 32
+// columns, row stride ld).  Thread t holds rows t and t + 256 in registers
+// (rows >= h are zero, so every leaf runs exactly 32 steps: a zero
+// subcolumn gives tau = 0).  Outputs (chunk layout, row-major, stride 32):
+// Y rows kb..ke (unit lower trapezoid), YT = Y T, T[z] (dlarft
+// forward/columnwise: H_0 H_1 ... = I - Y T Y^T), R[z] (32x32 upper).
+// Per column one scalar and one 32-wide reduction; the latter gives both
+// w = v^T P (trailing columns) and Y^T v (the new T column), and thread a of
+// wave 0 extends row a of T in registers: T[a][j] = -tau_j sum_c T[a][c] q_c.
+constexpr int QT = 256;
+__global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ src, int64_t ld,
+                                                     int c, int nc, int m,
+                                                     double *__restrict__ Yo,
+                                                     double *__restrict__ To,
+                                                     double *__restrict__ Ro,
+                                                     double *__restrict__ YTo) {
+  __shared__ double prow[SB_B];
+  __shared__ double nrm[QT / 64];
+  __shared__ double red[QT / 64][SB_B];
+  __shared__ double qv[SB_B];
+  __shared__ double Ts[SB_B][SB_B + 1];
+  const int z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kb = z * c, ke = (z == nc - 1) ? m : kb + c, h = ke - kb;
+  double r0[SB_B], r1[SB_B];
+  auto load_row = [&](int i, double(&r)[SB_B]) {
+    if (i < h) {
+      const double *p = src + int64_t(kb + i) * ld;
+#pragma unroll
+      for (int l = 0; l < SB_B; ++l) r[l] = p[l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < SB_B; ++l) r[l] = 0.0;
+    }
+  };
+  load_row(tid, r0);
+  load_row(tid + QT, r1);
+  for (int idx = tid; idx < SB_B * (SB_B + 1); idx += QT) (&Ts[0][0])[idx] = 0.0;
+  const int mycol = rs_col(lane);
+  auto step = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const double x0 = r0[j], x1 = r1[j];
+    if (tid == j) {
+#pragma unroll
+      for (int l = 0; l < SB_B; ++l) prow[l] = r0[l];
+    }
+    const double s_w = wave_allsum(((tid > j) ? x0 * x0 : 0.0) + x1 * x1);
+    if (lane == 0) nrm[wid] = s_w;
+    __syncthreads();
+    const double s = (nrm[0] + nrm[1]) + (nrm[2] + nrm[3]);
+    const double alpha = prow[j];
+    double tau = 0.0, scal = 0.0, beta = alpha;
+    if (s != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + s), alpha);
+      tau = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    const double v0 = (tid > j) ? x0 * scal : (tid == j ? 1.0 : 0.0);
+    const double v1 = x1 * scal;
+    // q_l = sum_i v_i P[i][l]: l > j -> w_l, l < j -> (Y^T v)_l
+    const double q = reduce_scatter32<j>(r0, r1, v0, v1, lane);
+    if ((lane & 1) == 0) red[wid][mycol] = q;
+    __syncthreads();
+    if (tid < SB_B) qv[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    __syncthreads();
+    const double tv0 = tau * v0, tv1 = tau * v1;
+#pragma unroll
+    for (int l = j + 1; l < SB_B; ++l) {
+      const double w = qv[l];
+      r0[l] -= tv0 * w;
+      r1[l] -= tv1 * w;
+    }
+    r0[j] = (tid > j) ? v0 : (tid == j ? beta : r0[j]);
+    r1[j] = v1;
+    if (tid < j) {  // row tid of T: T[tid][j] = -tau sum_c T[tid][c] q_c (T[tid][c<tid] = 0)
+      double a = 0.0;
+#pragma unroll
+      for (int cc = 0; cc < j; ++cc) a += Ts[tid][cc] * qv[cc];
+      Ts[tid][j] = -tau * a;
+    }
+    if (tid == j) Ts[j][j] = tau;
+  };
+  [&]<int... J>(std::integer_sequence<int, J...>) {
+    (step(std::integral_constant<int, J>{}), ...);
+  }(std::make_integer_sequence<int, SB_B>{});
+  if (tid < SB_B) {
+    double *ro = Ro + size_t(z) * SB_B * SB_B + tid * SB_B;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) ro[l] = (l >= tid) ? r0[l] : 0.0;
+  }
+  __syncthreads();
+  auto emit = [&](int i, double(&r)[SB_B]) {
+    if (i >= h) return;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) r[l] = (i == l) ? 1.0 : (i > l ? r[l] : 0.0);  // Y row
+    double *yo = Yo + int64_t(kb + i) * SB_B;
+    double *yt = YTo + int64_t(kb + i) * SB_B;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) yo[l] = r[l];
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) {
+      double a = 0.0;
+#pragma unroll
+      for (int a2 = 0; a2 <= l; ++a2) a += r[a2] * Ts[a2][l];
+      yt[l] = a;
+    }
+  };
+  emit(tid, r0);
+  emit(tid + QT, r1);
+  for (int idx = tid; idx < SB_B * SB_B; idx += QT)
+    To[size_t(z) * SB_B * SB_B + idx] = Ts[idx >> 5][idx & 31];
+}
+
+hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int m, double *Y,
+                     double *T, double *R, double *YT) {
+  const int hmax = (nc == 1) ? m : std::max(SB_C, m - (nc - 1) * SB_C);
+  if (hmax > 2 * QT) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tsqr_qr_kernel, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T, R,
+                     YT);
+  return hipGetLastError();
+}
+
+// Per (column block J of 32, chunk I): P = Y_I^T Z[chunk rows, J cols]
+// (32 x 32) on FP64 MFMA, then
+//   MODE 0: M[I-block rows, J-block cols] = T_I^T P            (two-sided update)
+//   MODE 1: Z[chunk rows, J cols] -= Y_I (T_I P)                (back-transform Q Z)
+// 8 waves, wave w owns chunk rows 64w..64w+63 (chunks hold < 512 rows) as
+// eight 16x16 C-layout fragments; since the f64 MFMA C/D layout (lane l,
+// reg q -> row (l>>4)+4q, col l&15) equals the B-operand layout for four
+// consecutive K-steps, the same registers are the B operand of P = Y^T Z and
+// the accumulator of Z -= Y (T P).  GATHER: stacked row s lives at Z row
+// map(s) (TSQR levels >= 1).
+template <int MODE, bool GATHER>
+__global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
+                                                  const double *__restrict__ T,
+                                                  double *__restrict__ Z, int64_t ldz, int ncols,
+                                                  int c, int nc, int rows, RowMap mp,
+                                                  double *__restrict__ M, int64_t ldm) {
+  __shared__ double red[8][SB_B][SB_B + 1];
+  __shared__ double Ps[SB_B][SB_B + 1];
+  __shared__ double Ms[SB_B][SB_B + 1];
+  const int J = blockIdx.x, I = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kb = I * c, ke = (I == nc - 1) ? rows : kb + c;
+  const int h = ke - kb;
+  const int c0 = J * SB_B;
+  const int lr = lane >> 4, lc = lane & 15;
+  doublex4 F[4][2];
+  // load the wave's 64 x 32 slab of Z (zeros outside the chunk / columns)
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      int zr = -1;
+      if (rl < h) zr = GATHER ? mp.fwd(kb + rl) : kb + rl;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col = c0 + cb * 16 + lc;
+        F[rb][cb][q] = (zr >= 0 && col < ncols) ? Z[int64_t(zr) * ldz + col] : 0.0;
+      }
+    }
+  // P_w = Y_w^T Z_w
+  doublex4 Pa[2][2];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + 4 * q + lr;
+      double ya[2];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+        ya[ia] = rl < h ? Y[int64_t(kb + rl) * SB_B + ia * 16 + lc] : 0.0;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][q], Pa[ia][cb], 0, 0, 0);
+    }
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[wid][ia * 16 + lr + 4 * q][cb * 16 + lc] = Pa[ia][cb][q];
+  __syncthreads();
+  for (int idx = tid; idx < SB_B * SB_B; idx += 512) {
+    const int a = idx >> 5, cc = idx & 31;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[w][a][cc];
+    Ps[a][cc] = v;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < SB_B * SB_B; idx += 512)
+    Ms[idx >> 5][idx & 31] = T[size_t(I) * SB_B * SB_B + idx];
+  __syncthreads();
+  double mval[2];
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 512, ++t) {
+    const int a = idx >> 5, cc = idx & 31;
+    double v = 0.0;
+    if (MODE == 0) {
+      for (int e = 0; e <= a; ++e) v += Ms[e][a] * Ps[e][cc];
+      if (c0 + cc < ldm) M[int64_t(I * SB_B + a) * ldm + c0 + cc] = v;
+    } else {
+      for (int e = a; e < SB_B; ++e) v += Ms[a][e] * Ps[e][cc];
+      mval[t] = v;
+    }
+  }
+  if (MODE == 0) return;
+  __syncthreads();  // T no longer read: Ms <- T P
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 512, ++t) Ms[idx >> 5][idx & 31] = mval[t];
+  __syncthreads();
+  // Z_w -= Y_w Ms
+#pragma unroll
+  for (int k0 = 0; k0 < SB_B; k0 += 4) {
+    double bm[2];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) bm[cb] = Ms[k0 + lr][cb * 16 + lc];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int rl = wid * 64 + rb * 16 + lc;
+      const double ya = rl < h ? -Y[int64_t(kb + rl) * SB_B + k0 + lr] : 0.0;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+        F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm[cb], F[rb][cb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      if (rl >= h) continue;
+      const int zr = GATHER ? mp.fwd(kb + rl) : kb + rl;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col = c0 + cb * 16 + lc;
+        if (col < ncols) Z[int64_t(zr) * ldz + col] = F[rb][cb][q];
+      }
+    }
+}
+
+// A22 -= Yd X^T + X Yd^T - Yd S Yd^T,  S = (M + M^T)/2  (== Yd W^T + W Yd^T
+// with W = X - Yd M / 2).  Yd block-diagonal over chunks of c rows:
+//   (Yd X^T)[r][c'] = sum_l Y[r][l] X[c'][I(r)*32 + l]
+//   (X Yd^T)[r][c'] = sum_l X[r][J(c')*32 + l] Y[c'][l]
+//   (Yd S Yd^T)[r][c'] = (Y[r] S_{I(r)J(c')}) . Y[c']
+// 64x64 lower tiles (c is a multiple of 64: a tile lies in one chunk),
+// K = 96 in three segments, mirrored: A22 stays bitwise symmetric.
+constexpr int S2T = 64, S2K = 16, S2P = 4;
+__global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, int64_t lda, int m,
+                                                       int c, int nc,
+                                                       const double *__restrict__ Y,
+                                                       const double *__restrict__ X,
+                                                       int64_t ldx,
+                                                       const double *__restrict__ M,
+                                                       int64_t ldm) {
+  __shared__ double As[S2K][S2T + S2P];
+  __shared__ double Bs[S2K][S2T + S2P];
+  __shared__ double YS[SB_B][S2T + S2P];   // -(Y_rows S_IJ)^T, k-major
+  __shared__ double Ss[SB_B][SB_B + 1];
+  const int b = blockIdx.x;
+  int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= b) ++I;
+  while (I * (I + 1) / 2 > b) --I;
+  const int J = b - I * (I + 1) / 2;
+  const int tm = I * S2T, tn = J * S2T;
+  const int ci = min(tm / c, nc - 1), cj = min(tn / c, nc - 1);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  // S_IJ and YS = -(Y_rows S_IJ)
+  for (int idx = tid; idx < SB_B * SB_B; idx += 256) {
+    const int x = idx >> 5, y = idx & 31;
+    Ss[x][y] = 0.5 * (M[int64_t(ci * SB_B + x) * ldm + cj * SB_B + y] +
+                      M[int64_t(cj * SB_B + y) * ldm + ci * SB_B + x]);
+  }
+  __syncthreads();
+  {
+    const int i = tid >> 2, b0 = (tid & 3) * 8;  // row i, columns b0..b0+7
+    const int gr = tm + i;
+    double yr[SB_B];
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) yr[l] = gr < m ? Y[int64_t(gr) * SB_B + l] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      double v = 0.0;
+#pragma unroll
+      for (int l = 0; l < SB_B; ++l) v += yr[l] * Ss[l][b0 + q];
+      YS[b0 + q][i] = -v;
+    }
+  }
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  const int sr = tid >> 2, sk = (tid & 3) * 4;
+  for (int k0 = 0; k0 < 3 * SB_B; k0 += S2K) {
+    const int seg = k0 / SB_B;
+    const int kl = (k0 & 31) + sk;
+    if (seg < 2) {
+      const int gr = tm + sr;
+      const double *src = seg ? X + int64_t(gr) * ldx + cj * SB_B + kl : Y + int64_t(gr) * SB_B + kl;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) As[sk + t][sr] = gr < m ? src[t] : 0.0;
+    }
+    {
+      const int gr = tn + sr;
+      const double *src = seg == 0 ? X + int64_t(gr) * ldx + ci * SB_B + kl : Y + int64_t(gr) * SB_B + kl;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) Bs[sk + t][sr] = gr < m ? src[t] : 0.0;
+    }
+    __syncthreads();
+    double(*Ap)[S2T + S2P] = seg < 2 ? As : YS + (k0 & 31);
+#pragma unroll
+    for (int kq = 0; kq < S2K; kq += 4) {
+      double af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = Ap[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bs[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        const int gj = tn + wn * 32 + j * 16 + (lane & 15);
+        if (gi < m && gj < m && gi >= gj) {
+          double *p = A + int64_t(gi) * lda + gj;
+          const double v = *p - acc[i][j][r];
+          *p = v;
+          if (gi != gj) A[int64_t(gj) * lda + gi] = v;
+        }
+      }
+}
+
+// dst[s][:] = src[map(s)][:]
+__global__ void gather_rows_kernel(const double *__restrict__ src, int64_t lds, int ncols, int nrows,
+                                   RowMap mp, double *__restrict__ dst) {
+  const int s = blockIdx.y;
+  const int r = mp.fwd(s);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < ncols; c += gridDim.x * blockDim.x)
+    dst[int64_t(s) * ncols + c] = src[int64_t(r) * lds + c];
+}
+
+// dst[map(s)][:] = src[s][:]
+__global__ void scatter_rows_kernel(const double *__restrict__ src, int ncols, int nrows, RowMap mp,
+                                    double *__restrict__ dst, int64_t ldd) {
+  const int s = blockIdx.y;
+  const int r = mp.fwd(s);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < ncols; c += gridDim.x * blockDim.x)
+    dst[int64_t(r) * ldd + c] = src[int64_t(s) * ncols + c];
+}
+
+// A22 -= Ye U^T... in scattered form: U (nS x m) = Y_l W^T.
+//   z = 0: rows map(s): A[map(s)][c] -= U[s][c] + (c in set ? U[t(c)][map(s)] : 0)
+//   z = 1: rows r not in set, columns map(t): A[r][map(t)] -= U[t][r]
+__global__ void sym_scatter_kernel(double *__restrict__ A, int64_t lda, int m, int nS, RowMap mp,
+                                   const double *__restrict__ U, int pass) {
+  if (pass == 0) {
+    const int s = blockIdx.y;
+    if (s >= nS) return;
+    const int r = mp.fwd(s);
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < m; c += gridDim.x * blockDim.x) {
+      const int t = mp.inv(c);
+      double v = U[int64_t(s) * m + c];
+      if (t >= 0) v = v + U[int64_t(t) * m + r];
+      A[int64_t(r) * lda + c] -= v;
+    }
+  } else {
+    // rows r = blockIdx.x * 64 + (tid & 63), columns t = blockIdx.y*4 + (tid >> 6) ...
+    const int r = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (r >= m || mp.inv(r) >= 0) return;
+    for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < nS; t += gridDim.y * 4)
+      A[int64_t(r) * lda + mp.fwd(t)] -= U[int64_t(t) * m + r];
+  }
+}
+
+// A[r0+i][p+l] = [R; 0] and the transpose (i < m, l < 32).
+__global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, int r0, int m,
+                                   const double *__restrict__ R) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= m * SB_B) return;
+  const int i = idx >> 5, l = idx & 31;
+  const double v = (i < SB_B) ? R[i * SB_B + l] : 0.0;
+  A[int64_t(r0 + i) * lda + p + l] = v;
+  A[int64_t(p + l) * lda + r0 + i] = v;
+}
+
+
+}  // namespace
+
+namespace tg {
+
+#define TG_CHK(x)                     \
+  do {                                \
+    hipError_t e_ = (x);              \
+    if (e_ != hipSuccess) return e_;  \
+  } while (0)
+
+hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b) {
+  for (const SbPanel &P : pl.panels) {
+    const int m = P.m, r0 = P.r0;
+    double *A22 = A + int64_t(r0) * lda + r0;
+    RowMap mp{};
+    for (int l = 0; l < P.nl; ++l) mp.nc[l] = P.L[l].nc;
+    int rb = 0;
+    for (int l = 0; l < P.nl; ++l) {
+      const SbLevel &L = P.L[l];
+      double *Yl = b.Y + L.yoff, *Tl = b.T + L.toff;
+      const int nc = L.nc, rows = L.rows, w = nc * SB_B;
+      if (l == 0)
+        TG_CHK(launch_qr(st, A + int64_t(r0) * lda + P.p, lda, nc, m, Yl, Tl, b.R[rb], b.YT));
+      else
+        TG_CHK(launch_qr(st, b.R[rb ^ 1], SB_B, nc, rows, Yl, Tl, b.R[rb], b.YT));
+      mp.lv = l;
+      if (l == 0) {
+        // X = A22 blockdiag(YT)   (m x w)
+        ChunkSpec cx{SB_C, nc, m, 1, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
+        TG_CHK(dgemm_chunked(st, false, false, cx, 1.0, A22, lda, b.YT, SB_B, 0.0, b.X, w));
+        // M = Td^T Yd^T X  (w x w)
+        hipLaunchKernelGGL((ytz_kernel<0, false>), dim3(nc, nc), dim3(512), 0, st, Yl, Tl, b.X,
+                           int64_t(w), w, SB_C, nc, m, mp, b.M, int64_t(w));
+        TG_CHK(hipGetLastError());
+        const int nt = cdiv(m, S2T);
+        hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                           int64_t(lda), m, SB_C, nc, Yl, b.X, int64_t(w), b.M, int64_t(w));
+        TG_CHK(hipGetLastError());
+      } else {
+        // Gr = A22[S, :]  (rows x m)
+        hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
+                           int64_t(lda), m, rows, mp, b.Gr);
+        TG_CHK(hipGetLastError());
+        // X = Gr^T blockdiag(YT)   (m x w)
+        ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
+        TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, b.YT, SB_B, 0.0, b.X, w));
+        // Xs = X[S, :]  (rows x w)
+        hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(w, 256), rows), dim3(256), 0, st, b.X,
+                           int64_t(w), w, rows, mp, b.Xs);
+        TG_CHK(hipGetLastError());
+        hipLaunchKernelGGL((ytz_kernel<0, false>), dim3(nc, nc), dim3(512), 0, st, Yl, Tl, b.Xs,
+                           int64_t(w), w, SB_C, nc, rows, mp, b.M, int64_t(w));
+        TG_CHK(hipGetLastError());
+        ChunkSpec cw{SB_C, nc, rows, SB_B, 0, 0, int64_t(SB_B) * w, w, 0, -1, w, SB_B};
+        TG_CHK(dgemm_chunked(st, false, false, cw, -0.5, Yl, SB_B, b.M, w, 1.0, b.Xs, w));
+        hipLaunchKernelGGL(scatter_rows_kernel, dim3(cdiv(w, 256), rows), dim3(256), 0, st, b.Xs,
+                           w, rows, mp, b.X, int64_t(w));
+        TG_CHK(hipGetLastError());
+        // U = Y_l W^T  (rows x m)
+        ChunkSpec cu{SB_C, nc, rows, SB_B, 0, 0, SB_B, m, 0, -1, m, SB_B};
+        TG_CHK(dgemm_chunked(st, false, true, cu, 1.0, Yl, SB_B, b.X, w, 0.0, b.U, m));
+        hipLaunchKernelGGL(sym_scatter_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
+                           int64_t(lda), m, rows, mp, b.U, 0);
+        TG_CHK(hipGetLastError());
+        hipLaunchKernelGGL(sym_scatter_kernel, dim3(cdiv(m, 64), std::min(64, cdiv(rows, 4))),
+                           dim3(256), 0, st, A22, int64_t(lda), m, rows, mp, b.U, 1);
+        TG_CHK(hipGetLastError());
+      }
+      rb ^= 1;
+    }
+    hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, st, A,
+                       int64_t(lda), P.p, r0, m, b.R[rb ^ 1]);
+    TG_CHK(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
+                       const SbBufs &b) {
+  (void)n;
+  for (auto it = pl.panels.rbegin(); it != pl.panels.rend(); ++it) {
+    const SbPanel &P = *it;
+    double *Zs = Z + int64_t(P.r0) * k;
+    RowMap mp{};
+    for (int l = 0; l < P.nl; ++l) mp.nc[l] = P.L[l].nc;
+    for (int l = P.nl - 1; l >= 0; --l) {  // Q = D_0 E_1 E_2 ...: top level first
+      const SbLevel &L = P.L[l];
+      mp.lv = l;
+      if (l > 0)
+        hipLaunchKernelGGL((ytz_kernel<1, true>), dim3(cdiv(k, SB_B), L.nc), dim3(512), 0, st,
+                           b.Y + L.yoff, b.T + L.toff, Zs, int64_t(k), k, SB_C, L.nc, L.rows, mp,
+                           nullptr, int64_t(0));
+      else
+        hipLaunchKernelGGL((ytz_kernel<1, false>), dim3(cdiv(k, SB_B), L.nc), dim3(512), 0, st,
+                           b.Y + L.yoff, b.T + L.toff, Zs, int64_t(k), k, SB_C, L.nc, L.rows, mp,
+                           nullptr, int64_t(0));
+      TG_CHK(hipGetLastError());
+    }
+  }
+  return hipSuccess;
+}
+
+}  // namespace tg

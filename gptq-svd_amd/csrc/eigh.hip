@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "../../include/truncgptq.h"
+#include "band.h"
 #include "common.h"
 #include "gemm64.h"
 #include "reduce.h"
@@ -783,9 +784,17 @@ __global__ void transpose_kernel(const double *__restrict__ Z, int n, int k, dou
 // ===========================================================================
 // C ABI
 // ===========================================================================
+// Two-stage reduction (band.hip) in front of the tridiagonalisation.
+bool two_stage(int n) {
+  const char *e = getenv("TG_EIGH_TWOSTAGE");
+  return e && e[0] == '1' && n > tg::SB_B + 1;
+}
+
 extern "C" size_t tg_eigh_workspace_size(int n) {
   tg::Sizer s;
   tri_layout(s, n, nullptr);
+  tg::SbPlan pl(n);
+  tg::sb_layout(s, n, n, pl, nullptr);
   return s.off + 256;
 }
 
@@ -799,7 +808,11 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   tg::Arena ar(ws, ws_bytes);
   Tri w{};
   tri_layout(ar, n, &w);
+  tg::SbPlan pl(n);
+  tg::SbBufs sb{};
+  tg::sb_layout(ar, n, n, pl, &sb);
   TG_WS(ar);
+  if (two_stage(n)) TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
   TG_HIP(hipMemsetAsync(w.V, 0, sizeof(double) * size_t(n) * n, st));
   TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
   TG_HIP(hipMemsetAsync(w.e, 0, sizeof(double) * n, st));
@@ -894,6 +907,9 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   tg::Arena ar(ws, ws_bytes);
   Tri w{};
   tri_layout(ar, n, &w);
+  tg::SbPlan pl(n);
+  tg::SbBufs sb{};
+  tg::sb_layout(ar, n, n, pl, &sb);
   TG_WS(ar);
   const double *bnd = w.scal;
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
@@ -925,6 +941,7 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
     }
     tg::prof_end(st, btok2);
   }
+  if (two_stage(n)) TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
   hipLaunchKernelGGL(transpose_kernel, dim3(tg::cdiv(k, 32), tg::cdiv(n, 32)), dim3(32, 8), 0, st,
                      w.Z, n, k, Vh, ldv);
   TG_LAUNCHED();

@@ -31,35 +31,92 @@ __device__ inline double to_f64<__hip_bfloat16>(__hip_bfloat16 v) { return doubl
 constexpr int KC = 16;
 constexpr int PAD = 4;
 
-// Stage op(X) tile into a k-major LDS image S[KC][W + PAD] covering
-// rows r0..r0+W of op(X) (op(X) is R x K) and k0..k0+KC.
+// Staging of an op(X) tile into a k-major LDS image S[KC][W + PAD] covering
+// rows r0..r0+W of op(X) (op(X) is R x K) and k0..k0+KC, split into a
+// global->register load (issued one K-slab ahead) and a register->LDS store.
 //  TRANS == false: X stored R x K (ld), element (r, k) at X[r*ld + k]
 //  TRANS == true : X stored K x R (ld), element (r, k) at X[k*ld + r]
 template <class T, int W, bool TRANS>
-__device__ inline void stage(const T *__restrict__ X, int64_t ld, int R, int K, int r0, int k0,
-                             double (*S)[W + PAD]) {
-  const int tid = threadIdx.x;
-  constexpr int PER = W * KC / 256;  // elements per thread
-  if (!TRANS) {
-    // each thread: one row, PER consecutive k
-    constexpr int TPR = KC / PER;  // threads per row
-    const int r = tid / TPR, kb = (tid % TPR) * PER;
-    const int gr = r0 + r;
+struct Stg {
+  static constexpr int PER = W * KC / 256;  // elements per thread
+  double v[PER];
+  __device__ inline void load(const T *__restrict__ X, int64_t ld, int R, int K, int r0, int k0) {
+    const int tid = threadIdx.x;
+    if (!TRANS) {  // one row, PER consecutive k
+      constexpr int TPR = KC / PER;
+      const int r = tid / TPR, kb = (tid % TPR) * PER;
+      const int gr = r0 + r;
 #pragma unroll
-    for (int t = 0; t < PER; ++t) {
-      const int gk = k0 + kb + t;
-      S[kb + t][r] = (gr < R && gk < K) ? to_f64(X[int64_t(gr) * ld + gk]) : 0.0;
-    }
-  } else {
-    // each thread: one k, PER consecutive rows
-    constexpr int TPK = W / PER;
-    const int k = tid / TPK, rb = (tid % TPK) * PER;
-    const int gk = k0 + k;
+      for (int t = 0; t < PER; ++t) {
+        const int gk = k0 + kb + t;
+        v[t] = (gr < R && gk < K) ? to_f64(X[int64_t(gr) * ld + gk]) : 0.0;
+      }
+    } else {  // one k, PER consecutive rows
+      constexpr int TPK = W / PER;
+      const int k = tid / TPK, rb = (tid % TPK) * PER;
+      const int gk = k0 + k;
 #pragma unroll
-    for (int t = 0; t < PER; ++t) {
-      const int gr = r0 + rb + t;
-      S[k][rb + t] = (gr < R && gk < K) ? to_f64(X[int64_t(gk) * ld + gr]) : 0.0;
+      for (int t = 0; t < PER; ++t) {
+        const int gr = r0 + rb + t;
+        v[t] = (gr < R && gk < K) ? to_f64(X[int64_t(gk) * ld + gr]) : 0.0;
+      }
     }
+  }
+  __device__ inline void store(double (*S)[W + PAD]) const {
+    const int tid = threadIdx.x;
+    if (!TRANS) {
+      constexpr int TPR = KC / PER;
+      const int r = tid / TPR, kb = (tid % TPR) * PER;
+#pragma unroll
+      for (int t = 0; t < PER; ++t) S[kb + t][r] = v[t];
+    } else {
+      constexpr int TPK = W / PER;
+      const int k = tid / TPK, rb = (tid % TPK) * PER;
+#pragma unroll
+      for (int t = 0; t < PER; ++t) S[k][rb + t] = v[t];
+    }
+  }
+};
+
+// acc += op(A)[tm:tm+BM, kb:ke] op(B)[kb:ke, tn:tn+BN], 4 waves as 2x2.
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>
+__device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
+                                const TB_ *__restrict__ B, int64_t ldb, int M, int N, int kb,
+                                int ke, int tm, int tn, double (*As)[BM + PAD],
+                                double (*Bs)[BN + PAD],
+                                doublex4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  Stg<TA_, BM, TA> sa;
+  Stg<TB_, BN, !TB> sb;  // op(B) staged as op(B)^T (N x K)
+  if (kb < ke) {
+    sa.load(A, lda, M, ke, tm, kb);
+    sb.load(B, ldb, N, ke, tn, kb);
+  }
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+    sa.store(As);
+    sb.store(Bs);
+    __syncthreads();
+    if (k0 + KC < ke) {
+      sa.load(A, lda, M, ke, tm, k0 + KC);
+      sb.load(B, ldb, N, ke, tn, k0 + KC);
+    }
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      double af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
   }
 }
 
@@ -98,26 +155,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
   const int kb = blockIdx.z * kchunk;
   const int ke = min(K, kb + kchunk);
   C += int64_t(blockIdx.z) * zstride;
-  for (int k0 = kb; k0 < ke; k0 += KC) {
-    stage<TA_, BM, TA>(A, lda, M, ke, tm, k0, As);
-    // op(B) is K x N; stage it as op(B)^T (N x K) with the transposed flag
-    stage<TB_, BN, !TB>(B, ldb, N, ke, tn, k0, Bs);
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
-      double af[FM], bf[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-  }
+  mainloop<TA_, TB_, BM, BN, TA, TB>(A, lda, B, ldb, M, N, kb, ke, tm, tn, As, Bs, acc);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -165,25 +203,7 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < K; k0 += KC) {
-    stage<double, BM, TA>(A, lda, M, K, tm, k0, As);
-    stage<double, BN, !TB>(B, ldb, N, K, tn, k0, Bs);
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
-      double af[FM], bf[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-  }
+  mainloop<double, double, BM, BN, TA, TB>(A, lda, B, ldb, M, N, 0, K, tm, tn, As, Bs, acc);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -272,12 +292,22 @@ hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, 
   const int hmax = std::max(cs.c, cs.m - (cs.nc - 1) * cs.c);
   const int M = cs.M < 0 ? hmax : cs.M, N = cs.N < 0 ? hmax : cs.N;
   if (M <= 0 || N <= 0) return hipSuccess;
-  const bool big = int64_t(cdiv(M, 128)) * cdiv(N, 128) * cs.nc >= 256;
+  const bool big = int64_t(cdiv(M, 128)) * cdiv(N, 128) * cs.nc >= 256 && N > 64;
+  const bool narrow = N <= 32;
+#define TG_CH2(BM_, BN_, TA_, TB_)                                                             \
+  hipLaunchKernelGGL((dgemm_chunked_kernel<BM_, BN_, TA_, TB_>),                              \
+                     dim3(cdiv(N, BN_), cdiv(M, BM_), cs.nc), dim3(256), 0, st, cs, alpha, A, \
+                     lda, B, ldb, beta, C, ldc)
 #define TG_CH(BM_, TA_, TB_)                                                                   \
   hipLaunchKernelGGL((dgemm_chunked_kernel<BM_, BM_, TA_, TB_>),                              \
                      dim3(cdiv(N, BM_), cdiv(M, BM_), cs.nc), dim3(256), 0, st, cs, alpha, A, \
                      lda, B, ldb, beta, C, ldc)
-  if (big) {
+  if (narrow) {
+    if (!ta && !tb) TG_CH2(64, 32, false, false);
+    else if (!ta && tb) TG_CH2(64, 32, false, true);
+    else if (ta && !tb) TG_CH2(64, 32, true, false);
+    else TG_CH2(64, 32, true, true);
+  } else if (big) {
     if (!ta && !tb) TG_CH(128, false, false);
     else if (!ta && tb) TG_CH(128, false, true);
     else if (ta && !tb) TG_CH(128, true, false);
@@ -289,6 +319,7 @@ hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, 
     else TG_CH(64, true, true);
   }
 #undef TG_CH
+#undef TG_CH2
   return hipGetLastError();
 }
 

@@ -136,6 +136,15 @@ def test_eigh(lib, kind, n):
     assert orth <= (1e-8 if kind == "graded" else 1e-10)
 
 
+@pytest.mark.parametrize("kind,n", [("wishart", 40), ("wishart", 300), ("wishart", 600),
+                                    ("lowrank", 1100), ("graded", 300), ("clustered", 544),
+                                    ("wishart", 4200)])
+def test_eigh_two_stage(lib, monkeypatch, kind, n):
+    """Full -> band (TSQR panels, 1-3 levels) in front of the tridiagonalisation."""
+    monkeypatch.setenv("TG_EIGH_TWOSTAGE", "1")
+    test_eigh(lib, kind, n)
+
+
 @pytest.mark.parametrize("name", golden_names("p_"))
 def test_process_hessian_alt_golden(g, oracle_mod, name):
     d = load_golden(name)
