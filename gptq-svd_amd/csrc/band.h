@@ -37,7 +37,15 @@ struct SbBufs {
   double *Gr, *U;         // gathered rows / symmetric update (ncmax*32 x n)
   double *Xs;             // gathered rows of X (ncmax*32 x ncmax*32)
   double *Zg, *P, *Mz;    // back-transformation temporaries (ncmax*32 x k)
+  // stage 2 (bulge.hip)
+  double *Bst;            // band storage n x 2b
+  double *V2, *tau2;      // bulge-chasing reflectors ((n-2) x smax x b, (n-2) x smax)
+  double *T2;             // Q2 block T factors
+  unsigned *prog;         // pipeline progress per sweep group
 };
+
+int sb_smax(int n);
+size_t sb2st_t2_count(int n);
 
 template <class A>
 void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
@@ -62,11 +70,24 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.Zg, w * kmax);
   take(b.P, w * kmax);
   take(b.Mz, w * kmax);
+  const size_t nsw = size_t(std::max(1, n - 2)), smax = size_t(sb_smax(n));
+  take(b.Bst, size_t(n) * 2 * SB_B);
+  take(b.V2, nsw * smax * SB_B);
+  take(b.tau2, nsw * smax);
+  take(b.T2, sb2st_t2_count(n));
+  if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw);
+  else ar.template take<unsigned>(nsw);
 }
 
 // A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth
 // SB_B in place (full storage, zeros outside the band); reflectors in bufs.
 hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b);
+// Band (in A after sy2sb) -> tridiagonal (d, e) by bulge chasing.
+hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
+                 double *tau2, unsigned *prog, double *d, double *e);
+// Z (n x k row-major) <- Q2 Z.
+hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
+                       const double *tau2, double *T2);
 // Z (n x k row-major) <- Q1 Z.
 hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                        const SbBufs &b);

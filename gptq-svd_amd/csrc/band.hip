@@ -328,13 +328,20 @@ __global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int rl = wid * 64 + rb * 16 + lr + 4 * q;
-      int zr = -1;
-      if (rl < h) zr = GATHER ? mp.fwd(kb + rl) : kb + rl;
+      const int rc = min(rl, h - 1);
+      const int zr = GATHER ? mp.fwd(kb + rc) : kb + rc;
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int col = c0 + cb * 16 + lc;
-        F[rb][cb][q] = (zr >= 0 && col < ncols) ? Z[int64_t(zr) * ldz + col] : 0.0;
-      }
+      for (int cb = 0; cb < 2; ++cb)
+        F[rb][cb][q] = Z[int64_t(zr) * ldz + min(c0 + cb * 16 + lc, ncols - 1)];
+    }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+        F[rb][cb][q] = (rl < h && c0 + cb * 16 + lc < ncols) ? F[rb][cb][q] : 0.0;
     }
   // P_w = Y_w^T Z_w
   doublex4 Pa[2][2];
@@ -350,7 +357,9 @@ __global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
       double ya[2];
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia)
-        ya[ia] = rl < h ? Y[int64_t(kb + rl) * SB_B + ia * 16 + lc] : 0.0;
+        ya[ia] = Y[int64_t(kb + min(rl, h - 1)) * SB_B + ia * 16 + lc];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ya[ia] = rl < h ? ya[ia] : 0.0;
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
@@ -400,7 +409,8 @@ __global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const int rl = wid * 64 + rb * 16 + lc;
-      const double ya = rl < h ? -Y[int64_t(kb + rl) * SB_B + k0 + lr] : 0.0;
+      const double yl = Y[int64_t(kb + min(rl, h - 1)) * SB_B + k0 + lr];
+      const double ya = rl < h ? -yl : 0.0;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
         F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm[cb], F[rb][cb], 0, 0, 0);
@@ -479,18 +489,25 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
   for (int k0 = 0; k0 < 3 * SB_B; k0 += S2K) {
     const int seg = k0 / SB_B;
     const int kl = (k0 & 31) + sk;
-    if (seg < 2) {
-      const int gr = tm + sr;
-      const double *src = seg ? X + int64_t(gr) * ldx + cj * SB_B + kl : Y + int64_t(gr) * SB_B + kl;
+    double va[4], vb[4];
+    {
+      const int gr = tm + sr, grc = min(gr, m - 1);
+      const double *src = seg ? X + int64_t(grc) * ldx + cj * SB_B + kl : Y + int64_t(grc) * SB_B + kl;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) As[sk + t][sr] = gr < m ? src[t] : 0.0;
+      for (int t = 0; t < 4; ++t) va[t] = src[t];
     }
     {
-      const int gr = tn + sr;
-      const double *src = seg == 0 ? X + int64_t(gr) * ldx + ci * SB_B + kl : Y + int64_t(gr) * SB_B + kl;
+      const int gr = tn + sr, grc = min(gr, m - 1);
+      const double *src = seg == 0 ? X + int64_t(grc) * ldx + ci * SB_B + kl : Y + int64_t(grc) * SB_B + kl;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) Bs[sk + t][sr] = gr < m ? src[t] : 0.0;
+      for (int t = 0; t < 4; ++t) vb[t] = src[t];
     }
+    if (seg < 2) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) As[sk + t][sr] = tm + sr < m ? va[t] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) Bs[sk + t][sr] = tn + sr < m ? vb[t] : 0.0;
     __syncthreads();
     double(*Ap)[S2T + S2P] = seg < 2 ? As : YS + (k0 & 31);
 #pragma unroll

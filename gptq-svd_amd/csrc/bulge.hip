@@ -1,0 +1,684 @@
+// Stage 2 of the two-stage eigensolver: band (half-bandwidth b = SB_B) ->
+// symmetric tridiagonal by bulge chasing, plus the back-transformation Q2.
+//
+// Second half of the reduction inside `torch.linalg.eigh`
+// (/root/reference/src/TruncGPTQ/gptq_utils.py:92).  Algorithm (one column
+// per sweep): sweep j, task s takes the reflector rows R = [r1, r1 + b),
+// r1 = j + 1 + s b, annihilating column j (s = 0) or the first bulge column
+// r1 - b (s > 0), and applies it two-sided to the window [r1 - b, r1 + 2b):
+//   B[R, Lft] <- H B[R, Lft],  B[R, R] <- H B[R, R] H,  B[Rgt, R] <- B[Rgt, R] H.
+// Task (j, s) overlaps sweep j-1's tasks s-1 .. s+2 only, so sweeps run as a
+// pipeline with a lag of 3 tasks.  GPU mapping: one wave per task; a
+// workgroup owns G_SW consecutive sweeps and advances them in lock-step
+// (wave q runs task t - 3q at step t; the tasks of one step are disjoint).
+// Workgroups hand over through a per-group step counter, published with an
+// agent-scope release every PUB steps and read with an acquire.
+//
+// Band storage (lower, with bulge room): Bst[c * LDB + d] = B[c + d][c],
+// d < 2b.  Reflectors of (j, s): V2[(j * smax + s) * b + i], tau2[j * smax + s].
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "band.h"
+#include "common.h"
+
+namespace {
+
+using tg::SB_B;
+constexpr int LDB = 2 * SB_B;
+
+__device__ inline double xchg32(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = (threadIdx.x & 32) != 0;
+  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+}
+__device__ inline double xchg16(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool up = (threadIdx.x & 16) != 0;
+  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+}
+__device__ inline double wsum(double s) {  // full wave sum, result in every lane
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  return s;
+}
+
+__device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) / SB_B + 1 : 0; }
+
+// ---------------------------------------------------------------------------
+// LDS-resident pipeline.  A workgroup owns G_SW consecutive sweeps; at step t
+// wave q runs task t - 3q.  The band columns the group touches at step t span
+// [low(t), high(t)) with high(t) - low(t) < 8b, so the group keeps them in an
+// LDS ring of RING band columns (64 doubles each): each step it prefetches the
+// b columns step t+1 adds, and writes back the columns no later task of the
+// group touches.  Hand-off to the next group: the write-backs are plain stores
+// (they stay in the XCD's L2), drained with vmcnt(0) and a barrier before one
+// lane publishes the step count with an sc1 store; the consumer polls with sc1
+// loads and reads columns with sc1 buffer loads (L1 bypassed, L2-served).
+// This is coherent because every worker runs on the same XCD: workgroups read
+// HW_REG_XCC_ID, the first arrival fixes the XCD, the others exit, and the
+// workers take sweep groups from a queue in increasing order (dependencies
+// point only to lower groups, so any number of resident workers is safe).
+// ---------------------------------------------------------------------------
+constexpr int G_SW = 2;              // sweeps per group (waves per workgroup)
+constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
+constexpr int BT = 128 * G_SW;       // threads per workgroup (a wave pair per sweep)
+
+struct WaveScratch {
+  double vs[SB_B];
+  double ws[SB_B];
+};
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline int rslot(int c) { return c & (RING - 1); }
+
+// Task (j, s) by a pair of waves on the LDS ring (element (r, c) at
+// R[slot(c)][r - c]).  Both waves form the reflector from x = B[R, col]; then
+// role 0 applies it to the left block A = B[R, Lft] and rows 0..15 of the
+// lower block G = B[Rgt, R], role 1 to the diagonal block D = B[R, R] and
+// rows 16..31 of G.  The three blocks are disjoint, so the waves never talk.
+template <bool FULL>
+__device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, int s, int role,
+                                               double *__restrict__ V2,
+                                               double *__restrict__ tau2, int smax,
+                                               WaveScratch &W) {
+  const int lane = threadIdx.x & 63, li = lane & 31, hf = lane >> 5;
+  const int r1 = j + 1 + s * SB_B;
+  const int L = FULL ? SB_B : min(SB_B, n - r1);
+  const int col = (s == 0) ? j : r1 - SB_B;
+  const int lo = FULL ? r1 - SB_B : max(0, r1 - SB_B);
+  const int nl = FULL ? SB_B : r1 - lo;
+  const int ng = FULL ? SB_B : min(SB_B, n - (r1 + L));
+  double *Rf = &R[0][0];
+  auto at = [&](int c, int d) { return rslot(c) * LDB + d; };
+  const double x = (FULL || li < L) ? Rf[at(col, r1 + min(li, L - 1) - col)] : 0.0;
+  // block loads (issued before the reflector's reductions)
+  double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li, k = hf + 2q)
+  double g[8];   // G rows gr = 16 role + (lane & 15), columns k = (lane >> 4) + 4q
+  const int gr = 16 * role + (lane & 15), gk0 = lane >> 4;
+  if (role == 0) {
+    const int ca = FULL ? li : min(li, max(nl - 1, 0));
+    const int abase = at(lo + ca, r1 - lo - ca);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = hf + 2 * q;
+      if (FULL) e[q] = Rf[abase + i];
+      else e[q] = (li < nl && i < L) ? Rf[abase + min(i, L - 1)] : 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      const int cc = min(li, k), off = li > k ? li - k : k - li;
+      if (FULL) e[q] = Rf[at(r1 + cc, off)];
+      else e[q] = (li < L && k < L) ? Rf[at(r1 + min(cc, L - 1), off)] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = gk0 + 4 * q;
+    if (FULL) g[q] = Rf[at(r1 + k, SB_B + gr - k)];
+    else {
+      const int kc = min(k, L - 1);
+      const double gv = Rf[at(r1 + kc, L + min(gr, max(ng - 1, 0)) - kc)];
+      g[q] = (gr < ng && k < L) ? gv : 0.0;
+    }
+  }
+  // reflector (identical in both waves)
+  const double sig = wsum((hf == 0 && li >= 1) ? x * x : 0.0);
+  const double alpha = __shfl(x, 0);
+  double tau = 0.0, scal = 0.0, beta = alpha;
+  if (sig != 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sig), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  const double v = (li == 0) ? 1.0 : ((FULL || li < L) ? x * scal : 0.0);
+  if (hf == 0) W.vs[li] = v;
+  wave_sync();
+  double vk[16], vg[8];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) vk[q] = W.vs[hf + 2 * q];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) vg[q] = W.vs[gk0 + 4 * q];
+  // lower block rows: u_r = sum_k G[r][k] v_k, G -= tau u v^T
+  double u = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) u += g[q] * vg[q];
+  u += xchg16(u);
+  u += xchg32(u);
+  if (role == 0) {
+    // left block: w_c = sum_i v_i A[i][c]
+    double wc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wc += vk[q] * e[q];
+    wc += xchg32(wc);
+    if (FULL || li < nl) {
+      const int c = li;
+      double *Ac = Rf + at(lo + c, r1 - lo - c);
+      const bool piv = (lo + c == col);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = hf + 2 * q;
+        if (FULL || i < L) Ac[i] = piv ? (i == 0 ? beta : 0.0) : e[q] - tau * vk[q] * wc;
+      }
+    }
+    if (hf == 0) V2[(int64_t(j) * smax + s) * SB_B + li] = v;
+    if (lane == 0) tau2[int64_t(j) * smax + s] = tau;
+  } else {
+    double p = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) p += e[q] * vk[q];
+    p += xchg32(p);
+    p *= tau;
+    const double pv = wsum(hf == 0 ? p * v : 0.0);
+    const double w = p - 0.5 * tau * pv * v;
+    if (hf == 0) W.ws[li] = w;
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      if ((FULL || li < L) && k <= li) Rf[at(r1 + k, li - k)] = e[q] - v * W.ws[k] - w * vk[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = gk0 + 4 * q;
+    if (FULL || (gr < ng && k < L)) Rf[at(r1 + k, L + gr - k)] = g[q] - tau * u * vg[q];
+  }
+}
+
+__device__ inline int group_steps(int n, int nsw, int G) {
+  const int j0 = G * G_SW;
+  const int g = min(G_SW, nsw - j0);
+  return 3 * (g - 1) + ntasks(n, j0);
+}
+
+// Lowest column any task of the group touches at step >= t (n if none).
+__device__ inline int group_low(int n, int nsw, int j0, int g, int t) {
+  int lowc = n;
+  for (int q = 0; q < g; ++q) {
+    const int j = j0 + q;
+    int s = t - 3 * q;
+    if (s < 0) s = 0;
+    if (s >= ntasks(n, j)) continue;
+    const int r1 = j + 1 + s * SB_B;
+    lowc = min(lowc, max(0, r1 - SB_B));
+  }
+  return lowc;
+}
+// One past the highest column any task of the group touches at steps <= t.
+__device__ inline int group_high(int n, int j0, int t) {
+  return min(n, j0 + 1 + (t + 1) * SB_B);
+}
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, int n,
+                                                       double *__restrict__ V2,
+                                                       double *__restrict__ tau2, int smax,
+                                                       unsigned *__restrict__ prog,
+                                                       unsigned *__restrict__ ctl,
+                                                       unsigned long long *__restrict__ stats) {
+  uint64_t sw = 0, stk = 0, sbar = 0, spf = 0, swb = 0, nsteps = 0;
+  __shared__ double R[RING][LDB];
+  __shared__ WaveScratch wsc[2 * G_SW];
+  __shared__ int sh_G;
+  const int tid = threadIdx.x, wid = tid >> 6;
+  // workers: one XCD only (ctl[0] = chosen XCD + 1, ctl[1] = group queue)
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned expect = 0;
+    __hip_atomic_compare_exchange_strong(ctl, &expect, x + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned chosen = expect == 0 ? x + 1 : expect;
+    sh_G = (chosen == x + 1) ? 0 : -1;
+  }
+  __syncthreads();
+  if (sh_G < 0) return;
+  const int nsw = n - 2;
+  const int ngroups = tg::cdiv(nsw, G_SW);
+  const int bytes = n * LDB * int(sizeof(double));
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(B, 0, bytes, 0x00020000);
+  constexpr int SC1 = 16;
+  const int nthr_col = LDB / 2;  // threads per column for 16-B transfers
+  while (true) {
+    if (tid == 0) sh_G = int(atomicAdd(ctl + 1, 1u));
+    __syncthreads();
+    const int G = sh_G;
+    __syncthreads();
+    if (G >= ngroups) break;
+    const int j0 = G * G_SW;
+    const int g = min(G_SW, nsw - j0);
+    const int total = group_steps(n, nsw, G);
+    const int ptotal = G > 0 ? group_steps(n, nsw, G - 1) : 0;
+    int known = (G > 0) ? 0 : 1 << 30;
+    auto wait_for = [&](int need) {
+      need = min(need, ptotal + 1);  // ptotal + 1: producer finished and fully written back
+      if (known >= need) return;
+      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               unsigned(need)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up
+            __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      known = need;
+      sw += __builtin_amdgcn_s_memrealtime() - tw;
+    };
+    // column loader: columns [c0, c1) (c1 - c0 <= SB_B) with 16-B sc1 loads into registers
+    double2 pf[SB_B * LDB / 2 / BT + 1];
+    constexpr int PFN = SB_B * LDB / 2 / BT + 1;
+    auto load_cols = [&](int c0, int c1) {
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) {
+        const int idx = tid + u * BT;  // 16-B chunk index
+        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
+        const int cc = min(c, max(c1 - 1, 0));
+        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (cc * LDB + 2 * h) * 8, 0, SC1);
+        pf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                             __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+      }
+    };
+    auto store_pf = [&](int c0, int c1) {
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) {
+        const int idx = tid + u * BT;
+        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
+        if (c < c1 && idx < SB_B * nthr_col) {
+          R[rslot(c)][2 * h] = pf[u].x;
+          R[rslot(c)][2 * h + 1] = pf[u].y;
+        }
+      }
+    };
+    auto write_back = [&](int c0, int c1) {  // plain 16-B stores from LDS
+      for (int idx = tid; idx < (c1 - c0) * nthr_col; idx += BT) {
+        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
+        const double2 v = make_double2(R[rslot(c)][2 * h], R[rslot(c)][2 * h + 1]);
+        const u32x2 lo2 = __builtin_bit_cast(u32x2, v.x), hi2 = __builtin_bit_cast(u32x2, v.y);
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                               (c * LDB + 2 * h) * 8, 0, 0);
+      }
+    };
+    // initial window: [low(0), high(0))
+    int ld = max(0, j0 + 1 - SB_B), wb = ld;
+    wait_for(3 * G_SW);
+    for (int c0 = ld; c0 < group_high(n, j0, 0); c0 += SB_B) {
+      const int c1 = min(c0 + SB_B, group_high(n, j0, 0));
+      load_cols(c0, c1);
+      store_pf(c0, c1);
+    }
+    ld = group_high(n, j0, 0);
+    __syncthreads();
+    for (int t = 0; t < total; ++t) {
+      // prefetch the columns step t + 1 adds
+      const int nh = group_high(n, j0, t + 1);
+      const bool pre = t + 1 < total && nh > ld;
+      if (pre) {
+        wait_for(t + 1 + 3 * G_SW);
+        load_cols(ld, nh);
+      }
+      const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
+      const int pair = wid >> 1, role = wid & 1;
+      const int s = t - 3 * pair;
+      if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
+        const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
+        if (r1 >= SB_B && r1 + 2 * SB_B <= n)
+          bulge_task_lds<true>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+        else
+          bulge_task_lds<false>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+      }
+      const uint64_t c1t = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();
+      const uint64_t c2t = __builtin_amdgcn_s_memrealtime();
+      if (pre) {
+        store_pf(ld, nh);
+        ld = nh;
+      }
+      const uint64_t c3t = __builtin_amdgcn_s_memrealtime();
+      stk += c1t - c0t;
+      sbar += c2t - c1t;
+      spf += c3t - c2t;
+      ++nsteps;
+      // progress t: steps < t are complete and their write-backs drained
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      swb += __builtin_amdgcn_s_memrealtime() - c3t;
+      if (tid == 0)
+        __hip_atomic_store(prog + G, unsigned(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // retire columns no later task touches (drained at the end of the next step)
+      const int nl = (t + 1 < total) ? group_low(n, nsw, j0, g, t + 1) : ld;
+      if (nl > wb) {
+        write_back(wb, min(nl, ld));
+        wb = min(nl, ld);
+      }
+    }
+    if (wb < ld) write_back(wb, ld);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(prog + G, unsigned(total + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (stats && tid == 0) {
+    atomicAdd(stats + 0, 1ull);
+    atomicAdd(stats + 1, (unsigned long long)sw);
+    atomicAdd(stats + 2, (unsigned long long)stk);
+    atomicAdd(stats + 3, (unsigned long long)sbar);
+    atomicAdd(stats + 4, (unsigned long long)spf);
+    atomicAdd(stats + 5, (unsigned long long)swb);
+    atomicAdd(stats + 6, (unsigned long long)nsteps);
+  }
+}
+
+// Bst[c][d] = A[c + d][c] for d <= b, 0 for b < d < 2b.
+__global__ void extract_band_kernel(const double *__restrict__ A, int64_t lda, int n,
+                                    double *__restrict__ Bst) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * LDB) return;
+  const int c = idx / LDB, d = idx % LDB;
+  Bst[idx] = (d <= SB_B && c + d < n) ? A[int64_t(c + d) * lda + c] : 0.0;
+}
+
+__global__ void extract_tri_kernel(const double *__restrict__ Bst, int n, double *__restrict__ dg,
+                                   double *__restrict__ e) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dg[i] = Bst[int64_t(i) * LDB];
+  e[i] = (i + 1 < n) ? Bst[int64_t(i) * LDB + 1] : 0.0;
+}
+
+}  // namespace
+
+namespace tg {
+
+int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
+
+hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
+                 double *tau2, unsigned *prog, double *d, double *e) {
+  hipLaunchKernelGGL(extract_band_kernel, dim3(cdiv(int64_t(n) * LDB, 256)), dim3(256), 0, st, A,
+                     int64_t(lda), n, Bst);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  const int nsw = n - 2;
+  if (nsw > 0) {
+    const int ngroups = cdiv(nsw, G_SW);
+    err = hipMemsetAsync(prog, 0, sizeof(unsigned) * (ngroups + 4), st);
+    if (err != hipSuccess) return err;
+    unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] timeout flag
+    unsigned long long *stats = nullptr;
+    const bool want = getenv("TG_BULGE_STATS") != nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (want) {
+      (void)hipMalloc(&stats, 8 * sizeof(unsigned long long));
+      (void)hipMemsetAsync(stats, 0, 8 * sizeof(unsigned long long), st);
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      (void)hipEventRecord(e0, st);
+    }
+    hipLaunchKernelGGL(bulge_lds_kernel, dim3(256), dim3(BT), 0, st, Bst, n, V2, tau2, sb_smax(n),
+                       prog, ctl, stats);
+    err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    if (want) {
+      (void)hipEventRecord(e1, st);
+      unsigned long long h[8];
+      (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
+      (void)hipStreamSynchronize(st);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      const double W = double(h[0]), S = double(h[6]);
+      fprintf(stderr,
+              "bulge: %.2f ms, workers %.0f, steps/worker %.0f; per step (us): wait %.2f task %.2f "
+              "bar %.2f pfstore %.2f wb %.2f\n",
+              ms, W, S / W, h[1] / 100.0 / S, h[2] / 100.0 / S, h[3] / 100.0 / S, h[4] / 100.0 / S,
+              h[5] / 100.0 / S);
+      (void)hipFree(stats);
+    }
+  }
+  hipLaunchKernelGGL(extract_tri_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, Bst, n, d, e);
+  return hipGetLastError();
+}
+
+}  // namespace tg
+
+// ---------------------------------------------------------------------------
+// Back-transformation Z <- Q2 Z.  Reflectors are grouped into blocks
+// (G2, s) = sweeps 32 G2 .. 32 G2 + 31 at step s: a staircase Y of 63 rows
+// (column a = reflector of sweep 32 G2 + a, rows a .. a + 31 of the block,
+// block rows start at 32 G2 + 1 + 32 s) with Q_block = H_0 H_1 ... H_31 =
+// I - Y T Y^T.  Valid order (== applying the reflectors in reverse): later
+// sweep groups first, steps ascending within a group; blocks overlap only
+// with (G2, s-1) and (G2+1 or later, s' < s + 1), so level
+// s + (NG2 - 1 - G2) is a set of row-disjoint blocks: one launch per level.
+// ---------------------------------------------------------------------------
+namespace {
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+constexpr int QB = 32;           // sweeps per block (= SB_B)
+constexpr int QR = QB + SB_B - 1;  // rows per block (63)
+
+__device__ inline bool refl_valid(int n, int j, int s) { return j <= n - 3 && s < ntasks(n, j); }
+
+__global__ __launch_bounds__(256) void q2_tfactor_kernel(const double *__restrict__ V2,
+                                                         const double *__restrict__ tau2, int n,
+                                                         int smax, double *__restrict__ T2) {
+  __shared__ double Vs[QB][SB_B];
+  __shared__ double Gs[QB][QB + 1];
+  __shared__ double Ts[QB][QB + 1];
+  __shared__ double taus[QB];
+  const int G2 = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
+  const int j0 = G2 * QB;
+  double *Tout = T2 + (int64_t(G2) * smax + s) * QB * QB;
+  if (!refl_valid(n, j0, s)) return;
+  for (int idx = tid; idx < QB * SB_B; idx += 256) {
+    const int a = idx / SB_B, i = idx % SB_B;
+    Vs[a][i] = refl_valid(n, j0 + a, s) ? V2[(int64_t(j0 + a) * smax + s) * SB_B + i] : 0.0;
+  }
+  if (tid < QB) taus[tid] = refl_valid(n, j0 + tid, s) ? tau2[int64_t(j0 + tid) * smax + s] : 0.0;
+  __syncthreads();
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + 256 * q, a = idx >> 5, c = idx & 31;
+    double g = 0.0;
+    if (a < c)
+      for (int i = c; i < a + SB_B; ++i) g += Vs[a][i - a] * Vs[c][i - c];
+    Gs[a][c] = g;
+    Ts[a][c] = 0.0;
+  }
+  __syncthreads();
+  for (int c = 0; c < QB; ++c) {
+    const double tc = taus[c];
+    if (tid < c) {
+      double acc = 0.0;
+      for (int e = tid; e < c; ++e) acc += Ts[tid][e] * Gs[e][c];
+      Ts[tid][c] = -tc * acc;
+    }
+    if (tid == c) Ts[c][c] = tc;
+    __syncthreads();
+  }
+  for (int idx = tid; idx < QB * QB; idx += 256) Tout[idx] = Ts[idx >> 5][idx & 31];
+}
+
+// One level: blockIdx.y enumerates the level's blocks, each wave one
+// 32-column slab of Z (n x k row-major) over the block's rows (64-row tile
+// in registers as eight 16x16 C-layout fragments).
+__global__ __launch_bounds__(256) void q2_apply_kernel(double *__restrict__ Z, int k, int n,
+                                                       const double *__restrict__ V2,
+                                                       const double *__restrict__ T2, int smax,
+                                                       int ng2, int level, int s_lo) {
+  const int s = s_lo + blockIdx.y;
+  const int G2 = ng2 - 1 - (level - s);
+  const int j0 = G2 * QB;
+  if (G2 < 0 || !refl_valid(n, j0, s)) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int c0 = (blockIdx.x * 4 + wid) * 32;
+  const int rb0 = j0 + 1 + s * SB_B;  // first row of the block
+  __shared__ double Vs[QB][SB_B + 1];
+  __shared__ double Ts[QB][QB + 1];
+  {
+    const double *Tb = T2 + (int64_t(G2) * smax + s) * QB * QB;
+    double vv[4], tt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q, a = idx >> 5, d = idx & 31;
+      const int jj = refl_valid(n, j0 + a, s) ? j0 + a : j0;  // clamp to a valid reflector
+      vv[q] = V2[(int64_t(jj) * smax + s) * SB_B + d];
+      tt[q] = Tb[idx];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q, a = idx >> 5, d = idx & 31;
+      Vs[a][d] = refl_valid(n, j0 + a, s) ? vv[q] : 0.0;
+      Ts[a][d] = tt[q];
+    }
+  }
+  __syncthreads();
+  if (c0 >= k) return;
+  // Y[i][a] = v_a[i - a]  (rows past n hold zeros in v)
+  auto yval = [&](int i, int a) -> double {
+    const int d = i - a;
+    return (d >= 0 && d < SB_B) ? Vs[a][d] : 0.0;
+  };
+  doublex4 F[4][2];
+  {
+    double zl[4][4][2];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const int row = min(rb0 + rb * 16 + lr + 4 * q, n - 1);
+          const int col = min(c0 + cb * 16 + lc, k - 1);
+          zl[rb][q][cb] = Z[int64_t(row) * k + col];
+        }
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = rb * 16 + lr + 4 * q;
+        const bool ok = i < QR && rb0 + i < n;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          F[rb][cb][q] = (ok && c0 + cb * 16 + lc < k) ? zl[rb][q][cb] : 0.0;
+      }
+  }
+  // P = Y^T Z  (32 x 32)
+  doublex4 Pa[2][2];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = rb * 16 + 4 * q + lr;
+      double ya[2];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ya[ia] = yval(i, ia * 16 + lc);
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][q], Pa[ia][cb], 0, 0, 0);
+    }
+  // M = T P   (T upper triangular 32 x 32); B operand of K-step (ia, q) = Pa[ia][cb][q]
+  doublex4 Ma[2][2];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) Ma[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = kb * 16 + 4 * q + lr;
+      double ta[2];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ta[ia] = Ts[ia * 16 + lc][kk];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          Ma[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ta[ia], Pa[kb][cb][q], Ma[ia][cb], 0, 0, 0);
+    }
+  // Z -= Y M
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = kb * 16 + 4 * q + lr;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const double ya = -yval(rb * 16 + lc, kk);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][q], F[rb][cb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = rb * 16 + lr + 4 * q;
+      const int row = rb0 + i;
+      if (i >= QR || row >= n) continue;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col = c0 + cb * 16 + lc;
+        if (col < k) Z[int64_t(row) * k + col] = F[rb][cb][q];
+      }
+    }
+}
+
+}  // namespace
+
+namespace tg {
+
+hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
+                       const double *tau2, double *T2) {
+  const int nsw = n - 2;
+  if (nsw <= 0) return hipSuccess;
+  const int smax = sb_smax(n);
+  const int ng2 = cdiv(nsw, QB);
+  hipLaunchKernelGGL(q2_tfactor_kernel, dim3(smax, ng2), dim3(256), 0, st, V2, tau2, n, smax, T2);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  const int nlev = smax + ng2 - 1;
+  for (int level = 0; level < nlev; ++level) {
+    const int s_lo = std::max(0, level - (ng2 - 1)), s_hi = std::min(smax - 1, level);
+    if (s_hi < s_lo) continue;
+    hipLaunchKernelGGL(q2_apply_kernel, dim3(cdiv(k, 128), s_hi - s_lo + 1), dim3(256), 0, st, Z,
+                       k, n, V2, T2, smax, ng2, level, s_lo);
+    err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+size_t sb2st_t2_count(int n) {
+  const int nsw = std::max(1, n - 2);
+  return size_t(cdiv(nsw, QB)) * sb_smax(n) * QB * QB;
+}
+
+}  // namespace tg

@@ -34,7 +34,7 @@ struct Sizer {
   }
 };
 
-inline int cdiv(int64_t a, int64_t b) { return int((a + b - 1) / b); }
+__host__ __device__ inline int cdiv(int64_t a, int64_t b) { return int((a + b - 1) / b); }
 
 // Sampled HIP-event timing of tagged kernel classes (tg_profile_* in the C ABI).
 // A launch site calls prof_begin/prof_end around the launch on its stream; when

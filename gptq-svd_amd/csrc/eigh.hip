@@ -785,9 +785,10 @@ __global__ void transpose_kernel(const double *__restrict__ Z, int n, int k, dou
 // C ABI
 // ===========================================================================
 // Two-stage reduction (band.hip) in front of the tridiagonalisation.
+// TG_EIGH_TWOSTAGE=0 selects the one-stage reduction (kept for A/B tests).
 bool two_stage(int n) {
   const char *e = getenv("TG_EIGH_TWOSTAGE");
-  return e && e[0] == '1' && n > tg::SB_B + 1;
+  return !(e && e[0] == '0') && n > tg::SB_B + 1;
 }
 
 extern "C" size_t tg_eigh_workspace_size(int n) {
@@ -812,7 +813,12 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   tg::SbBufs sb{};
   tg::sb_layout(ar, n, n, pl, &sb);
   TG_WS(ar);
-  if (two_stage(n)) TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
+  const bool ts = two_stage(n);
+  if (ts) {
+    TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
+    TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.tau2, sb.prog, w.d, w.e));
+  }
+  if (!ts) {
   TG_HIP(hipMemsetAsync(w.V, 0, sizeof(double) * size_t(n) * n, st));
   TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
   TG_HIP(hipMemsetAsync(w.e, 0, sizeof(double) * n, st));
@@ -856,6 +862,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
       tg::prof_end(st, tok);
     }
   }
+  }  // one-stage
   // eigenvalues of T
   double *bnd = w.scal;
   hipLaunchKernelGGL(tri_bounds_kernel, dim3(1), dim3(256), 0, st, w.d, w.e, n, bnd);
@@ -920,7 +927,12 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-9, w.Z);
   TG_LAUNCHED();
   // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
-  const int nref = n - 1;
+  const bool ts = two_stage(n);
+  const int nref = ts ? 0 : n - 1;
+  if (ts) {
+    TG_HIP(tg::sb_apply_q2(st, n, w.Z, k, sb.V2, sb.tau2, sb.T2));
+    TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
+  }
   if (nref > 0) {
     const int nblk = tg::cdiv(nref, BT);
     hipLaunchKernelGGL(tfactor_kernel, dim3(nblk), dim3(256), 0, st, w.V, n, nref, w.tau, w.Tf);
@@ -941,7 +953,6 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
     }
     tg::prof_end(st, btok2);
   }
-  if (two_stage(n)) TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
   hipLaunchKernelGGL(transpose_kernel, dim3(tg::cdiv(k, 32), tg::cdiv(n, 32)), dim3(32, 8), 0, st,
                      w.Z, n, k, Vh, ldv);
   TG_LAUNCHED();

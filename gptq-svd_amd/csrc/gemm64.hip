@@ -46,20 +46,20 @@ struct Stg {
       constexpr int TPR = KC / PER;
       const int r = tid / TPR, kb = (tid % TPR) * PER;
       const int gr = r0 + r;
+      const int grc = min(gr, R - 1);
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
-        const int gk = k0 + kb + t;
-        v[t] = (gr < R && gk < K) ? to_f64(X[int64_t(gr) * ld + gk]) : 0.0;
-      }
+      for (int t = 0; t < PER; ++t) v[t] = to_f64(X[int64_t(grc) * ld + min(k0 + kb + t, K - 1)]);
+#pragma unroll
+      for (int t = 0; t < PER; ++t) v[t] = (gr < R && k0 + kb + t < K) ? v[t] : 0.0;
     } else {  // one k, PER consecutive rows
       constexpr int TPK = W / PER;
       const int k = tid / TPK, rb = (tid % TPK) * PER;
       const int gk = k0 + k;
+      const int gkc = min(gk, K - 1);
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
-        const int gr = r0 + rb + t;
-        v[t] = (gr < R && gk < K) ? to_f64(X[int64_t(gk) * ld + gr]) : 0.0;
-      }
+      for (int t = 0; t < PER; ++t) v[t] = to_f64(X[int64_t(gkc) * ld + min(r0 + rb + t, R - 1)]);
+#pragma unroll
+      for (int t = 0; t < PER; ++t) v[t] = (gk < K && r0 + rb + t < R) ? v[t] : 0.0;
     }
   }
   __device__ inline void store(double (*S)[W + PAD]) const {
@@ -120,6 +120,45 @@ __device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
   }
 }
 
+// C = alpha acc + beta C for the 4-wave tile; the beta != 0 reads are issued
+// together (clamped addresses) so they overlap instead of serialising.
+template <int BM, int BN, bool SYRK>
+__device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double alpha, double beta,
+                                double *__restrict__ C, int64_t ldc, int M, int N, int tm,
+                                int tn) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  double cv[FM][FN][4];
+  if (beta != 0.0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = min(tm + wm * WM + i * 16 + (lane >> 4) + 4 * r, M - 1);
+          const int gj = min(tn + wn * WN + j * 16 + (lane & 15), N - 1);
+          cv[i][j][r] = C[int64_t(gi) * ldc + gj];
+        }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
+        const int gj = tn + wn * WN + j * 16 + (lane & 15);
+        if (gi < M && gj < N) {
+          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * cv[i][j][r];
+          C[int64_t(gi) * ldc + gj] = v;
+          if (SYRK && tm != tn) C[int64_t(gj) * ldc + gi] = v;
+        }
+      }
+}
+
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK>
 __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha,
                                                     const TA_ *__restrict__ A, int64_t lda,
@@ -130,8 +169,6 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
   __shared__ double Bs[KC][BN + PAD];
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
   int tm, tn;
   if (SYRK) {  // blockIdx.x enumerates lower-triangle tiles (I >= J)
     const int b = blockIdx.x;
@@ -156,21 +193,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
   const int ke = min(K, kb + kchunk);
   C += int64_t(blockIdx.z) * zstride;
   mainloop<TA_, TB_, BM, BN, TA, TB>(A, lda, B, ldb, M, N, kb, ke, tm, tn, As, Bs, acc);
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
-        const int gj = tn + wn * WN + j * 16 + (lane & 15);
-        if (gi < M && gj < N) {
-          double *p = C + int64_t(gi) * ldc + gj;
-          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *p;
-          *p = v;
-          if (SYRK && tm != tn) C[int64_t(gj) * ldc + gi] = v;
-        }
-      }
+  epilogue<BM, BN, SYRK>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
 // Chunked variant: blockIdx.z = chunk; offsets/dims from ChunkSpec.
@@ -196,27 +219,13 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
   A += int64_t(kb) * cs.a_kb + int64_t(z) * cs.a_z;
   B += int64_t(kb) * cs.b_kb + int64_t(z) * cs.b_z;
   C += int64_t(kb) * cs.c_kb + int64_t(z) * cs.c_z;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
   doublex4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
   mainloop<double, double, BM, BN, TA, TB>(A, lda, B, ldb, M, N, 0, K, tm, tn, As, Bs, acc);
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
-        const int gj = tn + wn * WN + j * 16 + (lane & 15);
-        if (gi < M && gj < N) {
-          double *p = C + int64_t(gi) * ldc + gj;
-          *p = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *p;
-        }
-      }
+  epilogue<BM, BN, false>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>

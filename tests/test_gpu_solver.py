@@ -139,9 +139,9 @@ def test_eigh(lib, kind, n):
 @pytest.mark.parametrize("kind,n", [("wishart", 40), ("wishart", 300), ("wishart", 600),
                                     ("lowrank", 1100), ("graded", 300), ("clustered", 544),
                                     ("wishart", 4200)])
-def test_eigh_two_stage(lib, monkeypatch, kind, n):
-    """Full -> band (TSQR panels, 1-3 levels) in front of the tridiagonalisation."""
-    monkeypatch.setenv("TG_EIGH_TWOSTAGE", "1")
+def test_eigh_one_stage(lib, monkeypatch, kind, n):
+    """The one-stage dlatrd-style reduction (TG_EIGH_TWOSTAGE=0) stays correct."""
+    monkeypatch.setenv("TG_EIGH_TWOSTAGE", "0")
     test_eigh(lib, kind, n)
 
 
