@@ -33,6 +33,7 @@ struct SbPlan {
 struct SbBufs {
   double *Y, *T;          // reflector storage for all panels (persist until back-transform)
   double *YT, *X, *G, *M; // per-panel temporaries
+  double *YTl[SB_LV];     // Y T of TSQR levels >= 1 (computed on a side stream)
   double *R[2];           // TSQR R stacks (ping-pong between levels)
   double *Gr, *U;         // gathered rows / symmetric update (ncmax*32 x n)
   double *Xs;             // gathered rows of X (ncmax*32 x ncmax*32)
@@ -59,6 +60,7 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.Y, pl.ytotal + 1);
   take(b.T, pl.ttotal + 1);
   take(b.YT, size_t(n) * SB_B);
+  for (int l = 1; l < SB_LV; ++l) take(b.YTl[l], w * SB_B);
   take(b.X, size_t(n) * w);
   take(b.G, w * w);
   take(b.M, w * w);

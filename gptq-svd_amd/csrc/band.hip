@@ -23,6 +23,8 @@
 // for the back-transformation Z <- Q1 Z of the eigenvectors.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <utility>
 
 #include "band.h"
@@ -129,11 +131,10 @@ __device__ inline int rs_col(int lane) {
   return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
          ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
 }
-// q_l = v0 r0[l] + v1 r1[l] (0 for l == J), formed inside the first step.
-template <int J>
+// q_l = v0 r0[l] + v1 r1[l], formed inside the first step.
 __device__ inline double reduce_scatter32(const double (&r0)[32], const double (&r1)[32],
                                           double v0, double v1, int lane) {
-  auto qf = [&](int l) { return l == J ? 0.0 : v0 * r0[l] + v1 * r1[l]; };
+  auto qf = [&](int l) { return v0 * r0[l] + v1 * r1[l]; };
   double p[16];
   {
     const bool up = (lane & 32) != 0;
@@ -175,6 +176,37 @@ __device__ inline double reduce_scatter32(const double (&r0)[32], const double (
   return p[0] + xdpp<DPP_XOR1>(p[0]);
 }
 
+// Uniform-index access to a register array: a switch on the (scalar) index
+// keeps every access static, so the array stays in VGPRs.
+#define TG_CASES32(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
+  X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) \
+  X(28) X(29) X(30) X(31)
+__device__ inline void ugets(const double (&a)[32], const double (&b)[32], int j, double &x,
+                             double &y) {
+  switch (j) {
+#define TG_GET(k)  \
+  case k:          \
+    x = a[k];      \
+    y = b[k];      \
+    break;
+    TG_CASES32(TG_GET)
+#undef TG_GET
+    default: x = y = 0.0;
+  }
+}
+__device__ inline void usets(double (&a)[32], double (&b)[32], int j, double x, double y) {
+  switch (j) {
+#define TG_SET(k)  \
+  case k:          \
+    a[k] = x;      \
+    b[k] = y;      \
+    break;
+    TG_CASES32(TG_SET)
+#undef TG_SET
+    default: break;
+  }
+}
+
 // Householder QR of one leaf (chunk z of `m` rows, rows kb..ke of src, 32
 // columns, row stride ld).  Thread t holds rows t and t + 256 in registers
 // (rows >= h are zero, so every leaf runs exactly 32 steps: a zero
@@ -190,12 +222,15 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
                                                      double *__restrict__ Yo,
                                                      double *__restrict__ To,
                                                      double *__restrict__ Ro,
-                                                     double *__restrict__ YTo) {
+                                                     double *__restrict__ YTo,
+                                                     unsigned long long *__restrict__ qst) {
   __shared__ double prow[SB_B];
+  uint64_t ph[5] = {0, 0, 0, 0, 0};
   __shared__ double nrm[QT / 64];
   __shared__ double red[QT / 64][SB_B];
-  __shared__ double qv[SB_B];
+  __shared__ double qw[SB_B], taus[SB_B];
   __shared__ double Ts[SB_B][SB_B + 1];
+  __shared__ double Gs[SB_B][SB_B + 1];
   const int z = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kb = z * c, ke = (z == nc - 1) ? m : kb + c, h = ke - kb;
   double r0[SB_B], r1[SB_B];
@@ -213,9 +248,10 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
   load_row(tid + QT, r1);
   for (int idx = tid; idx < SB_B * (SB_B + 1); idx += QT) (&Ts[0][0])[idx] = 0.0;
   const int mycol = rs_col(lane);
-  auto step = [&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const double x0 = r0[j], x1 = r1[j];
+  for (int j = 0; j < SB_B; ++j) {
+    const uint64_t p0 = __builtin_amdgcn_s_memrealtime();
+    double x0, x1;
+    ugets(r0, r1, __builtin_amdgcn_readfirstlane(j), x0, x1);
     if (tid == j) {
 #pragma unroll
       for (int l = 0; l < SB_B; ++l) prow[l] = r0[l];
@@ -223,6 +259,7 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     const double s_w = wave_allsum(((tid > j) ? x0 * x0 : 0.0) + x1 * x1);
     if (lane == 0) nrm[wid] = s_w;
     __syncthreads();
+    const uint64_t p1 = __builtin_amdgcn_s_memrealtime();
     const double s = (nrm[0] + nrm[1]) + (nrm[2] + nrm[3]);
     const double alpha = prow[j];
     double tau = 0.0, scal = 0.0, beta = alpha;
@@ -233,32 +270,58 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     }
     const double v0 = (tid > j) ? x0 * scal : (tid == j ? 1.0 : 0.0);
     const double v1 = x1 * scal;
-    // q_l = sum_i v_i P[i][l]: l > j -> w_l, l < j -> (Y^T v)_l
-    const double q = reduce_scatter32<j>(r0, r1, v0, v1, lane);
+    // q_l = sum_i v_i P[i][l]: l > j -> w_l, l < j -> (Y^T v)_l (q_j is never used)
+    const double q = reduce_scatter32(r0, r1, v0, v1, lane);
+    const uint64_t p2 = __builtin_amdgcn_s_memrealtime();
     if ((lane & 1) == 0) red[wid][mycol] = q;
     __syncthreads();
-    if (tid < SB_B) qv[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    const uint64_t p3 = __builtin_amdgcn_s_memrealtime();
+    if (tid < SB_B) {
+      const double a = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+      qw[tid] = tid > j ? a : 0.0;
+      Gs[tid][j] = tid < j ? a : 0.0;  // (Y^T v_j)_tid, the T recurrence input
+    }
+    if (tid == 0) taus[j] = tau;
     __syncthreads();
+    const uint64_t p4 = __builtin_amdgcn_s_memrealtime();
     const double tv0 = tau * v0, tv1 = tau * v1;
 #pragma unroll
-    for (int l = j + 1; l < SB_B; ++l) {
-      const double w = qv[l];
+    for (int l = 0; l < SB_B; ++l) {
+      const double w = qw[l];
       r0[l] -= tv0 * w;
       r1[l] -= tv1 * w;
     }
-    r0[j] = (tid > j) ? v0 : (tid == j ? beta : r0[j]);
-    r1[j] = v1;
-    if (tid < j) {  // row tid of T: T[tid][j] = -tau sum_c T[tid][c] q_c (T[tid][c<tid] = 0)
-      double a = 0.0;
+    usets(r0, r1, __builtin_amdgcn_readfirstlane(j), (tid > j) ? v0 : (tid == j ? beta : x0), v1);
+    const uint64_t p5 = __builtin_amdgcn_s_memrealtime();
+    ph[0] += p1 - p0; ph[1] += p2 - p1; ph[2] += p3 - p2; ph[3] += p4 - p3; ph[4] += p5 - p4;
+  }
+  if (qst && tid == 0) {
+    for (int k = 0; k < 5; ++k) atomicAdd(qst + k, (unsigned long long)ph[k]);
+    atomicAdd(qst + 5, 1ull);
+  }
+  // T (dlarft, forward columnwise): row a is independent of the other rows:
+  // T[a][j] = -tau_j sum_{c<j} T[a][c] G[c][j], T[a][a] = tau_a, T[a][c<a] = 0.
+  __syncthreads();
+  if (tid < SB_B) {
+    double trow[SB_B];
 #pragma unroll
-      for (int cc = 0; cc < j; ++cc) a += Ts[tid][cc] * qv[cc];
-      Ts[tid][j] = -tau * a;
+    for (int c2 = 0; c2 < SB_B; ++c2) trow[c2] = 0.0;
+#pragma unroll
+    for (int j = 0; j < SB_B; ++j) {
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+      for (int c2 = 0; c2 < j; c2 += 4) {
+        a0 += trow[c2] * Gs[c2][j];
+        if (c2 + 1 < j) a1 += trow[c2 + 1] * Gs[c2 + 1][j];
+        if (c2 + 2 < j) a2 += trow[c2 + 2] * Gs[c2 + 2][j];
+        if (c2 + 3 < j) a3 += trow[c2 + 3] * Gs[c2 + 3][j];
+      }
+      const double tj = taus[j];
+      trow[j] = (tid < j) ? -tj * ((a0 + a1) + (a2 + a3)) : (tid == j ? tj : 0.0);
     }
-    if (tid == j) Ts[j][j] = tau;
-  };
-  [&]<int... J>(std::integer_sequence<int, J...>) {
-    (step(std::integral_constant<int, J>{}), ...);
-  }(std::make_integer_sequence<int, SB_B>{});
+#pragma unroll
+    for (int c2 = 0; c2 < SB_B; ++c2) Ts[tid][c2] = trow[c2];
+  }
   if (tid < SB_B) {
     double *ro = Ro + size_t(z) * SB_B * SB_B + tid * SB_B;
 #pragma unroll
@@ -291,8 +354,21 @@ hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int 
                      double *T, double *R, double *YT) {
   const int hmax = (nc == 1) ? m : std::max(SB_C, m - (nc - 1) * SB_C);
   if (hmax > 2 * QT) return hipErrorInvalidValue;
+  static unsigned long long *qst = nullptr;
+  static bool want = getenv("TG_QR_STATS") != nullptr;
+  if (want && !qst) {
+    (void)hipMalloc(&qst, 8 * sizeof(unsigned long long));
+    (void)hipMemset(qst, 0, 8 * sizeof(unsigned long long));
+    atexit([] {
+      unsigned long long h[8];
+      (void)hipMemcpy(h, qst, sizeof(h), hipMemcpyDeviceToHost);
+      fprintf(stderr, "qr per column (us): norm+bar %.2f  scal+rs %.2f  red+bar %.2f  qv+bar %.2f  upd+T %.2f (WGs %llu)\n",
+              h[0] / 100.0 / h[5] / 32, h[1] / 100.0 / h[5] / 32, h[2] / 100.0 / h[5] / 32,
+              h[3] / 100.0 / h[5] / 32, h[4] / 100.0 / h[5] / 32, h[5]);
+    });
+  }
   hipLaunchKernelGGL(tsqr_qr_kernel, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T, R,
-                     YT);
+                     YT, qst);
   return hipGetLastError();
 }
 
@@ -606,21 +682,56 @@ namespace tg {
     if (e_ != hipSuccess) return e_;  \
   } while (0)
 
+// Side stream + events for the TSQR levels >= 1 (created once per device).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
+};
+static hipError_t side_stream(SideStream *&out) {
+  static SideStream ss[64];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  SideStream &x = ss[dev & 63];
+  if (!x.s) {
+    if ((e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess) return e;
+    for (int i = 0; i < 2; ++i) {
+      if ((e = hipEventCreateWithFlags(&x.ev0[i], hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&x.ev1[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+  }
+  out = &x;
+  return hipSuccess;
+}
+
 hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b) {
+  SideStream *ss = nullptr;
+  TG_CHK(side_stream(ss));
+  int pi = 0;
   for (const SbPanel &P : pl.panels) {
     const int m = P.m, r0 = P.r0;
     double *A22 = A + int64_t(r0) * lda + r0;
     RowMap mp{};
     for (int l = 0; l < P.nl; ++l) mp.nc[l] = P.L[l].nc;
-    int rb = 0;
+    // level-0 QR on the main stream; levels >= 1 (QR of the stacked R's) on
+    // the side stream, overlapping level 0's two-sided update.
+    TG_CHK(launch_qr(st, A + int64_t(r0) * lda + P.p, lda, P.L[0].nc, m, b.Y + P.L[0].yoff,
+                     b.T + P.L[0].toff, b.R[0], b.YT));
+    const int ph = pi & 1;
+    if (P.nl > 1) {
+      TG_CHK(hipEventRecord(ss->ev0[ph], st));
+      TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[ph], 0));
+      for (int l = 1; l < P.nl; ++l) {
+        const SbLevel &L = P.L[l];
+        TG_CHK(launch_qr(ss->s, b.R[(l - 1) & 1], SB_B, L.nc, L.rows, b.Y + L.yoff, b.T + L.toff,
+                         b.R[l & 1], b.YTl[l]));
+      }
+      TG_CHK(hipEventRecord(ss->ev1[ph], ss->s));
+    }
     for (int l = 0; l < P.nl; ++l) {
       const SbLevel &L = P.L[l];
       double *Yl = b.Y + L.yoff, *Tl = b.T + L.toff;
       const int nc = L.nc, rows = L.rows, w = nc * SB_B;
-      if (l == 0)
-        TG_CHK(launch_qr(st, A + int64_t(r0) * lda + P.p, lda, nc, m, Yl, Tl, b.R[rb], b.YT));
-      else
-        TG_CHK(launch_qr(st, b.R[rb ^ 1], SB_B, nc, rows, Yl, Tl, b.R[rb], b.YT));
       mp.lv = l;
       if (l == 0) {
         // X = A22 blockdiag(YT)   (m x w)
@@ -634,14 +745,16 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
         hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
                            int64_t(lda), m, SB_C, nc, Yl, b.X, int64_t(w), b.M, int64_t(w));
         TG_CHK(hipGetLastError());
+        if (P.nl > 1) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));
       } else {
+        double *YTl = b.YTl[l];
         // Gr = A22[S, :]  (rows x m)
         hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
                            int64_t(lda), m, rows, mp, b.Gr);
         TG_CHK(hipGetLastError());
         // X = Gr^T blockdiag(YT)   (m x w)
         ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
-        TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, b.YT, SB_B, 0.0, b.X, w));
+        TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w));
         // Xs = X[S, :]  (rows x w)
         hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(w, 256), rows), dim3(256), 0, st, b.X,
                            int64_t(w), w, rows, mp, b.Xs);
@@ -664,11 +777,11 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
                            dim3(256), 0, st, A22, int64_t(lda), m, rows, mp, b.U, 1);
         TG_CHK(hipGetLastError());
       }
-      rb ^= 1;
     }
     hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, st, A,
-                       int64_t(lda), P.p, r0, m, b.R[rb ^ 1]);
+                       int64_t(lda), P.p, r0, m, b.R[(P.nl - 1) & 1]);
     TG_CHK(hipGetLastError());
+    ++pi;
   }
   return hipSuccess;
 }

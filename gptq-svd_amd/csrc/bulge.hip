@@ -43,9 +43,22 @@ __device__ inline double xchg16(double x) {
   const bool up = (threadIdx.x & 16) != 0;
   return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
 }
-__device__ inline double wsum(double s) {  // full wave sum, result in every lane
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+template <int CTRL>
+__device__ inline double xdpp(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Full wave sum in every lane without the LDS crossbar: pairings lane^32,
+// lane^16 (permlane swaps), lane^15 / lane^7 (DPP row mirrors), lane^3,
+// lane^1 (quad_perm) flip a new bit each.
+__device__ inline double wsum(double s) {
+  s += xchg32(s);
+  s += xchg16(s);
+  s += xdpp<0x140>(s);
+  s += xdpp<0x141>(s);
+  s += xdpp<0x1B>(s);
+  s += xdpp<0xB1>(s);
   return s;
 }
 
@@ -68,7 +81,8 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // ---------------------------------------------------------------------------
 constexpr int G_SW = 2;              // sweeps per group (waves per workgroup)
 constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
-constexpr int BT = 128 * G_SW;       // threads per workgroup (a wave pair per sweep)
+constexpr int NCW = 2 * G_SW;        // compute waves (a wave pair per sweep)
+constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
 
 struct WaveScratch {
   double vs[SB_B];
@@ -85,9 +99,8 @@ __device__ inline int rslot(int c) { return c & (RING - 1); }
 
 // Task (j, s) by a pair of waves on the LDS ring (element (r, c) at
 // R[slot(c)][r - c]).  Both waves form the reflector from x = B[R, col]; then
-// role 0 applies it to the left block A = B[R, Lft] and rows 0..15 of the
-// lower block G = B[Rgt, R], role 1 to the diagonal block D = B[R, R] and
-// rows 16..31 of G.  The three blocks are disjoint, so the waves never talk.
+// role 0 applies it to the left block A = B[R, Lft] and the
+// lower block G = B[Rgt, R], role 1 to the diagonal block D = B[R, R].  The three blocks are disjoint, so the waves never talk.
 template <bool FULL>
 __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, int s, int role,
                                                double *__restrict__ V2,
@@ -105,8 +118,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
   const double x = (FULL || li < L) ? Rf[at(col, r1 + min(li, L - 1) - col)] : 0.0;
   // block loads (issued before the reflector's reductions)
   double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li, k = hf + 2q)
-  double g[8];   // G rows gr = 16 role + (lane & 15), columns k = (lane >> 4) + 4q
-  const int gr = 16 * role + (lane & 15), gk0 = lane >> 4;
+  double g[16];  // role 0: G (lane row li, k = hf + 2q)
   if (role == 0) {
     const int ca = FULL ? li : min(li, max(nl - 1, 0));
     const int abase = at(lo + ca, r1 - lo - ca);
@@ -125,14 +137,16 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       else e[q] = (li < L && k < L) ? Rf[at(r1 + min(cc, L - 1), off)] : 0.0;
     }
   }
+  if (role == 0) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int k = gk0 + 4 * q;
-    if (FULL) g[q] = Rf[at(r1 + k, SB_B + gr - k)];
-    else {
-      const int kc = min(k, L - 1);
-      const double gv = Rf[at(r1 + kc, L + min(gr, max(ng - 1, 0)) - kc)];
-      g[q] = (gr < ng && k < L) ? gv : 0.0;
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      if (FULL) g[q] = Rf[at(r1 + k, SB_B + li - k)];
+      else {
+        const int kc = min(k, L - 1);
+        const double gv = Rf[at(r1 + kc, L + min(li, max(ng - 1, 0)) - kc)];
+        g[q] = (li < ng && k < L) ? gv : 0.0;
+      }
     }
   }
   // reflector (identical in both waves)
@@ -147,18 +161,20 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
   const double v = (li == 0) ? 1.0 : ((FULL || li < L) ? x * scal : 0.0);
   if (hf == 0) W.vs[li] = v;
   wave_sync();
-  double vk[16], vg[8];
+  double vk[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) vk[q] = W.vs[hf + 2 * q];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) vg[q] = W.vs[gk0 + 4 * q];
-  // lower block rows: u_r = sum_k G[r][k] v_k, G -= tau u v^T
-  double u = 0.0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) u += g[q] * vg[q];
-  u += xchg16(u);
-  u += xchg32(u);
   if (role == 0) {
+    // lower block: u_r = sum_k G[r][k] v_k, G -= tau u v^T (row r = li)
+    double u = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u += g[q] * vk[q];
+    u += xchg32(u);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = g[q] - tau * u * vk[q];
+    }
     // left block: w_c = sum_i v_i A[i][c]
     double wc = 0.0;
 #pragma unroll
@@ -191,11 +207,6 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       const int k = hf + 2 * q;
       if ((FULL || li < L) && k <= li) Rf[at(r1 + k, li - k)] = e[q] - v * W.ws[k] - w * vk[q];
     }
-  }
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int k = gk0 + 4 * q;
-    if (FULL || (gr < ng && k < L)) Rf[at(r1 + k, L + gr - k)] = g[q] - tau * u * vg[q];
   }
 }
 
@@ -254,6 +265,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(B, 0, bytes, 0x00020000);
   constexpr int SC1 = 16;
   const int nthr_col = LDB / 2;  // threads per column for 16-B transfers
+  constexpr int nthr_col_c = LDB / 2;
   while (true) {
     if (tid == 0) sh_G = int(atomicAdd(ctl + 1, 1u));
     __syncthreads();
@@ -329,49 +341,95 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     }
     ld = group_high(n, j0, 0);
     __syncthreads();
+    const int wlane = tid & 63;
     for (int t = 0; t < total; ++t) {
-      // prefetch the columns step t + 1 adds
-      const int nh = group_high(n, j0, t + 1);
-      const bool pre = t + 1 < total && nh > ld;
-      if (pre) {
-        wait_for(t + 1 + 3 * G_SW);
-        load_cols(ld, nh);
-      }
       const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
-      const int pair = wid >> 1, role = wid & 1;
-      const int s = t - 3 * pair;
-      if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
-        const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
-        if (r1 >= SB_B && r1 + 2 * SB_B <= n)
-          bulge_task_lds<true>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
-        else
-          bulge_task_lds<false>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+      if (wid < NCW) {
+        const int pair = wid >> 1, role = wid & 1;
+        const int s = t - 3 * pair;
+        if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
+          const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
+          if (r1 >= SB_B && r1 + 2 * SB_B <= n)
+            bulge_task_lds<true>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+          else
+            bulge_task_lds<false>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+        }
+      } else if (wid == NCW) {
+        // writer: retire the columns step t-1 left behind, drain, publish t
+        const int nl = group_low(n, nsw, j0, g, t);
+        if (nl > wb) {
+          for (int idx = wlane; idx < (nl - wb) * nthr_col; idx += 64) {
+            const int c = wb + idx / nthr_col, h = idx % nthr_col;
+            const double2 v = make_double2(R[rslot(c)][2 * h], R[rslot(c)][2 * h + 1]);
+            const u32x2 lo2 = __builtin_bit_cast(u32x2, v.x), hi2 = __builtin_bit_cast(u32x2, v.y);
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                   (c * LDB + 2 * h) * 8, 0, 0);
+          }
+          wb = nl;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wlane == 0)
+          __hip_atomic_store(prog + G, unsigned(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        // loader: columns step t + 1 adds
+        const int nh = group_high(n, j0, t + 1);
+        if (t + 1 < total && nh > ld) {
+          const int need = min(t + 1 + 3 * G_SW, ptotal + 1);
+          if (G > 0 && known < need) {
+            if (wlane == 0) {
+              const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+              while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                     unsigned(need)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up
+                  __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+                }
+              }
+            }
+            known = need;
+            __builtin_amdgcn_wave_barrier();
+          }
+          constexpr int PW = SB_B * nthr_col_c / 64;  // 16-B chunks per lane
+          double2 buf[PW];
+#pragma unroll
+          for (int u = 0; u < PW; ++u) {
+            const int idx = wlane + 64 * u;
+            const int c = min(ld + idx / nthr_col, nh - 1), h = idx % nthr_col;
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
+            buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                                  __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+          }
+#pragma unroll
+          for (int u = 0; u < PW; ++u) {
+            const int idx = wlane + 64 * u;
+            const int c = ld + idx / nthr_col, h = idx % nthr_col;
+            if (c < nh) {
+              R[rslot(c)][2 * h] = buf[u].x;
+              R[rslot(c)][2 * h + 1] = buf[u].y;
+            }
+          }
+        }
+        if (t + 1 < total) ld = max(ld, nh);
       }
       const uint64_t c1t = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
+      // every wave tracks ld / wb (only the I/O waves act on them)
+      if (wid != NCW + 1 && t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
+      if (wid != NCW) wb = max(wb, group_low(n, nsw, j0, g, t));
       const uint64_t c2t = __builtin_amdgcn_s_memrealtime();
-      if (pre) {
-        store_pf(ld, nh);
-        ld = nh;
-      }
-      const uint64_t c3t = __builtin_amdgcn_s_memrealtime();
       stk += c1t - c0t;
       sbar += c2t - c1t;
-      spf += c3t - c2t;
       ++nsteps;
-      // progress t: steps < t are complete and their write-backs drained
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      swb += __builtin_amdgcn_s_memrealtime() - c3t;
-      if (tid == 0)
-        __hip_atomic_store(prog + G, unsigned(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // retire columns no later task touches (drained at the end of the next step)
-      const int nl = (t + 1 < total) ? group_low(n, nsw, j0, g, t + 1) : ld;
-      if (nl > wb) {
-        write_back(wb, min(nl, ld));
-        wb = min(nl, ld);
+      if ((tid & 63) == 0) {
+        __shared__ unsigned long long wt[8];
+        if (t == 0 && G == sh_G) {}
+        (void)wt;
+        if (stats) atomicAdd(stats + 8 + wid, (unsigned long long)(c1t - c0t));
       }
     }
+    // group end: write back what is left, drain, publish done
     if (wb < ld) write_back(wb, ld);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -428,8 +486,8 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     const bool want = getenv("TG_BULGE_STATS") != nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (want) {
-      (void)hipMalloc(&stats, 8 * sizeof(unsigned long long));
-      (void)hipMemsetAsync(stats, 0, 8 * sizeof(unsigned long long), st);
+      (void)hipMalloc(&stats, 16 * sizeof(unsigned long long));
+      (void)hipMemsetAsync(stats, 0, 16 * sizeof(unsigned long long), st);
       (void)hipEventCreate(&e0);
       (void)hipEventCreate(&e1);
       (void)hipEventRecord(e0, st);
@@ -440,7 +498,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     if (err != hipSuccess) return err;
     if (want) {
       (void)hipEventRecord(e1, st);
-      unsigned long long h[8];
+      unsigned long long h[16];
       (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
       (void)hipStreamSynchronize(st);
       float ms = 0.f;
@@ -451,6 +509,9 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
               "bar %.2f pfstore %.2f wb %.2f\n",
               ms, W, S / W, h[1] / 100.0 / S, h[2] / 100.0 / S, h[3] / 100.0 / S, h[4] / 100.0 / S,
               h[5] / 100.0 / S);
+      fprintf(stderr, "  per-wave busy per step (us):");
+      for (int w = 0; w < NCW + 2; ++w) fprintf(stderr, " w%d %.2f", w, h[8 + w] / 100.0 / S);
+      fprintf(stderr, "\n");
       (void)hipFree(stats);
     }
   }
