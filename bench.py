@@ -36,6 +36,7 @@ PEAKS = {  # MI355X_MICROARCH.md chip table (spec / dense)
     "hbm": ("GB/s", 8000.0),
     "fp32_mfma": ("TFLOP/s", 157.3),
     "fp64_mfma": ("TFLOP/s", 78.6),
+    "fp64": ("TFLOP/s", 78.6),  # FP64 vector peak = FP64 matrix peak on MI355X
 }
 # kernel class -> roofline it is bound by
 BOUND = {
@@ -47,6 +48,11 @@ BOUND = {
     "bisect": ("hbm", "bytes"),
     "inverse_iteration": ("hbm", "bytes"),
     "back_transform": ("fp64_mfma", "flops"),
+    "bulge_chase": ("fp64", "flops"),     # latency-bound pipeline (3n dependent tasks)
+    "tsqr_leaf": ("fp64", "flops"),       # latency-bound (32 dependent columns)
+    "band_update": ("hbm", "bytes"),
+    "q1_apply": ("hbm", "bytes"),
+    "q2_apply": ("hbm", "bytes"),
 }
 
 
@@ -258,6 +264,7 @@ def main():
         else:
             achieved = per_launch / (avg_ms * 1e-3) / 1e12
         roof = dict(kernel=name, bound="hbm" if kind == "hbm" else "mfma",
+                    peak_kind=kind,
                     achieved=round(achieved, 3), peak=peak, unit=unit,
                     frac=round(achieved / peak, 4), traffic=None,
                     avg_launch_ms=round(avg_ms, 5), launches_per_step=p["launches"] // args.steps)

@@ -71,7 +71,8 @@ DTYPES = {torch.float16: TG_F16, torch.bfloat16: TG_BF16, torch.float32: TG_F32,
 
 
 PROF_CLASSES = ["tri_symv", "cross_gemm", "quant_block", "tri_syr2k", "pivot_step", "bisect",
-                "inverse_iteration", "back_transform"]
+                "inverse_iteration", "back_transform", "bulge_chase", "tsqr_leaf", "band_update",
+                "q1_apply", "q2_apply"]
 
 
 def profile_enable(on: bool = True, every: int = 1) -> None:

@@ -354,6 +354,8 @@ hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int 
                      double *T, double *R, double *YT) {
   const int hmax = (nc == 1) ? m : std::max(SB_C, m - (nc - 1) * SB_C);
   if (hmax > 2 * QT) return hipErrorInvalidValue;
+  // Householder QR of the nc leaves: ~2 h b^2 flops per leaf
+  auto tok = tg::prof_begin(st, tg::PROF_TSQR, 16.0 * m * SB_B, 2.0 * m * SB_B * SB_B);
   static unsigned long long *qst = nullptr;
   static bool want = getenv("TG_QR_STATS") != nullptr;
   if (want && !qst) {
@@ -369,6 +371,7 @@ hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int 
   }
   hipLaunchKernelGGL(tsqr_qr_kernel, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T, R,
                      YT, qst);
+  tg::prof_end(st, tok);
   return hipGetLastError();
 }
 
@@ -742,8 +745,11 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
                            int64_t(w), w, SB_C, nc, m, mp, b.M, int64_t(w));
         TG_CHK(hipGetLastError());
         const int nt = cdiv(m, S2T);
+        // HBM: lower tiles of A22 read, both triangles written (1.5 m^2 doubles)
+        auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
         hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
                            int64_t(lda), m, SB_C, nc, Yl, b.X, int64_t(w), b.M, int64_t(w));
+        prof_end(st, tok);
         TG_CHK(hipGetLastError());
         if (P.nl > 1) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));
       } else {
@@ -797,6 +803,8 @@ hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl
     for (int l = P.nl - 1; l >= 0; --l) {  // Q = D_0 E_1 E_2 ...: top level first
       const SbLevel &L = P.L[l];
       mp.lv = l;
+      // HBM: read + write of the level's rows of Z
+      auto tok = prof_begin(st, PROF_Q1, 16.0 * double(L.rows) * k, 4.0 * double(L.rows) * SB_B * k);
       if (l > 0)
         hipLaunchKernelGGL((ytz_kernel<1, true>), dim3(cdiv(k, SB_B), L.nc), dim3(512), 0, st,
                            b.Y + L.yoff, b.T + L.toff, Zs, int64_t(k), k, SB_C, L.nc, L.rows, mp,
@@ -805,6 +813,7 @@ hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl
         hipLaunchKernelGGL((ytz_kernel<1, false>), dim3(cdiv(k, SB_B), L.nc), dim3(512), 0, st,
                            b.Y + L.yoff, b.T + L.toff, Zs, int64_t(k), k, SB_C, L.nc, L.rows, mp,
                            nullptr, int64_t(0));
+      prof_end(st, tok);
       TG_CHK(hipGetLastError());
     }
   }

@@ -492,8 +492,15 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       (void)hipEventCreate(&e1);
       (void)hipEventRecord(e0, st);
     }
+    // ~12.3 kflop per task (3 blocks of b x b, rank-1 each), n^2/(2b) tasks;
+    // band streamed once per sweep group (load + write-back, L2-resident)
+    double ntask = 0.0;
+    for (int j = 0; j < nsw; ++j) ntask += (n - 3 - j) / SB_B + 1;
+    auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / G_SW,
+                          12.0 * SB_B * SB_B * ntask);
     hipLaunchKernelGGL(bulge_lds_kernel, dim3(256), dim3(BT), 0, st, Bst, n, V2, tau2, sb_smax(n),
                        prog, ctl, stats);
+    tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;
     if (want) {
@@ -729,8 +736,11 @@ hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2
   for (int level = 0; level < nlev; ++level) {
     const int s_lo = std::max(0, level - (ng2 - 1)), s_hi = std::min(smax - 1, level);
     if (s_hi < s_lo) continue;
+    const double rows = double(s_hi - s_lo + 1) * QR;
+    auto tok = tg::prof_begin(st, tg::PROF_Q2, 16.0 * rows * k, 4.0 * rows * QB * k + 2.0 * QB * QB * k);
     hipLaunchKernelGGL(q2_apply_kernel, dim3(cdiv(k, 128), s_hi - s_lo + 1), dim3(256), 0, st, Z,
                        k, n, V2, T2, smax, ng2, level, s_lo);
+    tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;
   }

@@ -41,7 +41,9 @@ __host__ __device__ inline int cdiv(int64_t a, int64_t b) { return int((a + b - 
 // profiling is on, every `every`-th launch of the class is bracketed by events
 // and its algorithmic bytes / flops are recorded for roofline reporting.
 enum ProfId { PROF_TRI_SYMV = 0, PROF_CROSS_GEMM = 1, PROF_QBLOCK = 2, PROF_SYR2K = 3,
-              PROF_PIVSTEP = 4, PROF_BISECT = 5, PROF_INVIT = 6, PROF_BACKTR = 7, PROF_N = 8 };
+              PROF_PIVSTEP = 4, PROF_BISECT = 5, PROF_INVIT = 6, PROF_BACKTR = 7,
+              PROF_BULGE = 8, PROF_TSQR = 9, PROF_SBUPD = 10, PROF_Q1 = 11, PROF_Q2 = 12,
+              PROF_N = 13 };
 struct ProfTok {
   int id = -1;
   int slot = -1;

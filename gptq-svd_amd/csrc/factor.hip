@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "../../include/truncgptq.h"
@@ -46,7 +47,11 @@ struct PivWs {
   int32_t *perm; // n      position -> original index
   int32_t *pos;  // n      original index -> position
   unsigned *cnt;
+  double *pp;    // PGMAX x PPS  per-workgroup step partials (value, position, row, L row)
+  double *bc;    // PPS          last arriver's broadcast (pivot, its L row, swap)
+  unsigned *flag;
 };
+constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
 
 template <class A>
 void piv_layout(A &ar, int n, int k, PivWs *p) {
@@ -58,6 +63,9 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
     else ar.template take<T>(cnt);
   };
   take(q.B, size_t(k) * n);
+  take(q.pp, size_t(2) * PGMAX * PPS);
+  take(q.bc, PPS);
+  take(q.flag, 16);
   take(q.Hk, size_t(n) * n);
   take(q.dsc, n);
   take(q.L, size_t(n) * k);
@@ -199,6 +207,229 @@ __global__ __launch_bounds__(256) void piv_step_kernel(int n, int k, int i, int 
   if (i + 1 < k) argmax_publish(bv, bp, i + 1, n, w);
 }
 
+// Persistent form of the pivot steps of one panel (steps ps .. pe-1): one
+// launch instead of one per pivot.  Thread (block b, lane x) owns rows
+// r = (b * 256 + x) + u * G * 256 (u < RPT) and keeps their panel of L in
+// registers.  Per step every workgroup publishes its best candidate (Schur
+// diagonal, dgeqp3 position, row, and that row's panel of L) with sc1 stores
+// and takes an arrival ticket; the last arriver does dgeqp3's swap
+// bookkeeping and broadcasts the next pivot (its diagonal, row and L panel)
+// plus the swapped pair; the others poll the broadcast flag.  All
+// cross-workgroup data moves by sc1 stores + vmcnt(0) + flag/ticket and sc1
+// loads (MI355X_MICROARCH.md "Valid forms"), so placement does not matter.
+__device__ inline double ld1(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st1(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline int ld1i(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st1i(int32_t *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Worker selection: the launch has at least 8 (G - 1) + 1 workgroups; each
+// takes a ticket on its XCD (HW_REG_XCC_ID) and the first XCD to hand out G
+// tickets becomes the worker set (pigeonhole: one always does); the others
+// exit.  Workers then hand data over through that XCD's L2: plain stores +
+// vmcnt(0) + agent atomic ticket, sc1 (L1-bypassing) loads.
+template <int RPT>
+__global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, int pe, int G,
+                                                        PivWs w) {
+  extern __shared__ int permL[];  // n: position -> row (every workgroup keeps a copy)
+  __shared__ double sv[4], lrow[PB + 1];
+  __shared__ int spos[4], swin[4], s_g, s_me;
+  __shared__ double s_best;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned *xc = w.flag + 4;  // [0..7] tickets per XCD, [8] chosen XCD + 1
+    const unsigned tk = __hip_atomic_fetch_add(xc + (x & 7), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    int me = -1;
+    if (tk < unsigned(G)) {
+      if (tk == unsigned(G) - 1) {
+        unsigned expect = 0;
+        __hip_atomic_compare_exchange_strong(xc + 8, &expect, x + 1, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unsigned ch;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((ch = __hip_atomic_load(xc + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;
+      }
+      if (ch == x + 1) me = int(tk);
+    }
+    s_me = me;
+  }
+  __syncthreads();
+  const int me = s_me;
+  if (me < 0) return;
+  for (int x = tid; x < n; x += 256) permL[x] = w.perm[x];
+  const unsigned base = __hip_atomic_load(w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int rows[RPT], posr[RPT];
+  double dsr[RPT], lr[RPT][PB];
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    rows[u] = me * 256 + tid + u * G * 256;
+    const bool ok = rows[u] < n;
+    posr[u] = ok ? w.pos[rows[u]] : n;
+    dsr[u] = ok ? w.dsc[rows[u]] : 0.0;
+#pragma unroll
+    for (int l = 0; l < PB; ++l) lr[u][l] = 0.0;
+  }
+  __syncthreads();
+  int piv = permL[ps];
+  double dpiv = w.dsc[piv];
+  for (int i = ps; i < pe; ++i) {
+    const int t = i - ps;
+    const double ljj = sqrt(fmax(dpiv, 0.0));
+    const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
+    const double *hrow = w.Hk + size_t(piv) * n;
+    double bv = -INFINITY;
+    int bp = n, bu = -1;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int r = rows[u];
+      if (r >= n) continue;
+      if (r == piv) {  // the pivot row itself
+        w.L[size_t(r) * k + i] = ljj;
+        w.LT[size_t(t) * n + r] = ljj;
+#pragma unroll
+        for (int l = 0; l < PB; ++l)
+          if (l == t) lr[u][l] = ljj;
+        continue;
+      }
+      if (posr[u] <= i) continue;
+      double v = hrow[r];
+#pragma unroll
+      for (int l = 0; l < PB; ++l) v -= l < t ? lr[u][l] * lrow[l] : 0.0;
+      const double lv = v * inv;
+      w.L[size_t(r) * k + i] = lv;
+      w.LT[size_t(t) * n + r] = lv;
+#pragma unroll
+      for (int l = 0; l < PB; ++l)
+        if (l == t) lr[u][l] = lv;
+      dsr[u] -= lv * lv;
+      if (dsr[u] > bv || (dsr[u] == bv && posr[u] < bp)) {
+        bv = dsr[u];
+        bp = posr[u];
+        bu = u;
+      }
+    }
+    if (i + 1 >= k) break;  // dgeqp3 stops after k steps: no swap into position k
+    // workgroup candidate (largest diagonal, first dgeqp3 position)
+    int bw = tid;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(bv, off);
+      const int op = __shfl_xor(bp, off), ow = __shfl_xor(bw, off);
+      if (ov > bv || (ov == bv && op < bp)) {
+        bv = ov;
+        bp = op;
+        bw = ow;
+      }
+    }
+    if (lane == 0) {
+      sv[wid] = bv;
+      spos[wid] = bp;
+      swin[wid] = bw;
+    }
+    __syncthreads();
+    int wq = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (sv[q] > sv[wq] || (sv[q] == sv[wq] && spos[q] < spos[wq])) wq = q;
+    // publish: value, position, row, the row's L panel (slot parity = step parity)
+    double *mine = w.pp + (size_t(i & 1) * PGMAX + me) * PPS;
+    if (tid == swin[wq] && bu >= 0) {
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        if (u == bu) {
+          mine[2] = double(rows[u]);
+#pragma unroll
+          for (int l = 0; l < PB; ++l)
+            if (l <= t) mine[8 + l] = lr[u][l];
+        }
+    }
+    if (tid == 0) {
+      mine[0] = sv[wq];
+      mine[1] = double(spos[wq]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // all-to-all: wait for every workgroup's candidate of this step
+    if (tid == 0) {
+      __hip_atomic_fetch_add(w.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = base + unsigned(G) * unsigned(t + 1);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // 2 s: give up
+      }
+    }
+    __syncthreads();
+    const double *slots = w.pp + size_t(i & 1) * PGMAX * PPS;
+    if (wid == 0) {
+      double v = -INFINITY;
+      int p2 = n, g = lane;
+      if (lane < G) {
+        v = ld1(slots + size_t(lane) * PPS);
+        p2 = int(ld1(slots + size_t(lane) * PPS + 1));
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(v, off);
+        const int op = __shfl_xor(p2, off), og = __shfl_xor(g, off);
+        if (ov > v || (ov == v && (op < p2 || (op == p2 && og < g)))) {
+          v = ov;
+          p2 = op;
+          g = og;
+        }
+      }
+      if (lane == 0) {
+        s_best = v;
+        s_g = g;
+        spos[0] = p2;
+      }
+    }
+    __syncthreads();
+    const int g = s_g, q = spos[0];
+    const double *win = slots + size_t(g) * PPS;
+    if (tid <= t) lrow[tid] = ld1(win + 8 + tid);
+    if (tid == 64) sv[0] = ld1(win + 2);
+    __syncthreads();
+    const int rowb = int(sv[0]);
+    const int a = permL[i + 1];
+    __syncthreads();
+    if (tid == 0 && q != i + 1) {  // dgeqp3 swap of positions i+1 and q (every copy)
+      permL[i + 1] = rowb;
+      permL[q] = a;
+      if (me == 0) {
+        w.perm[i + 1] = rowb;
+        w.perm[q] = a;
+        w.pos[rowb] = i + 1;
+        w.pos[a] = q;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      if (rows[u] == rowb) posr[u] = i + 1;
+      else if (rows[u] == a && q != i + 1) posr[u] = q;
+    }
+    dpiv = s_best;
+    piv = rowb;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < RPT; ++u)
+    if (rows[u] < n) w.dsc[rows[u]] = dsr[u];
+}
+
 // Rx[t][j] = L[perm[j]][t] for j >= t (upper trapezoidal), perm64 = perm.
 __global__ void rx_gather_kernel(int n, int k, PivWs w, double *__restrict__ Rx, int ldr,
                                  int64_t *__restrict__ perm64) {
@@ -316,14 +547,38 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
   const int g0 = std::min(PGMAX, tg::cdiv(n, 256));
   hipLaunchKernelGGL(piv_init_kernel, dim3(g0), dim3(256), 0, st, n, w);
   TG_LAUNCHED();
+  const int G = std::max(1, std::min(PGMAX, tg::cdiv(n, 256)));
+  const int rpt = tg::cdiv(n, G * 256);
+  const bool persistent = rpt <= 2 && n <= 32768 && getenv("TG_PIVOT_STEPWISE") == nullptr;
+  if (persistent && n * sizeof(int) > 64 * 1024) {
+    TG_HIP(hipFuncSetAttribute((const void *)piv_panel_kernel<1>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(n * sizeof(int))));
+    TG_HIP(hipFuncSetAttribute((const void *)piv_panel_kernel<2>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(n * sizeof(int))));
+  }
+  TG_HIP(hipMemsetAsync(w.flag, 0, 16 * sizeof(unsigned), st));
+  // the arrival counter of the panel kernels starts at 0 after piv_init
   for (int ps = 0; ps < k; ps += PB) {
     const int pe = std::min(ps + PB, k);
-    for (int i = ps; i < pe; ++i) {
-      const int g = std::max(1, std::min(PGMAX, tg::cdiv(n, 256)));
-      auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n - i) * (i - ps + 3), 0.0);
-      hipLaunchKernelGGL(piv_step_kernel, dim3(g), dim3(256), 0, st, n, k, i, ps, w);
+    if (persistent) {
+      // per-panel: n rows x (PB/2 + 3) doubles of H row, L panel and diagonal
+      auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n) * (pe - ps) * 3, 0.0);
+      const size_t lds = sizeof(int) * size_t(n);
+      TG_HIP(hipMemsetAsync(w.flag + 4, 0, 9 * sizeof(unsigned), st));
+      const int grid = 8 * G;  // >= 8 (G - 1) + 1: some XCD always collects G tickets
+      if (rpt == 1)
+        hipLaunchKernelGGL(piv_panel_kernel<1>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G, w);
+      else
+        hipLaunchKernelGGL(piv_panel_kernel<2>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G, w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
+    } else {
+      for (int i = ps; i < pe; ++i) {
+        auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n - i) * (i - ps + 3), 0.0);
+        hipLaunchKernelGGL(piv_step_kernel, dim3(G), dim3(256), 0, st, n, k, i, ps, w);
+        tg::prof_end(st, tok);
+        TG_LAUNCHED();
+      }
     }
     if (pe < k)  // Schur update with this panel's columns (all rows, original order)
       TG_HIP(tg::dsyrk_tn(st, n, pe - ps, -1.0, w.LT, n, 1.0, w.Hk, n));
