@@ -248,10 +248,10 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
   load_row(tid + QT, r1);
   for (int idx = tid; idx < SB_B * (SB_B + 1); idx += QT) (&Ts[0][0])[idx] = 0.0;
   const int mycol = rs_col(lane);
-  for (int j = 0; j < SB_B; ++j) {
+  auto step = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
     const uint64_t p0 = __builtin_amdgcn_s_memrealtime();
-    double x0, x1;
-    ugets(r0, r1, __builtin_amdgcn_readfirstlane(j), x0, x1);
+    const double x0 = r0[j], x1 = r1[j];
     if (tid == j) {
 #pragma unroll
       for (int l = 0; l < SB_B; ++l) prow[l] = r0[l];
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     const uint64_t p3 = __builtin_amdgcn_s_memrealtime();
     if (tid < SB_B) {
       const double a = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-      qw[tid] = tid > j ? a : 0.0;
+      qw[tid] = a;
       Gs[tid][j] = tid < j ? a : 0.0;  // (Y^T v_j)_tid, the T recurrence input
     }
     if (tid == 0) taus[j] = tau;
@@ -286,15 +286,19 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     const uint64_t p4 = __builtin_amdgcn_s_memrealtime();
     const double tv0 = tau * v0, tv1 = tau * v1;
 #pragma unroll
-    for (int l = 0; l < SB_B; ++l) {
+    for (int l = j + 1; l < SB_B; ++l) {
       const double w = qw[l];
       r0[l] -= tv0 * w;
       r1[l] -= tv1 * w;
     }
-    usets(r0, r1, __builtin_amdgcn_readfirstlane(j), (tid > j) ? v0 : (tid == j ? beta : x0), v1);
+    r0[j] = (tid > j) ? v0 : (tid == j ? beta : x0);
+    r1[j] = v1;
     const uint64_t p5 = __builtin_amdgcn_s_memrealtime();
     ph[0] += p1 - p0; ph[1] += p2 - p1; ph[2] += p3 - p2; ph[3] += p4 - p3; ph[4] += p5 - p4;
-  }
+  };
+  [&]<int... J>(std::integer_sequence<int, J...>) {
+    (step(std::integral_constant<int, J>{}), ...);
+  }(std::make_integer_sequence<int, SB_B>{});
   if (qst && tid == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(qst + k, (unsigned long long)ph[k]);
     atomicAdd(qst + 5, 1ull);

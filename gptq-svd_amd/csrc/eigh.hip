@@ -39,7 +39,7 @@ constexpr int SYT = 1024; // symv threads per workgroup
 constexpr int BT = 64;    // back-transformation block of reflectors
 constexpr int PST = 2 * NB + 2;  // partials stride
 constexpr int ML = 16;    // multisection lanes per eigenvalue
-constexpr int ROUNDS = 16;  // 17^16 > 2^65: interval shrinks below one ulp
+constexpr int ROUNDS = 14;  // 17^14 > 2^57: the Gershgorin interval shrinks below one ulp
 constexpr int SPLITK = 8;
 
 struct Tri {

@@ -237,7 +237,7 @@ __device__ inline void st1i(int32_t *p, int v) {
 // vmcnt(0) + agent atomic ticket, sc1 (L1-bypassing) loads.
 template <int RPT>
 __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, int pe, int G,
-                                                        PivWs w) {
+                                                        unsigned base, PivWs w) {
   extern __shared__ int permL[];  // n: position -> row (every workgroup keeps a copy)
   __shared__ double sv[4], lrow[PB + 1];
   __shared__ int spos[4], swin[4], s_g, s_me;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
   const int me = s_me;
   if (me < 0) return;
   for (int x = tid; x < n; x += 256) permL[x] = w.perm[x];
-  const unsigned base = __hip_atomic_load(w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // base = arrivals of earlier panel launches (G per step before ps), from the host
   int rows[RPT], posr[RPT];
   double dsr[RPT], lr[RPT][PB];
 #pragma unroll
@@ -367,12 +367,18 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
       __hip_atomic_fetch_add(w.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = base + unsigned(G) * unsigned(t + 1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      s_me = 0;
       while (__hip_atomic_load(w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // 2 s: give up
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: abandon, flag it
+          __hip_atomic_store(w.flag + 15, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_me = -1;
+          break;
+        }
       }
     }
     __syncthreads();
+    if (s_me < 0) return;
     const double *slots = w.pp + size_t(i & 1) * PGMAX * PPS;
     if (wid == 0) {
       double v = -INFINITY;
@@ -398,12 +404,12 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
       }
     }
     __syncthreads();
-    const int g = s_g, q = spos[0];
+    const int g = min(max(s_g, 0), G - 1), q = min(max(spos[0], i + 1), n - 1);
     const double *win = slots + size_t(g) * PPS;
     if (tid <= t) lrow[tid] = ld1(win + 8 + tid);
     if (tid == 64) sv[0] = ld1(win + 2);
     __syncthreads();
-    const int rowb = int(sv[0]);
+    const int rowb = min(max(int(sv[0]), 0), n - 1);
     const int a = permL[i + 1];
     __syncthreads();
     if (tid == 0 && q != i + 1) {  // dgeqp3 swap of positions i+1 and q (every copy)
@@ -567,9 +573,11 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
       TG_HIP(hipMemsetAsync(w.flag + 4, 0, 9 * sizeof(unsigned), st));
       const int grid = 8 * G;  // >= 8 (G - 1) + 1: some XCD always collects G tickets
       if (rpt == 1)
-        hipLaunchKernelGGL(piv_panel_kernel<1>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G, w);
+        hipLaunchKernelGGL(piv_panel_kernel<1>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G,
+                           unsigned(G) * unsigned(ps), w);
       else
-        hipLaunchKernelGGL(piv_panel_kernel<2>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G, w);
+        hipLaunchKernelGGL(piv_panel_kernel<2>, dim3(grid), dim3(256), lds, st, n, k, ps, pe, G,
+                           unsigned(G) * unsigned(ps), w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
     } else {
