@@ -22,6 +22,7 @@
 //      (dlarft T factors, FP64 MFMA GEMMs, split-K for the V^T Z products).
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 
@@ -397,22 +398,50 @@ __global__ void tri_bounds_kernel(const double *__restrict__ d, const double *__
 // Split T into unreduced blocks at |e_i| <= eps * ||T|| (LAPACK dstebz does the
 // same with a relative test); one thread scans (n is small).  es = e with the
 // split entries zeroed; bs/be = block of each position.
-__global__ void tri_split_kernel(const double *__restrict__ e, int n, const double *__restrict__ bnd,
-                                 double *__restrict__ es, int32_t *__restrict__ bs,
-                                 int32_t *__restrict__ be) {
-  if (threadIdx.x != 0) return;
+// One workgroup of 1024 threads: split flags in parallel, block starts by a
+// prefix max and block ends by a suffix min over per-thread chunks.
+__global__ __launch_bounds__(1024) void tri_split_kernel(const double *__restrict__ e, int n,
+                                                         const double *__restrict__ bnd,
+                                                         double *__restrict__ es,
+                                                         int32_t *__restrict__ bs,
+                                                         int32_t *__restrict__ be) {
+  __shared__ int cmax[1024], cmin[1024];
   const double tol = DBL_EPSILON * bnd[2];
-  int start = 0;
-  for (int i = 0; i < n; ++i) {
-    const bool split = i == n - 1 || fabs(e[i]) <= tol;
-    es[i] = (i == n - 1 || split) ? 0.0 : e[i];
-    if (split) {
-      for (int j = start; j <= i; ++j) {
-        bs[j] = start;
-        be[j] = i + 1;
-      }
-      start = i + 1;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int ch = (n + nt - 1) / nt, c0 = tid * ch, c1 = min(n, c0 + ch);
+  auto split = [&](int i) { return i == n - 1 || fabs(e[i]) <= tol; };
+  int lmax = 0, lmin = n;  // last split + 1 in the chunk / first split + 1 in the chunk
+  for (int i = c0; i < c1; ++i) {
+    const bool sp = split(i);
+    es[i] = sp ? 0.0 : e[i];
+    if (sp) {
+      lmax = i + 1;
+      if (lmin == n) lmin = i + 1;
     }
+  }
+  cmax[tid] = lmax;
+  cmin[tid] = lmin;
+  __syncthreads();
+  // exclusive prefix max / suffix min over chunks (Hillis-Steele, then shift)
+  for (int off = 1; off < nt; off <<= 1) {
+    const int a = tid >= off ? cmax[tid - off] : 0;
+    const int b = tid + off < nt ? cmin[tid + off] : n;
+    __syncthreads();
+    cmax[tid] = max(cmax[tid], a);
+    cmin[tid] = min(cmin[tid], b);
+    __syncthreads();
+  }
+  int start = tid > 0 ? cmax[tid - 1] : 0;
+  const int after = tid + 1 < nt ? cmin[tid + 1] : n;
+  // ends: walk the chunk backwards
+  int end = after;
+  for (int i = c1 - 1; i >= c0; --i) {
+    if (split(i)) end = i + 1;
+    be[i] = end;
+  }
+  for (int i = c0; i < c1; ++i) {
+    bs[i] = start;
+    if (split(i)) start = i + 1;
   }
 }
 
@@ -504,14 +533,29 @@ __global__ void rank_kernel(const double *__restrict__ w_asc, int n, double thr,
   if (threadIdx.x != 0) return;
   int k = n;
   if (rule == TG_RULE_ENERGY) {
+    // sequential sums (the reference's order), loads batched 16 at a time
     double total = 0.0;
-    for (int i = 0; i < n; ++i) total += S[i] * S[i];
+    for (int i0 = 0; i0 < n; i0 += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = S[min(i0 + u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (i0 + u < n) total += v[u] * v[u];
+    }
     const double target = (1.0 - thr) * total;
     double cs = 0.0;
     int cnt = 0;
-    for (int i = 0; i < n; ++i) {
-      cs += S[i] * S[i];
-      cnt += cs <= target;
+    for (int i0 = 0; i0 < n; i0 += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = S[min(i0 + u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (i0 + u < n) {
+          cs += v[u] * v[u];
+          cnt += cs <= target;
+        }
     }
     k = cnt < n ? cnt + 1 : cnt;
   } else if (rule == TG_RULE_MEAN_TRIMMED) {
@@ -552,7 +596,8 @@ constexpr int BCH = 16;  // backward-sweep chunk
 __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
                                                    const double *__restrict__ e, int n, int k,
                                                    const double *__restrict__ w_asc,
-                                                   const double *__restrict__ bnd, Tri w) {
+                                                   const double *__restrict__ bnd, int iters,
+                                                   Tri w) {
   const int jj = blockIdx.x * blockDim.x + threadIdx.x;
   if (jj >= k) return;
   const double lam = w_asc[n - 1 - jj];
@@ -572,7 +617,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
   auto at = [&](int i) { return size_t(i) * K + jj; };
   auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
   for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(b0 + i), uint32_t(jj)) + 0.25;
-  for (int it = 0; it < 3; ++it) {
+  for (int it = 0; it < iters; ++it) {
     // fused LU (dgttrf pattern) + forward substitution with the row interchanges
     double cur_d = d[0] - lam, cur_u = n > 1 ? e[0] : 0.0, xi = x[at(0)];
     for (int i0 = 0; i0 < n - 1; i0 += FCH) {
@@ -662,7 +707,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
           x[at(i0 + u)] = xv[u];
         }
     }
-    if (it == 2) {
+    if (it == iters - 1) {
       const double inv = 1.0 / sqrt(nrm);
       for (int i0 = 0; i0 < n; i0 += BCH) {
         double xv[BCH];
@@ -869,7 +914,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   TG_LAUNCHED();
   const int blocks = tg::cdiv(int64_t(n) * ML, 256);
   const size_t lds = 2 * sizeof(double) * size_t(n);
-  hipLaunchKernelGGL(tri_split_kernel, dim3(1), dim3(64), 0, st, w.e, n, bnd, w.es, w.bs, w.be);
+  hipLaunchKernelGGL(tri_split_kernel, dim3(1), dim3(1024), 0, st, w.e, n, bnd, w.es, w.bs, w.be);
   TG_LAUNCHED();
   hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.es, n, w.acol);
   TG_LAUNCHED();
@@ -920,8 +965,10 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   TG_WS(ar);
   const double *bnd = w.scal;
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
+  const char *ie = getenv("TG_INVIT_ITERS");
+  const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
   hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k, w_asc,
-                     bnd, w);
+                     bnd, iters, w);
   tg::prof_end(st, itok);
   TG_LAUNCHED();
   hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-9, w.Z);

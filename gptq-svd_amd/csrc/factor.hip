@@ -460,6 +460,62 @@ __global__ void gather_scale_kernel(const double *__restrict__ Vh, int ldv, cons
 }
 
 // Upper Cholesky of the pb x pb diagonal block at U[p][p] (in place), LDS.
+// Diagonal block of the U Cholesky (NU x NU, in LDS): U11 = chol_upper(G11)
+// written to U, and W = U11^-T (lower) to Wout, so the panel's off-diagonal
+// rows become one MFMA GEMM U12 = W G12.  X = U11^-1 by back substitution,
+// one column per thread group.
+constexpr int NU = 64;
+__global__ __launch_bounds__(256) void potrf_inv_kernel(double *__restrict__ U, int ldu, int p,
+                                                        int pb, double *__restrict__ Wout,
+                                                        int *__restrict__ info) {
+  __shared__ double a[NU][NU + 1];
+  __shared__ double x[NU][NU + 1];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
+    const int r = idx / NU, c = idx % NU;
+    a[r][c] = (r < pb && c < pb) ? U[size_t(p + r) * ldu + p + c] : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  for (int j = 0; j < NU; ++j) {
+    const double djj = a[j][j];
+    const double piv = sqrt(djj);
+    if (tid == 0 && !(djj > 0.0) && j < pb) atomicAdd(info, 1);
+    __syncthreads();
+    for (int c = j + 1 + tid; c < NU; c += blockDim.x) a[j][c] /= piv;
+    __syncthreads();
+    if (tid == 0) a[j][j] = piv;
+    const int m = NU - j - 1;
+    for (int idx = tid; idx < m * m; idx += blockDim.x) {
+      const int r = j + 1 + idx / m, c = j + 1 + idx % m;
+      if (c >= r) a[r][c] -= a[j][r] * a[j][c];
+    }
+    __syncthreads();
+  }
+  // X = U11^-1 (upper): column c by back substitution, 4 threads per column
+  // splitting each inner sum (fixed order: partials combined 0+1, 2+3, then).
+  {
+    const int c = tid >> 2, part = tid & 3;
+    for (int i = NU - 1; i >= 0; --i) {
+      double sacc = 0.0;
+      if (i < c)
+        for (int l = i + 1 + part; l <= c; l += 4) sacc += a[i][l] * x[l][c];
+      sacc += __shfl_xor(sacc, 1);
+      sacc += __shfl_xor(sacc, 2);
+      if (part == 0) x[i][c] = i > c ? 0.0 : ((i == c ? 1.0 : 0.0) - sacc) / a[i][i];
+      __syncthreads();
+    }
+  }
+  for (int idx = tid; idx < pb * pb; idx += blockDim.x) {
+    const int r = idx / pb, c = idx % pb;
+    U[size_t(p + r) * ldu + p + c] = c >= r ? a[r][c] : 0.0;
+  }
+  // W = X^T (lower), NU x NU, row stride NU
+  for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
+    const int r = idx / NU, c = idx % NU;
+    Wout[idx] = (r < pb && c < pb) ? x[c][r] : 0.0;
+  }
+}
+
 __global__ __launch_bounds__(256) void potf2_kernel(double *__restrict__ U, int ldu, int p, int pb,
                                                     int *__restrict__ info) {
   __shared__ double a[CB][CB + 1];
@@ -601,6 +657,7 @@ extern "C" size_t tg_ufactor_workspace_size(int n, int k) {
   tg::Sizer s;
   s.take<double>(size_t(k) * n);
   s.take<int>(16);
+  s.take<double>(NU * NU);
   return s.off + 256;
 }
 
@@ -619,6 +676,7 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   tg::Arena ar(ws, ws_bytes);
   double *A = ar.take<double>(size_t(k) * n);
   int *info = ar.take<int>(16);
+  double *Wb = ar.take<double>(NU * NU);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   hipLaunchKernelGGL(gather_scale_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
@@ -626,15 +684,17 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   TG_LAUNCHED();
   // G[:k, :] = A[:, :k]^T A   (k x n) into U
   TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));
-  for (int p = 0; p < k; p += CB) {
-    const int pb = std::min(CB, k - p);
-    hipLaunchKernelGGL(potf2_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, info);
+  // right-looking blocked Cholesky over the k rows, NU-row panels
+  for (int p = 0; p < k; p += NU) {
+    const int pb = std::min(NU, k - p);
+    hipLaunchKernelGGL(potrf_inv_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
     TG_LAUNCHED();
     const int c0 = p + pb;
     if (c0 < n) {
-      hipLaunchKernelGGL(trsm_rows_kernel, dim3(tg::cdiv(n - c0, 256)), dim3(256), 0, st, U, ldu,
-                         p, pb, c0, n);
-      TG_LAUNCHED();
+      // U12 = U11^-T G12, in place: one 64-row tile covers the panel's rows,
+      // so each workgroup reads its columns of G12 fully before writing them
+      double *P = U + size_t(p) * ldu + c0;
+      TG_HIP(tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu));
     }
     if (c0 < k) {
       const double *P = U + size_t(p) * ldu + c0;
