@@ -81,12 +81,12 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // ---------------------------------------------------------------------------
 constexpr int G_SW = 2;              // sweeps per group (waves per workgroup)
 constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
-constexpr int NCW = 2 * G_SW;        // compute waves (a wave pair per sweep)
+constexpr int NCW = 3 * G_SW;        // compute waves (three per sweep: left, diagonal, lower block)
 constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
 
 struct WaveScratch {
-  double vs[SB_B];
   double ws[SB_B];
+  double trash[64];  // target of the masked (upper-triangle) stores of the D update
 };
 
 __device__ inline void wave_sync() {
@@ -97,15 +97,64 @@ __device__ inline void wave_sync() {
 
 __device__ inline int rslot(int c) { return c & (RING - 1); }
 
-// Task (j, s) by a pair of waves on the LDS ring (element (r, c) at
-// R[slot(c)][r - c]).  Both waves form the reflector from x = B[R, col]; then
-// role 0 applies it to the left block A = B[R, Lft] and the
-// lower block G = B[Rgt, R], role 1 to the diagonal block D = B[R, R].  The three blocks are disjoint, so the waves never talk.
+// Task (j, s) by three waves on the LDS ring (element (r, c) at
+// R[slot(c)][r - c]): role 0 applies the reflector to the left block
+// A = B[R, Lft] (and stores it for Q2), role 1 to the diagonal block
+// D = B[R, R], role 2 to the lower block G = B[Rgt, R].  The blocks are
+// disjoint, so the waves never exchange data.  No wave reads the pivot
+// column the role-0 wave overwrites: the reflector of (j, s > 0) annihilates
+// the first column of the G block (j, s-1) just updated, so the role-2 wave
+// of (j, s-1) forms it from its registers and forwards (v, tau, beta) through
+// LDS (`rin` / `rout`, double-buffered by step); that of (j, 0) is formed one
+// step ahead by the same (then idle) role-2 wave (`first_refl`).
+struct Refl {
+  double v[SB_B];
+  double tau, beta;
+};
+
+__device__ __forceinline__ void make_refl(double x, int li, int hf, double &v, double &tau,
+                                          double &beta) {
+  const double sig = wsum((hf == 0 && li >= 1) ? x * x : 0.0);
+  const double alpha = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                                        __builtin_amdgcn_readfirstlane(__double2loint(x)));
+  double scal = 0.0;
+  tau = 0.0;
+  beta = alpha;
+  if (sig != 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sig), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  v = (li == 0) ? 1.0 : x * scal;
+}
+
+// Reflector of task (j, 0) (x = B[j+1 .. j+b, j], final once task (j-1, 1)
+// has run), formed one step ahead by one wave.
+__device__ __forceinline__ void first_refl(const double (*R)[LDB], int n, int j, Refl &out) {
+  const int lane = threadIdx.x & 63, li = lane & 31, hf = lane >> 5;
+  const int r1 = j + 1, L = min(SB_B, n - r1);
+  const double x = R[rslot(j)][1 + min(li, L - 1)];
+  double v, tau, beta;
+  make_refl(li < L ? x : 0.0, li, hf, v, tau, beta);
+  if (hf == 0) out.v[li] = v;
+  if (lane == 0) {
+    out.tau = tau;
+    out.beta = beta;
+  }
+}
+
+#ifdef TG_BULGE_PHASES
+__device__ unsigned long long g_ph[8];
+#define PH(i) const uint64_t ph##i = __builtin_amdgcn_s_memrealtime();
+#else
+#define PH(i)
+#endif
+
 template <bool FULL>
 __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, int s, int role,
-                                               double *__restrict__ V2,
+                                               bool has_next, double *__restrict__ V2,
                                                double *__restrict__ tau2, int smax,
-                                               WaveScratch &W) {
+                                               WaveScratch &W, const Refl &rin, Refl &rout) {
   const int lane = threadIdx.x & 63, li = lane & 31, hf = lane >> 5;
   const int r1 = j + 1 + s * SB_B;
   const int L = FULL ? SB_B : min(SB_B, n - r1);
@@ -115,10 +164,10 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
   const int ng = FULL ? SB_B : min(SB_B, n - (r1 + L));
   double *Rf = &R[0][0];
   auto at = [&](int c, int d) { return rslot(c) * LDB + d; };
-  const double x = (FULL || li < L) ? Rf[at(col, r1 + min(li, L - 1) - col)] : 0.0;
-  // block loads (issued before the reflector's reductions)
-  double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li, k = hf + 2q)
-  double g[16];  // role 0: G (lane row li, k = hf + 2q)
+  PH(0)
+  // block loads (issued before the reflector is needed)
+  double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li,
+                 // k = hf + 2q); role 2: G (lane row li, k = hf + 2q)
   if (role == 0) {
     const int ca = FULL ? li : min(li, max(nl - 1, 0));
     const int abase = at(lo + ca, r1 - lo - ca);
@@ -128,7 +177,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       if (FULL) e[q] = Rf[abase + i];
       else e[q] = (li < nl && i < L) ? Rf[abase + min(i, L - 1)] : 0.0;
     }
-  } else {
+  } else if (role == 1) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = hf + 2 * q;
@@ -136,77 +185,118 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       if (FULL) e[q] = Rf[at(r1 + cc, off)];
       else e[q] = (li < L && k < L) ? Rf[at(r1 + min(cc, L - 1), off)] : 0.0;
     }
-  }
-  if (role == 0) {
+  } else {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = hf + 2 * q;
-      if (FULL) g[q] = Rf[at(r1 + k, SB_B + li - k)];
+      if (FULL) e[q] = Rf[at(r1 + k, SB_B + li - k)];
       else {
         const int kc = min(k, L - 1);
         const double gv = Rf[at(r1 + kc, L + min(li, max(ng - 1, 0)) - kc)];
-        g[q] = (li < ng && k < L) ? gv : 0.0;
+        e[q] = (li < ng && k < L) ? gv : 0.0;
       }
     }
   }
-  // reflector (identical in both waves)
-  const double sig = wsum((hf == 0 && li >= 1) ? x * x : 0.0);
-  const double alpha = __shfl(x, 0);
-  double tau = 0.0, scal = 0.0, beta = alpha;
-  if (sig != 0.0) {
-    beta = -copysign(sqrt(alpha * alpha + sig), alpha);
-    tau = (beta - alpha) / beta;
-    scal = 1.0 / (alpha - beta);
-  }
-  const double v = (li == 0) ? 1.0 : ((FULL || li < L) ? x * scal : 0.0);
-  if (hf == 0) W.vs[li] = v;
-  wave_sync();
+  const double v = rin.v[li], tau = rin.tau, beta = rin.beta;
   double vk[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) vk[q] = W.vs[hf + 2 * q];
-  if (role == 0) {
+  for (int q = 0; q < 16; ++q) vk[q] = rin.v[hf + 2 * q];
+  if (role == 2) {
     // lower block: u_r = sum_k G[r][k] v_k, G -= tau u v^T (row r = li)
-    double u = 0.0;
+    double u0 = 0.0, u1 = 0.0, u2 = 0.0, u3 = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) u += g[q] * vk[q];
+    for (int q = 0; q < 16; q += 4) {
+      u0 += e[q] * vk[q];
+      u1 += e[q + 1] * vk[q + 1];
+      u2 += e[q + 2] * vk[q + 2];
+      u3 += e[q + 3] * vk[q + 3];
+    }
+    double u = (u0 + u1) + (u2 + u3);
     u += xchg32(u);
+    const double tu = tau * u;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = hf + 2 * q;
-      if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = g[q] - tau * u * vk[q];
+      e[q] = e[q] - tu * vk[q];
+      if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = e[q];
     }
+    if (has_next) {
+      // next reflector: x = updated column 0 of G (lanes hf == 0 hold G[li][0])
+      double vn, tn, bn;
+      make_refl((FULL || li < ng) ? e[0] : 0.0, li, hf, vn, tn, bn);
+      if (hf == 0) rout.v[li] = vn;
+      if (lane == 0) {
+        rout.tau = tn;
+        rout.beta = bn;
+      }
+    }
+  } else if (role == 0) {
     // left block: w_c = sum_i v_i A[i][c]
-    double wc = 0.0;
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) wc += vk[q] * e[q];
+    for (int q = 0; q < 16; q += 4) {
+      w0 += vk[q] * e[q];
+      w1 += vk[q + 1] * e[q + 1];
+      w2 += vk[q + 2] * e[q + 2];
+      w3 += vk[q + 3] * e[q + 3];
+    }
+    double wc = (w0 + w1) + (w2 + w3);
     wc += xchg32(wc);
     if (FULL || li < nl) {
       const int c = li;
       double *Ac = Rf + at(lo + c, r1 - lo - c);
       const bool piv = (lo + c == col);
+      const double twc = tau * wc;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = hf + 2 * q;
-        if (FULL || i < L) Ac[i] = piv ? (i == 0 ? beta : 0.0) : e[q] - tau * vk[q] * wc;
+        if (FULL || i < L) Ac[i] = piv ? (i == 0 ? beta : 0.0) : e[q] - twc * vk[q];
       }
     }
     if (hf == 0) V2[(int64_t(j) * smax + s) * SB_B + li] = v;
     if (lane == 0) tau2[int64_t(j) * smax + s] = tau;
   } else {
-    double p = 0.0;
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) p += e[q] * vk[q];
+    for (int q = 0; q < 16; q += 4) {
+      p0 += e[q] * vk[q];
+      p1 += e[q + 1] * vk[q + 1];
+      p2 += e[q + 2] * vk[q + 2];
+      p3 += e[q + 3] * vk[q + 3];
+    }
+    double p = (p0 + p1) + (p2 + p3);
+    PH(1)
     p += xchg32(p);
     p *= tau;
     const double pv = wsum(hf == 0 ? p * v : 0.0);
     const double w = p - 0.5 * tau * pv * v;
+    PH(2)
     if (hf == 0) W.ws[li] = w;
     wave_sync();
+    PH(3)
+    double wk[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wk[q] = W.ws[hf + 2 * q];
+    // branch-free: lanes outside the lower triangle store to a trash slot
+    double *tr = W.trash + lane;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = hf + 2 * q;
-      if ((FULL || li < L) && k <= li) Rf[at(r1 + k, li - k)] = e[q] - v * W.ws[k] - w * vk[q];
+      const bool ok = (FULL || li < L) && k <= li;
+      double *dst = ok ? Rf + at(r1 + k, li - k) : tr;
+      *dst = e[q] - v * wk[q] - w * vk[q];
     }
+#ifdef TG_BULGE_PHASES
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH(4)
+    if (FULL && lane == 0) {
+      atomicAdd(g_ph + 0, ph1 - ph0);
+      atomicAdd(g_ph + 1, ph2 - ph1);
+      atomicAdd(g_ph + 2, ph3 - ph2);
+      atomicAdd(g_ph + 3, ph4 - ph3);
+      atomicAdd(g_ph + 4, 1ull);
+    }
+#endif
   }
 }
 
@@ -244,7 +334,8 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
                                                        unsigned long long *__restrict__ stats) {
   uint64_t sw = 0, stk = 0, sbar = 0, spf = 0, swb = 0, nsteps = 0;
   __shared__ double R[RING][LDB];
-  __shared__ WaveScratch wsc[2 * G_SW];
+  __shared__ WaveScratch wsc[NCW];
+  __shared__ Refl rfl[G_SW][2];
   __shared__ int sh_G;
   const int tid = threadIdx.x, wid = tid >> 6;
   // workers: one XCD only (ctl[0] = chosen XCD + 1, ctl[1] = group queue)
@@ -341,18 +432,25 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     }
     ld = group_high(n, j0, 0);
     __syncthreads();
+    if (wid == 2) first_refl(R, n, j0, rfl[0][0]);
+    __syncthreads();
     const int wlane = tid & 63;
     for (int t = 0; t < total; ++t) {
       const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
       if (wid < NCW) {
-        const int pair = wid >> 1, role = wid & 1;
+        const int pair = wid / 3, role = wid % 3;
         const int s = t - 3 * pair;
         if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
           const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
+          const bool nx = s + 1 < ntasks(n, jj);
+          const Refl &ri = rfl[pair][t & 1];
+          Refl &ro = rfl[pair][(t + 1) & 1];
           if (r1 >= SB_B && r1 + 2 * SB_B <= n)
-            bulge_task_lds<true>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+            bulge_task_lds<true>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
           else
-            bulge_task_lds<false>(R, n, jj, s, role, V2, tau2, smax, wsc[wid]);
+            bulge_task_lds<false>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
+        } else if (pair < g && pair > 0 && s == -1 && role == 2) {
+          first_refl(R, n, j0 + pair, rfl[pair][(t + 1) & 1]);
         }
       } else if (wid == NCW) {
         // writer: retire the columns step t-1 left behind, drain, publish t
@@ -519,6 +617,12 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       fprintf(stderr, "  per-wave busy per step (us):");
       for (int w = 0; w < NCW + 2; ++w) fprintf(stderr, " w%d %.2f", w, h[8 + w] / 100.0 / S);
       fprintf(stderr, "\n");
+#ifdef TG_BULGE_PHASES
+      unsigned long long ph[8];
+      (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph));
+      fprintf(stderr, "  D wave phases (us): loads+matvec %.3f reduce %.3f sync %.3f update %.3f (n %llu)\n",
+              ph[0] / 100.0 / ph[4], ph[1] / 100.0 / ph[4], ph[2] / 100.0 / ph[4], ph[3] / 100.0 / ph[4], ph[4]);
+#endif
       (void)hipFree(stats);
     }
   }
