@@ -190,6 +190,27 @@ def cpu_baseline(H, W, args):
                         f"factorisation {t1 - t0:.2f}s + quantize/pack {t2 - t1:.2f}s"))
 
 
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
+                        "pmc_traffic.json")
+
+
+def pmc_traffic(cls, args):
+    """HBM bytes per launch of kernel class `cls` from the committed rocprofv3
+    PMC passes (tools/profile_round.sh + tools/pmc_traffic.py; FETCH_SIZE
+    doubled per the gfx950 correction).  Counters cannot be read inside a
+    timed run, so the value comes from the profile of the same default
+    workload; null for other workloads or classes without a PMC pass."""
+    default = (args.n, args.m, args.tokens, args.bits, args.group, args.sym) == (
+        4096, 4096, 3072, 4, 128, False)
+    if not default or not os.path.exists(PMC_FILE):
+        return {}
+    ent = json.load(open(PMC_FILE)).get(cls)
+    if not ent:
+        return {}
+    return dict(traffic=ent["traffic_bytes"], traffic_unit="bytes/launch",
+                traffic_source=os.path.relpath(PMC_FILE, os.path.dirname(PMC_FILE) + "/../.."))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +289,7 @@ def main():
                     achieved=round(achieved, 3), peak=peak, unit=unit,
                     frac=round(achieved / peak, 4), traffic=None,
                     avg_launch_ms=round(avg_ms, 5), launches_per_step=p["launches"] // args.steps)
+        roof.update(pmc_traffic(name, args))
 
     extra = {}
     if rank == 0:
