@@ -51,6 +51,10 @@ _SIGS = {
     "tg_quantize_workspace_size": ([_i, _i, _i], _sz),
     "tg_gptq_quantize": ([_vp, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _vp,
                           _vp, _vp, _sz], _i),
+    "tg_gptq_quantize_loop": ([_vp, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i,
+                               _vp, _vp, _vp, _sz], _i),
+    "tg_hinv_chol_workspace_size": ([_i], _sz),
+    "tg_hinv_chol": ([_vp, _vp, _i, _i, _vp, _d, _i, _vp, _i, ctypes.POINTER(_i), _vp, _sz], _i),
     "tg_pack_codes": ([_vp, _vp, _i, _i, _i, _vp], _i),
     "tg_pack_zeros": ([_vp, _vp, _i, _i, _i, _i, _vp], _i),
 }

@@ -577,6 +577,137 @@ __global__ void zero_lower_kernel(double *__restrict__ U, int ldu, int k) {
     U[size_t(r) * ldu + c] = 0.0;
 }
 
+
+// Right-looking blocked upper Cholesky of the first k rows of the symmetric
+// n x n matrix in U (upper triangle read): U[:k, :] <- R with R^T R = G
+// restricted to those rows (k = n: the full factor).  NU-row panels: the
+// diagonal block and its inverse in LDS (potrf_inv_kernel), the panel rows as
+// one MFMA GEMM U12 = U11^-T G12, the trailing update as a second GEMM.
+// info[0] counts non-positive pivots.
+hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, double *Wb,
+                           int *info) {
+  for (int p = 0; p < k; p += NU) {
+    const int pb = std::min(NU, k - p);
+    hipLaunchKernelGGL(potrf_inv_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int c0 = p + pb;
+    if (c0 < n) {
+      // in place: one 64-row tile covers the panel's rows, so each workgroup
+      // reads its columns of G12 fully before writing them
+      double *P = U + size_t(p) * ldu + c0;
+      e = tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
+      if (e != hipSuccess) return e;
+    }
+    if (c0 < k) {
+      const double *P = U + size_t(p) * ldu + c0;
+      e = tg::dgemm(st, true, false, k - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
+                    U + size_t(c0) * ldu + c0, ldu);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// GPTQ comparator factor (process_hessian, gptq_utils.py:129-165):
+// R = chol_upper(inv(H_p + damp I)), H_p = H[perm][:, perm].  With J the
+// reversal, chol_upper(J H_p J) = U' gives H_p = Ut Ut^T for the upper
+// Ut = J U'^T J, hence inv(H_p) = Ut^-T Ut^-1 and R = Ut^-1 = J (U'^-1)^T J:
+// one Cholesky and one triangular inverse instead of the reference's
+// cholesky -> cholesky_inverse -> cholesky (same matrix, other rounding).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void diag_mean_kernel(const double *__restrict__ H, int64_t ldh,
+                                                        int n, double *__restrict__ mean) {
+  __shared__ double part[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += H[i * ldh + i];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += part[i];  // fixed order: deterministic
+    t /= double(n);
+    mean[0] = (t == 0.0) ? 1.0 : t;              // :144-145
+  }
+}
+
+// A[i][j] = H[p(n-1-i)][p(n-1-j)] + (i == j) damp * mean
+__global__ void flip_damp_kernel(const double *__restrict__ H, int64_t ldh, int n,
+                                 const int64_t *__restrict__ perm, double damp,
+                                 const double *__restrict__ mean, double *__restrict__ A) {
+  const int i = blockIdx.y;
+  const int64_t pi = perm ? perm[n - 1 - i] : n - 1 - i;
+  const double dm = damp * mean[0];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int64_t pj = perm ? perm[n - 1 - j] : n - 1 - j;
+    double v = H[pi * ldh + pj];
+    if (i == j) v += dm;
+    A[int64_t(i) * n + j] = v;
+  }
+}
+
+// Y_bb = U_bb^-1 for every NU x NU diagonal block b (one workgroup each);
+// the rest of Y is left to the caller (zeroed, then filled by GEMMs).
+__global__ __launch_bounds__(256) void trinv_diag_kernel(const double *__restrict__ U, int ldu,
+                                                         int n, double *__restrict__ Y, int ldy) {
+  __shared__ double a[NU][NU + 1];
+  __shared__ double x[NU][NU + 1];
+  const int p = blockIdx.x * NU, pb = min(NU, n - p), tid = threadIdx.x;
+  for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
+    const int r = idx / NU, c = idx % NU;
+    a[r][c] = (r < pb && c < pb) ? (c >= r ? U[size_t(p + r) * ldu + p + c] : 0.0)
+                                 : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  const int c = tid >> 2, part = tid & 3;
+  for (int i = NU - 1; i >= 0; --i) {
+    double sacc = 0.0;
+    if (i < c)
+      for (int l = i + 1 + part; l <= c; l += 4) sacc += a[i][l] * x[l][c];
+    sacc += __shfl_xor(sacc, 1);
+    sacc += __shfl_xor(sacc, 2);
+    if (part == 0) x[i][c] = i > c ? 0.0 : ((i == c ? 1.0 : 0.0) - sacc) / a[i][i];
+    __syncthreads();
+  }
+  for (int idx = tid; idx < pb * pb; idx += blockDim.x) {
+    const int r = idx / pb, cc = idx % pb;
+    Y[size_t(p + r) * ldy + p + cc] = x[r][cc];
+  }
+}
+
+// Off-diagonal blocks of Y = U^-1 (upper, n = multiple-of-NU split):
+// Y12 = -(Y11 U12) Y22, recursing on halves (diagonal blocks already in Y).
+hipError_t trinv_offdiag(hipStream_t st, const double *U, int ldu, double *Y, int ldy, int n,
+                         double *T) {
+  if (n <= NU) return hipSuccess;
+  const int nb = tg::cdiv(n, NU);
+  const int h = NU * ((nb + 1) / 2), h2 = n - h;
+  hipError_t e = trinv_offdiag(st, U, ldu, Y, ldy, h, T);
+  if (e == hipSuccess)
+    e = trinv_offdiag(st, U + size_t(h) * ldu + h, ldu, Y + size_t(h) * ldy + h, ldy, h2, T);
+  if (e != hipSuccess) return e;
+  // T = Y11 U12 (h x h2), Y12 = -T Y22
+  e = tg::dgemm(st, false, false, h, h2, h, 1.0, Y, ldy, U + h, ldu, 0.0, T, h2);
+  if (e != hipSuccess) return e;
+  return tg::dgemm(st, false, false, h, h2, h2, -1.0, T, h2, Y + size_t(h) * ldy + h, ldy, 0.0,
+                   Y + h, ldy);
+}
+
+// R[i][j] = Y[n-1-j][n-1-i] (j >= i), 0 below the diagonal
+__global__ void flip_transpose_kernel(const double *__restrict__ Y, int n, double *__restrict__ R,
+                                      int64_t ldr) {
+  const int i = blockIdx.y;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    R[i * ldr + j] = j >= i ? Y[int64_t(n - 1 - j) * n + (n - 1 - i)] : 0.0;
+}
+
+__global__ void identity_kernel(int n, double *__restrict__ R, int64_t ldr) {
+  const int i = blockIdx.y;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    R[i * ldr + j] = i == j ? 1.0 : 0.0;
+}
+
 }  // namespace
 
 extern "C" size_t tg_pivot_workspace_size(int n, int k) {
@@ -684,26 +815,83 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   TG_LAUNCHED();
   // G[:k, :] = A[:, :k]^T A   (k x n) into U
   TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));
-  // right-looking blocked Cholesky over the k rows, NU-row panels
-  for (int p = 0; p < k; p += NU) {
-    const int pb = std::min(NU, k - p);
-    hipLaunchKernelGGL(potrf_inv_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
-    TG_LAUNCHED();
-    const int c0 = p + pb;
-    if (c0 < n) {
-      // U12 = U11^-T G12, in place: one 64-row tile covers the panel's rows,
-      // so each workgroup reads its columns of G12 fully before writing them
-      double *P = U + size_t(p) * ldu + c0;
-      TG_HIP(tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu));
-    }
-    if (c0 < k) {
-      const double *P = U + size_t(p) * ldu + c0;
-      TG_HIP(tg::dgemm(st, true, false, k - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
-                       U + size_t(c0) * ldu + c0, ldu));
-    }
-  }
+  TG_HIP(chol_upper_rows(st, U, ldu, k, n, Wb, info));
   hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
                      dim3(256), 0, st, U, ldu, k);
   TG_LAUNCHED();
+  return 0;
+}
+
+namespace {
+template <class A>
+void hinv_layout(A &ar, int n, double **Aw, double **Yw, double **Tw, double **Wb, double **mean,
+                 int **info) {
+  const size_t h = size_t(NU) * ((tg::cdiv(n, NU) + 1) / 2);
+  auto t = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  double *d0, *d1, *d2, *d3, *d4;
+  int *i0;
+  t(Aw ? *Aw : d0, size_t(n) * n);
+  t(Yw ? *Yw : d1, size_t(n) * n);
+  t(Tw ? *Tw : d2, h * h);
+  t(Wb ? *Wb : d3, size_t(NU) * NU);
+  t(mean ? *mean : d4, 1);
+  t(info ? *info : i0, 16);
+}
+}  // namespace
+
+extern "C" size_t tg_hinv_chol_workspace_size(int n) {
+  tg::Sizer s;
+  hinv_layout(s, n, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_hinv_chol(void *stream, const double *H, int n, int ldh, const int64_t *perm,
+                            double damp_percent, int max_tries, double *R, int ldr,
+                            int *tries_used, void *ws, size_t ws_bytes) {
+  TG_ARG(H, 2, "null H");
+  TG_ARG(n >= 1, 3, "n < 1");
+  TG_ARG(ldh >= n, 4, "ldh < n");
+  TG_ARG(max_tries >= 1, 7, "max_tries < 1");
+  TG_ARG(R, 8, "null R");
+  TG_ARG(ldr >= n, 9, "ldr < n");
+  TG_ARG(tries_used, 10, "null tries_used");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  double *A, *Y, *T, *Wb, *mean;
+  int *info;
+  hinv_layout(ar, n, &A, &Y, &T, &Wb, &mean, &info);
+  TG_WS(ar);
+  const dim3 g2(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, n);
+  hipLaunchKernelGGL(diag_mean_kernel, dim3(1), dim3(256), 0, st, H, int64_t(ldh), n, mean);
+  TG_LAUNCHED();
+  // damping ladder of gptq_utils.py:148-160: damp = 10^e * damp_percent
+  double scale = 1.0;
+  for (int e = 0; e < max_tries; ++e, scale *= 10.0) {
+    hipLaunchKernelGGL(flip_damp_kernel, g2, dim3(256), 0, st, H, int64_t(ldh), n, perm,
+                       scale * damp_percent, mean, A);
+    TG_LAUNCHED();
+    TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+    TG_HIP(chol_upper_rows(st, A, n, n, n, Wb, info));
+    int h_info = 0;
+    TG_HIP(hipMemcpyAsync(&h_info, info, sizeof(int), hipMemcpyDeviceToHost, st));
+    TG_HIP(hipStreamSynchronize(st));
+    if (h_info != 0) continue;  // not positive definite at this damping: next rung
+    TG_HIP(hipMemsetAsync(Y, 0, sizeof(double) * size_t(n) * n, st));
+    hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(n, NU)), dim3(256), 0, st, A, n, n, Y, n);
+    TG_LAUNCHED();
+    TG_HIP(trinv_offdiag(st, A, n, Y, n, n, T));
+    hipLaunchKernelGGL(flip_transpose_kernel, g2, dim3(256), 0, st, Y, n, R, int64_t(ldr));
+    TG_LAUNCHED();
+    *tries_used = e;
+    return 0;
+  }
+  // every rung failed: identity (the reference's intended fallback, :162-164)
+  hipLaunchKernelGGL(identity_kernel, g2, dim3(256), 0, st, n, R, int64_t(ldr));
+  TG_LAUNCHED();
+  *tries_used = max_tries;
   return 0;
 }

@@ -96,12 +96,21 @@ __global__ void permute_kernel(const float *__restrict__ W, int n, const int32_t
 // Per-block prep: corr[c][j] = U[c, j] * (1/U[c, c])   (Triton :368-377)
 //                 SM[c][j]   = U[c, i2 + j] / U[c, c]   (:539-541)
 // ---------------------------------------------------------------------------
+// Loop mode (use_triton=False, :516-534, :544): corr and SM are the raw rows
+// U[c, :] and dg[c] = U[c, c] (the error is divided by it instead).
 __global__ void prep_block_kernel(const float *__restrict__ Ublk, int ldu, int bw, int nc,
                                   float *__restrict__ corr, int ldcorr, float *__restrict__ SM,
-                                  int ldsm) {
+                                  int ldsm, float *__restrict__ dg) {
   const int c = blockIdx.x;
   const float *urow = Ublk + size_t(c) * ldu;
   const float d = urow[c];
+  if (dg) {
+    if (threadIdx.x == 0) dg[c] = d;
+    for (int j = threadIdx.x; j < bw; j += blockDim.x) corr[size_t(c) * ldcorr + j] = urow[j];
+    if (SM)
+      for (int j = threadIdx.x; j < nc; j += blockDim.x) SM[size_t(c) * ldsm + j] = urow[bw + j];
+    return;
+  }
   const float inv = 1.0f / d;
   for (int j = threadIdx.x; j < bw; j += blockDim.x) corr[size_t(c) * ldcorr + j] = urow[j] * inv;
   for (int j = threadIdx.x; j < nc; j += blockDim.x) SM[size_t(c) * ldsm + j] = urow[bw + j] / d;
@@ -133,6 +142,7 @@ struct BlockArgs {
   int lde;
   const float *corr;
   int ldcorr;
+  const float *dg;  // loop mode: U[c, c] per block column
   // explicit s/z (tg_process_block) ...
   const float *s;
   int lds;
@@ -165,7 +175,7 @@ __device__ inline void load_sz(const BlockArgs &a, int row, int c, float &s, flo
   }
 }
 
-template <bool GATHER>
+template <bool GATHER, bool LOOP>
 __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
   extern __shared__ float smem[];
   const int bwp = a.bw + 1;           // odd row stride: lane-per-row access is conflict-free
@@ -204,10 +214,17 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
           const float x = wv[cc];
           float t = x / sv[cc];                               // :354
           t = t + zv[cc];
-          t = t + 0.5f;
-          const float qi = clampf(floorf(t), a.minq, a.maxq);  // :355
-          const float qv = (qi - zv[cc]) * sv[cc];             // :356
-          const float err = x - qv;                            // :358
+          float qi, err, qv;
+          if (LOOP) {                                         // :524-529
+            qi = clampf(rintf(t), a.minq, a.maxq);             // torch.round: half-to-even
+            qv = (qi - zv[cc]) * sv[cc];
+            err = (x - qv) / a.dg[p0 + cc];
+          } else {
+            t = t + 0.5f;
+            qi = clampf(floorf(t), a.minq, a.maxq);            // :355
+            qv = (qi - zv[cc]) * sv[cc];                       // :356
+            err = x - qv;                                      // :358
+          }
           if (row < a.m) {
             const int c = p0 + cc;
             a.Q[size_t(row) * a.ldq + c] = qv;
@@ -402,11 +419,12 @@ hipError_t ensure_block_smem() {
   static bool done = false;  // per-process; attribute is per function, device-independent
   if (done) return hipSuccess;
   const int bytes = int(block_smem(MAX_BLOCK));
-  hipError_t e = hipFuncSetAttribute((const void *)block_kernel<true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void *)block_kernel<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  hipError_t e = hipSuccess;
+  for (const void *f : {(const void *)block_kernel<true, false>,
+                        (const void *)block_kernel<false, false>,
+                        (const void *)block_kernel<true, true>}) {
+    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  }
   done = e == hipSuccess;
   return e;
 }
@@ -449,13 +467,14 @@ extern "C" int tg_process_block(void *stream, const float *w, int ldw, const flo
   TG_WS(ar);
   TG_HIP(ensure_block_smem());
   hipLaunchKernelGGL(prep_block_kernel, dim3(B), dim3(256), 0, st, R, ldr, B, 0, corr, B,
-                     (float *)nullptr, 0);
+                     (float *)nullptr, 0, (float *)nullptr);
   TG_LAUNCHED();
   BlockArgs a{};
   a.W = w; a.ldw = ldw; a.Q = q; a.ldq = ldq; a.codes = nullptr; a.ldc = 0; a.E = e; a.lde = lde;
   a.corr = corr; a.ldcorr = B; a.s = s; a.lds = lds; a.z = z; a.ldz = ldz;
   a.m = m; a.bw = B; a.minq = float(minq); a.maxq = float(maxq); a.code_off = 0;
-  hipLaunchKernelGGL(block_kernel<false>, dim3(tg::cdiv(m, RW)), dim3(256), block_smem(B), st, a);
+  hipLaunchKernelGGL((block_kernel<false, false>), dim3(tg::cdiv(m, RW)), dim3(256), block_smem(B),
+                     st, a);
   TG_LAUNCHED();
   return 0;
 }
@@ -464,7 +483,7 @@ extern "C" size_t tg_process_block_workspace_size(int B) { return sizeof(float) 
 
 namespace {
 struct QuantWs {
-  float *Wp, *Qp, *E, *corr, *SM;
+  float *Wp, *Qp, *E, *corr, *SM, *dg;
   uint8_t *cp;
   int32_t *inv, *perm32;
 };
@@ -483,6 +502,7 @@ void quant_layout(A &ar, int m, int n, int block, QuantWs *p) {
   t(q.E, size_t(m) * bp);
   t(q.corr, size_t(bp) * bp);
   t(q.SM, size_t(bp) * n);
+  t(q.dg, size_t(bp));
   t(q.cp, size_t(m) * n);
   t(q.inv, size_t(n));
   t(q.perm32, size_t(n));
@@ -495,10 +515,11 @@ extern "C" size_t tg_quantize_workspace_size(int m, int n, int block) {
   return s.off + 256;
 }
 
-extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, const float *U, int k,
-                                int ldu, const int64_t *perm, const float *scale,
-                                const float *zero, int group, int w_bits, int sym, int block,
-                                float *Wq, uint8_t *codes, void *ws, size_t ws_bytes) {
+static int gptq_quantize_impl(bool loop, void *stream, const float *W, int m, int n,
+                              const float *U, int k, int ldu, const int64_t *perm,
+                              const float *scale, const float *zero, int group, int w_bits,
+                              int sym, int block, float *Wq, uint8_t *codes, void *ws,
+                              size_t ws_bytes) {
   TG_ARG(W, 2, "null W");
   TG_ARG(m > 0, 3, "m <= 0");
   TG_ARG(n > 0, 4, "n <= 0");
@@ -536,17 +557,21 @@ extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, cons
     const int bw = i2 - i1;
     const int nc = n - i2;
     hipLaunchKernelGGL(prep_block_kernel, dim3(bw), dim3(256), 0, st, U + size_t(i1) * ldu + i1,
-                       ldu, bw, nc, q.corr, bp, q.SM, n);
+                       ldu, bw, nc, q.corr, bp, q.SM, n, loop ? q.dg : (float *)nullptr);
     TG_LAUNCHED();
     BlockArgs a{};
     a.W = q.Wp + i1; a.ldw = n; a.Q = q.Qp + i1; a.ldq = n; a.codes = q.cp + i1; a.ldc = n;
-    a.E = q.E; a.lde = bp; a.corr = q.corr; a.ldcorr = bp;
+    a.E = q.E; a.lde = bp; a.corr = q.corr; a.ldcorr = bp; a.dg = q.dg;
     a.scale = scale; a.zero = zero; a.perm = q.perm32; a.G = G; a.g = g; a.col0 = i1;
     a.m = m; a.bw = bw; a.minq = minq; a.maxq = maxq; a.code_off = code_off;
     auto qtok = tg::prof_begin(st, tg::PROF_QBLOCK, 4.0 * 4.0 * double(m) * bw,
                                double(m) * bw * (bw - 1));
-    hipLaunchKernelGGL(block_kernel<true>, dim3(tg::cdiv(m, RW)), dim3(256), block_smem(bw), st,
-                       a);
+    if (loop)
+      hipLaunchKernelGGL((block_kernel<true, true>), dim3(tg::cdiv(m, RW)), dim3(256),
+                         block_smem(bw), st, a);
+    else
+      hipLaunchKernelGGL((block_kernel<true, false>), dim3(tg::cdiv(m, RW)), dim3(256),
+                         block_smem(bw), st, a);
     tg::prof_end(st, qtok);
     TG_LAUNCHED();
     if (nc > 0) {
@@ -564,6 +589,22 @@ extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, cons
                      minq, maxq, code_off, Wq, codes);
   TG_LAUNCHED();
   return 0;
+}
+
+extern "C" int tg_gptq_quantize(void *stream, const float *W, int m, int n, const float *U, int k,
+                                int ldu, const int64_t *perm, const float *scale,
+                                const float *zero, int group, int w_bits, int sym, int block,
+                                float *Wq, uint8_t *codes, void *ws, size_t ws_bytes) {
+  return gptq_quantize_impl(false, stream, W, m, n, U, k, ldu, perm, scale, zero, group, w_bits,
+                            sym, block, Wq, codes, ws, ws_bytes);
+}
+
+extern "C" int tg_gptq_quantize_loop(void *stream, const float *W, int m, int n, const float *U,
+                                     int k, int ldu, const int64_t *perm, const float *scale,
+                                     const float *zero, int group, int w_bits, int sym, int block,
+                                     float *Wq, uint8_t *codes, void *ws, size_t ws_bytes) {
+  return gptq_quantize_impl(true, stream, W, m, n, U, k, ldu, perm, scale, zero, group, w_bits,
+                            sym, block, Wq, codes, ws, ws_bytes);
 }
 
 extern "C" int tg_pack_codes(void *stream, const uint8_t *codes, int m, int n, int w_bits,

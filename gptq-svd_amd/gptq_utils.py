@@ -14,6 +14,7 @@ fallback: CPU tensors raise ``RuntimeError``.
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 from typing import Optional, Tuple
 
@@ -23,7 +24,7 @@ from . import _lib
 from ._lib import call, ptr, stream, workspace
 
 __all__ = [
-    "HessianAccumulator", "process_hessian_alt", "Quantizer", "gptq_fwrd",
+    "HessianAccumulator", "process_hessian_alt", "process_hessian", "Quantizer", "gptq_fwrd",
     "triton_process_block", "log_quantization_error", "next_power_of_2",
     "truncated_spectral_factor", "pack_quantized",
 ]
@@ -126,6 +127,41 @@ def process_hessian_alt(H: torch.Tensor, threshold: float = 0.0005,
 
 
 # ---------------------------------------------------------------------------
+# §8(f) GPTQ comparator factor  (gptq_utils.py:129-165)
+# ---------------------------------------------------------------------------
+def process_hessian(H: torch.Tensor, actorder: bool = False,
+                    damp_percent: float = 0.01) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(H_inv_chol, perm): upper Cholesky factor of inv(H_p + damp I) with the
+    reference's damping ladder damp = 10^e * damp_percent * mean(diag H),
+    e = 0..4 (:148-160).  ActOrder: perm = argsort(diag H, descending) (stable
+    on ties; the reference's unstable CUDA sort leaves tie order unspecified).
+    When every rung fails the factor is the identity -- the reference's
+    intent at :162-164, which as written raises NameError (it tests
+    `H_inv_chol` but initialises `H_inv_factor`, :147).
+    """
+    _lib.require_cuda(H, "process_hessian H")
+    Hd = H.to(dtype=torch.float64).contiguous()
+    n = Hd.shape[0]
+    device = Hd.device
+    if actorder:
+        perm = torch.argsort(torch.diagonal(Hd), descending=True, stable=True)
+    else:
+        perm = torch.arange(n, device=device)
+    R = torch.empty((n, n), dtype=torch.float64, device=device)
+    tries = ctypes.c_int(0)
+    max_tries = 5
+    with torch.cuda.device(device):
+        ws = workspace(_lib.lib.tg_hinv_chol_workspace_size(n), device)
+        call("tg_hinv_chol", stream(), ptr(Hd), n, n, ptr(perm) if actorder else None,
+             float(damp_percent), max_tries, ptr(R), n, ctypes.byref(tries), ptr(ws), ws.numel())
+    if tries.value >= max_tries:
+        logging.warning(" Hessian is singular. Using Identity fallback.")
+    elif tries.value > 0:
+        logging.info(f"  Ref-GPTQ required high damping: {10 ** tries.value * damp_percent}")
+    return R, perm
+
+
+# ---------------------------------------------------------------------------
 # A7  (gptq_utils.py:230-272)
 # ---------------------------------------------------------------------------
 class Quantizer:
@@ -220,13 +256,12 @@ def gptq_fwrd(weight_mat: torch.Tensor, H_inv_sqrt: torch.Tensor, quantizer: Qua
     """Column-wise quantize + error propagation driven by U (= H_inv_sqrt).
 
     Returns (dequantised W in the original column order and dtype, rank).
+    use_triton=True: the TruncGPTQ block kernel semantics (:345-386, :537-545);
+    use_triton=False: the GPTQ-comparator column loop (:516-534, :544) --
+    round-half-even, error divided by U[c, c], raw U rows for propagation.
     The integer codes of the last call are kept on ``quantizer.codes``
     (uint8, original order, +2^(b-1) offset when sym) for packing.
     """
-    if not use_triton:
-        raise NotImplementedError(
-            "gptq_fwrd(use_triton=False) is the reference's GPTQ-comparator loop "
-            "(gptq_utils.py:516-534); it is not part of the TruncGPTQ hot path yet")
     allow_tf32 = torch.backends.cuda.matmul.allow_tf32       # :474-475, restored :565
     torch.backends.cuda.matmul.allow_tf32 = False
     try:
@@ -248,7 +283,8 @@ def gptq_fwrd(weight_mat: torch.Tensor, H_inv_sqrt: torch.Tensor, quantizer: Qua
         with torch.cuda.device(device):
             ws = workspace(_lib.lib.tg_quantize_workspace_size(out_features, in_features,
                                                                block_size), device)
-            call("tg_gptq_quantize", stream(), ptr(weight_mat), out_features, in_features,
+            call("tg_gptq_quantize" if use_triton else "tg_gptq_quantize_loop", stream(),
+                 ptr(weight_mat), out_features, in_features,
                  ptr(U), current_rank, U.shape[1], ptr(perm_d), ptr(scale), ptr(zero),
                  quantizer.group_size, quantizer.w_bits, int(quantizer.sym), block_size,
                  ptr(Wq), ptr(codes), ptr(ws), ws.numel())

@@ -117,6 +117,31 @@ int tg_gptq_quantize(void *stream, const float *W, int m, int n, const float *U,
                      int w_bits, int sym, int block, float *Wq, uint8_t *codes, void *ws,
                      size_t ws_bytes);
 
+/* ---- §8(f) GPTQ comparator: gptq_fwrd(use_triton=False)
+ * (gptq_utils.py:516-534 column loop, :544 cross-block GEMM) ---------------
+ * Same arguments as tg_gptq_quantize; U is the comparator's H_inv_sqrt
+ * (tg_hinv_chol).  Per column: q = clamp(round-half-even(w/s + z)),
+ * err = (w - (q - z) s) / U[c, c], later block columns w_j -= err * U[c, j];
+ * cross-block W[:, i2:] -= Err @ U[i1:i2, i2:] (k-ordered fmaf chain). */
+int tg_gptq_quantize_loop(void *stream, const float *W, int m, int n, const float *U, int k,
+                          int ldu, const int64_t *perm, const float *scale, const float *zero,
+                          int group, int w_bits, int sym, int block, float *Wq, uint8_t *codes,
+                          void *ws, size_t ws_bytes);
+
+/* ---- §8(f) GPTQ comparator: process_hessian (gptq_utils.py:129-165) ------
+ * R (n x n f64, ld ldr) = upper Cholesky factor of inv(H_p + damp I),
+ * H_p = H[perm][:, perm] (perm may be NULL = identity; actorder's perm is
+ * computed by the caller), damp = 10^e * damp_percent * mean(diag(H)) for
+ * e = 0 .. max_tries-1 until H_p + damp I is positive definite (the
+ * reference's ladder, :148-160).  *tries_used (host) = the rung e that
+ * succeeded, or max_tries when every rung failed, in which case R = I (the
+ * reference's intended fallback, :162-164).  Synchronises the stream once
+ * per rung (the reference's try/except is a host round trip too). */
+size_t tg_hinv_chol_workspace_size(int n);
+int tg_hinv_chol(void *stream, const double *H, int n, int ldh, const int64_t *perm,
+                 double damp_percent, int max_tries, double *R, int ldr, int *tries_used,
+                 void *ws, size_t ws_bytes);
+
 /* ---- A13: packing (absent in the reference; README.md:133) ----------------
  * codes (m x n uint8, offset form) -> qweight (n*b/32 x m int32, bit stream
  * along in_features; AutoGPTQ layout for b in {2,3,4,8}); zero (m x G f32)

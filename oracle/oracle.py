@@ -192,6 +192,67 @@ def process_block(w, s, z, R, min_q: int, max_q: int):
     return q, e
 
 
+def process_block_loop(w, s, z, Hinv1, min_q: int, max_q: int):
+    """The GPTQ-comparator column loop (use_triton=False, gptq_utils.py:516-534).
+
+    For each column i: q = clamp(round_half_even(w/s + z)); qv = (q - z) s;
+    err = (w - qv) / Hinv1[i, i]; w[:, i:] -= err * Hinv1[i, i:] (the K=1
+    matmul is one rounded product per element).  Returns (Q, Err).
+    """
+    w = np.array(w, dtype=F32, copy=True)
+    s = np.asarray(s, dtype=F32)
+    z = np.asarray(z, dtype=F32)
+    Hb = np.asarray(Hinv1, dtype=F32)
+    m, B = w.shape
+    q = np.empty_like(w)
+    e = np.empty_like(w)
+    lo, hi = F32(min_q), F32(max_q)
+    for c in range(B):
+        wc = w[:, c].copy()
+        qi = np.clip(np.rint(wc / s[:, c] + z[:, c]), lo, hi)
+        qv = (qi - z[:, c]) * s[:, c]
+        err = (wc - qv) / Hb[c, c]
+        q[:, c] = qv
+        e[:, c] = err
+        w[:, c:] = w[:, c:] - err[:, None] * Hb[c, c:][None, :]
+    return q, e
+
+
+# --------------------------------------------------------------------------
+# §8(f) GPTQ comparator factor   (gptq_utils.py:129-165)
+# --------------------------------------------------------------------------
+def process_hessian(H: np.ndarray, actorder: bool = False, damp_percent: float = 0.01):
+    """Restates process_hessian: damped Cholesky ladder, then
+    chol_upper(cholesky_inverse(L)) -- LAPACK potrf / potri / potrf, the
+    routines torch's CPU path calls.  Returns (H_inv_chol, perm, rung) with
+    rung = the damping exponent used (5 = identity fallback, the reference's
+    intent; as written it raises NameError there, :147 vs :162)."""
+    import scipy.linalg
+    Hd = np.asarray(H, dtype=np.float64)
+    n = Hd.shape[0]
+    if actorder:
+        perm = np.argsort(-np.diag(Hd), kind="stable")
+        Hd = Hd[perm][:, perm]
+    else:
+        perm = np.arange(n)
+    mean_diag = float(np.mean(np.diag(Hd)))
+    if mean_diag == 0:
+        mean_diag = 1.0
+    for e in range(5):
+        damp = 10 ** e * damp_percent
+        Hdmp = Hd.copy()
+        Hdmp[np.diag_indices(n)] += damp * mean_diag
+        try:
+            L = np.linalg.cholesky(Hdmp)
+            Linv = scipy.linalg.solve_triangular(L, np.eye(n), lower=True)
+            Hinv = Linv.T @ Linv
+            R = np.linalg.cholesky(Hinv).T
+        except np.linalg.LinAlgError:
+            continue
+        return R, perm, e
+    return np.eye(n), perm, 5
+
+
 # --------------------------------------------------------------------------
 # optional C kernel for the exact loop (fast; oracle/quant_ref.c)
 # --------------------------------------------------------------------------
@@ -213,6 +274,8 @@ def _clib():
             ctypes.c_int, ctypes.c_int, ctypes.c_int,               # ldu minq maxq
             fp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]       # Q codes nthreads
         lib.qref_gptq_fwrd.restype = ctypes.c_int
+        lib.qref_gptq_fwrd_loop.argtypes = lib.qref_gptq_fwrd.argtypes
+        lib.qref_gptq_fwrd_loop.restype = ctypes.c_int
         lib.qref_block.argtypes = [
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(ctypes.c_int32), fp, ctypes.c_int]
@@ -227,7 +290,7 @@ def _fp(a):
 
 def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
               gemm: str = "fma", impl: str = "numpy", return_codes: bool = False,
-              nthreads: int = 1):
+              nthreads: int = 1, use_triton: bool = True):
     """Restates gptq_fwrd(use_triton=True) (gptq_utils.py:459-565).
 
     W (m, n) any float; U (k, n) float64/float32 (cast to f32 like :483);
@@ -237,6 +300,8 @@ def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
           "torch" = torch CPU SGEMM (the reference's CPU run),
           "numpy" = numpy SGEMM.
     impl: "numpy" (vectorised restatement) or "c" (oracle/quant_ref.c; gemm must be "fma").
+    use_triton=False: the GPTQ-comparator loop (:516-534) and the raw cross
+    rows (:544) instead of the block kernel and the diagonal-scaled rows.
     """
     W = np.asarray(W, dtype=F32)
     m, n = W.shape
@@ -253,6 +318,7 @@ def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
     codes = np.zeros((m, n), dtype=np.int32)
 
     if impl == "c" and gemm == "torch":
+        assert use_triton, "the torch-SGEMM CPU baseline restates the TruncGPTQ path only"
         # exact C block loop + torch (MKL) SGEMM for the cross-block update: the
         # reference's own CPU semantics, fast enough for the bench CPU baseline
         import torch
@@ -280,7 +346,8 @@ def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
     elif impl == "c":
         assert gemm == "fma"
         Uc = np.ascontiguousarray(U32)
-        rc = _clib().qref_gptq_fwrd(m, n, k, block_size, _fp(Wp), _fp(S), _fp(Z), _fp(Uc),
+        fn = _clib().qref_gptq_fwrd if use_triton else _clib().qref_gptq_fwrd_loop
+        rc = fn(m, n, k, block_size, _fp(Wp), _fp(S), _fp(Z), _fp(Uc),
                                     Uc.shape[1], min_q, max_q, _fp(Q),
                                     codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                     nthreads)
@@ -289,12 +356,15 @@ def gptq_fwrd(W, U, perm, w_bits=4, group_size=128, sym=False, block_size=1024,
     else:
         for i1 in range(0, k, block_size):
             i2 = min(i1 + block_size, k)
-            qb, eb = process_block(Wp[:, i1:i2], S[:, i1:i2], Z[:, i1:i2], U32[i1:i2, i1:i2],
-                                   min_q, max_q)
+            blk = process_block if use_triton else process_block_loop
+            qb, eb = blk(Wp[:, i1:i2], S[:, i1:i2], Z[:, i1:i2], U32[i1:i2, i1:i2], min_q, max_q)
             Q[:, i1:i2] = qb
             if i2 < n:
                 diag = np.diagonal(U32[i1:i2, i1:i2])
-                scale_mat = (U32[i1:i2, i2:] / diag[:, None]).astype(F32)
+                if use_triton:
+                    scale_mat = (U32[i1:i2, i2:] / diag[:, None]).astype(F32)
+                else:
+                    scale_mat = np.ascontiguousarray(U32[i1:i2, i2:])
                 if gemm == "fma":
                     delta = fma_chain_matmul(eb, scale_mat)
                 elif gemm == "torch":

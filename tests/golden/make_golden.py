@@ -124,6 +124,46 @@ def gen_pipeline(g, spec, seed):
     return name, out
 
 
+# GPTQ comparator (process_hessian + gptq_fwrd(use_triton=False)):
+# name, n, m, N, xkind, bits, group, sym, actorder, block_size, H override
+GPTQ = [
+    ("g_n256_w4a", 256, 64, 384, "gaussian", 4, 128, False, False, 256, None),
+    ("g_n384_w3s_act", 384, 48, 512, "ar1", 3, 128, True, True, 512, None),
+    ("g_n256_w4a_lowrank", 256, 40, 96, "lognormal", 4, -1, False, False, 256, None),
+    ("g_n512_w4a_b128", 512, 64, 640, "gaussian", 4, 128, False, True, 128, None),
+    ("g_n128_w4a_indef", 128, 32, 0, "indef", 4, 128, False, False, 128, "indef"),
+]
+
+
+def gen_gptq(g, spec, seed):
+    name, n, m, N, xkind, bits, group, sym, actorder, bs, hov = spec
+    gen = torch.Generator().manual_seed(seed)
+    if hov == "indef":
+        # symmetric with one negative eigenvalue (-5% of the mean diagonal):
+        # rung 1e-2 fails, 1e-1 succeeds (the damping ladder, :148-160)
+        Qm = torch.linalg.qr(torch.randn(n, n, generator=gen, dtype=torch.float64))[0]
+        ev = torch.rand(n, generator=gen, dtype=torch.float64) + 0.5
+        ev[0] = -0.05 * float(ev.mean())
+        H = (Qm * ev) @ Qm.T
+        H = (H + H.T) / 2
+        X = None
+    else:
+        X = make_x(xkind, N, n, gen)
+        acc = g.HessianAccumulator(n, "cpu")
+        acc.add_batch(X)
+        H = acc.get_hessian()
+    Hinv_chol, perm = g.process_hessian(H, actorder=actorder, damp_percent=0.01)
+    W = torch.randn(m, n, generator=gen) * 0.05
+    q = g.Quantizer(w_bits=bits, group_size=group, sym=sym)
+    final_W, k = g.gptq_fwrd(W.clone(), Hinv_chol, q, perm, block_size=bs, use_triton=False)
+    scale, zero = q.scale.squeeze(-1), q.zero.squeeze(-1)
+    out = dict(H=H.numpy(), Hinv_chol=Hinv_chol.numpy(), perm=perm.numpy().astype(np.int64),
+               W=W.numpy(), final_W=final_W.numpy(), scale=scale.numpy(), zero=zero.numpy(),
+               bits=np.int64(bits), group=np.int64(group), sym=np.bool_(sym),
+               actorder=np.bool_(actorder), block_size=np.int64(bs), k=np.int64(k))
+    return name, out
+
+
 def gen_block(g, spec, seed):
     name, m, B, bits, sym = spec
     gen = torch.Generator().manual_seed(seed)
@@ -154,6 +194,12 @@ def main():
         name, d = gen_pipeline(g, spec, 2000 + i)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name, "k =", int(d["k"]))
+    for i, spec in enumerate(GPTQ):
+        if only and spec[0] not in only:
+            continue
+        name, d = gen_gptq(g, spec, 3000 + i)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+        print("wrote", name)
 
 
 if __name__ == "__main__":
