@@ -1,0 +1,231 @@
+"""Layer-sequential quantization loop: counterpart of the reference harness
+(/root/reference/src/TruncGPTQ/quantize.py:89-252 and model_utils.py:52-181),
+§8(f) rank 1.
+
+The reference's data flow is kept exactly: capture the inputs of the first
+decoder layer; for each layer and each sequenced group (q/k/v -> o ->
+gate/up -> down), hook the group's first linear, run every calibration batch
+through the layer to accumulate H (FP64 MFMA SYRK), factorise once per group
+(``process_hessian_alt`` for "eigh", ``process_hessian`` for "gptq"),
+quantize each linear of the group with ``gptq_fwrd`` (block 1024) and write
+the dequantised weight back; then re-run the calibration batches through the
+quantised layer to produce the next layer's inputs.
+
+What differs, deliberately:
+* no ``cleanup()`` (gc + empty_cache + device synchronize) after every batch
+  and every module (quantize.py:28-35): activations and H stay resident and
+  the work is stream-ordered -- 288 GB of HBM holds a whole layer's
+  calibration set several times over;
+* the re-forward stores each batch's actual size (the reference indexes with
+  the accumulation loop's last ``curr_batch_size``, quantize.py:233-234,
+  which drops rows when n_samples % batch_size != 0);
+* OPT works: its sublayer names (``self_attn.out_proj``, ``fc1``, ``fc2``)
+  are sequenced, and no ``model.model.rotary_emb`` is required
+  (quantize.py:98 reads it and never uses it);
+* optional packing: with ``pack=True`` every quantised linear's AutoGPTQ
+  tensors are kept (``export.save_quantized`` writes them).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+import torch
+from torch import nn
+
+from .gptq_utils import (HessianAccumulator, Quantizer, gptq_fwrd, pack_quantized,
+                         process_hessian, process_hessian_alt)
+
+__all__ = ["get_layers", "get_sequenced_groups", "capture_initial_inputs", "quantize_model",
+           "adaptive_eps"]
+
+
+def get_layers(model: nn.Module) -> nn.ModuleList:
+    """Decoder layers of Llama/Qwen (model.model.layers), OPT
+    (model.model.decoder.layers), GPT-style (transformer.h); model_utils.py:52-74."""
+    inner = getattr(model, "model", None)
+    if inner is not None:
+        if hasattr(inner, "layers"):
+            return inner.layers
+        if hasattr(inner, "decoder") and hasattr(inner.decoder, "layers"):
+            return inner.decoder.layers
+    if hasattr(model, "layers"):
+        return model.layers
+    if hasattr(model, "transformer") and hasattr(model.transformer, "h"):
+        return model.transformer.h
+    raise ValueError("Could not find layers in model architecture")
+
+
+# Sublayers that read the same input share one Hessian (model_utils.py:77-108),
+# in dependency order.  OPT's names are added (its out_proj / fc1 / fc2).
+_GROUPS = [
+    ["self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj"],
+    ["self_attn.o_proj", "self_attn.out_proj"],
+    ["mlp.gate_proj", "mlp.up_proj", "fc1"],
+    ["mlp.down_proj", "fc2"],
+]
+
+
+def get_sequenced_groups(layer: nn.Module) -> List[List[str]]:
+    names = {n for n, _ in layer.named_modules()}
+    groups = []
+    for cand in _GROUPS:
+        g = [n for n in cand if n in names]
+        if g:
+            groups.append(g)
+    return groups
+
+
+def adaptive_eps(layer_name: str, base_eps: float) -> float:
+    """quantize.py:17-20: down_proj / o_proj use a 10x smaller eps."""
+    if any(x in layer_name for x in ["down_proj", "o_proj"]):
+        return base_eps * 0.1
+    return base_eps
+
+
+def _to(v, device):
+    if isinstance(v, torch.Tensor):
+        return v.to(device)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to(x, device) for x in v)
+    return v
+
+
+def _submodule(root: nn.Module, name: str) -> nn.Module:
+    cur = root
+    for p in name.split("."):
+        cur = getattr(cur, p)
+    return cur
+
+
+class _Stop(Exception):
+    pass
+
+
+def capture_initial_inputs(model: nn.Module, input_ids_list: Sequence[torch.Tensor],
+                           device="cuda", batch_size: int = 1):
+    """Inputs of the first decoder layer for every calibration sequence, plus
+    the keyword arguments the model passes it (model_utils.py:123-181)."""
+    layers = get_layers(model)
+    ids = torch.cat(list(input_ids_list), dim=0)
+    n_samples, seq_len = ids.shape
+    dtype = next(model.parameters()).dtype
+    inps = torch.zeros((n_samples, seq_len, model.config.hidden_size), dtype=dtype, device=device)
+    state: Dict[str, Any] = {"i": 0, "kwargs": None}
+    first = layers[0]
+
+    def pre_hook(mod, args, kwargs):
+        x = args[0] if args else kwargs["hidden_states"]
+        b = x.shape[0]
+        inps[state["i"]: state["i"] + b] = x.to(device)
+        state["i"] += b
+        if state["kwargs"] is None:
+            state["kwargs"] = {k: v for k, v in kwargs.items() if k != "hidden_states"}
+        raise _Stop
+
+    h = first.register_forward_pre_hook(pre_hook, with_kwargs=True)
+    cfg = getattr(model, "config", None)
+    use_cache = getattr(cfg, "use_cache", None)
+    if cfg is not None:
+        cfg.use_cache = False  # as quantize.py:67: no KV cache object in the captured kwargs
+    try:
+        model_device = next(model.parameters()).device
+        for i in range(0, n_samples, batch_size):
+            try:
+                model(ids[i: i + batch_size].to(model_device), use_cache=False)
+            except _Stop:
+                pass
+    finally:
+        h.remove()
+        if cfg is not None:
+            cfg.use_cache = use_cache
+    kw = state["kwargs"] or {}
+    for k in ("past_key_values", "past_key_value"):
+        kw.pop(k, None)
+    return inps, kw
+
+
+@torch.no_grad()
+def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mode: str = "eigh",
+                   w_bits: int = 4, group_size: int = -1, sym: bool = False, eps: float = 1e-2,
+                   threshold_method: str = "mean_trimmed", actorder: bool = False,
+                   damp_percent: float = 0.01, use_adaptive_eps: bool = False,
+                   batch_size: int = 8, device="cuda", block_size: int = 1024,
+                   pack: bool = False, offload: bool = False) -> Dict[str, Any]:
+    """Quantise every sequenced linear of `model` in place (layer by layer).
+
+    mode "eigh" = TruncGPTQ (process_hessian_alt + gptq_fwrd(use_triton=True));
+    mode "gptq" = the GPTQ comparator (process_hessian + use_triton=False).
+    `offload`: move each layer to `device` for its turn and back to the CPU
+    afterwards (the reference's policy, quantize.py:101, :239); by default
+    the model stays where it is (a whole 8B/70B model fits in 288 GB).
+    Returns {"layer_stats": [...], "total_time": s, "packed": {name: tensors}}.
+    """
+    if mode not in ("eigh", "gptq"):
+        raise ValueError(f"mode must be 'eigh' or 'gptq', got {mode!r}")
+    t_start = time.time()
+    inps, layer_kwargs = capture_initial_inputs(model, input_ids_list, device=device,
+                                                batch_size=batch_size)
+    kw = {k: _to(v, device) for k, v in layer_kwargs.items()}
+    kw["use_cache"] = False
+    outs = torch.zeros_like(inps)
+    n_samples = inps.shape[0]
+    layers = get_layers(model)
+    qual = {id(m): n for n, m in model.named_modules()}  # packed tensors use state-dict names
+    stats: List[Dict[str, Any]] = []
+    packed: Dict[str, Dict[str, torch.Tensor]] = {}
+
+    def run_layer(layer, dst: Optional[torch.Tensor]):
+        for j in range(0, n_samples, batch_size):
+            out = layer(inps[j: j + batch_size], **kw)
+            if dst is not None:
+                out = out[0] if isinstance(out, (tuple, list)) else out
+                dst[j: j + out.shape[0]] = out
+
+    for i, layer in enumerate(layers):
+        t_layer = time.time()
+        if offload:
+            layer = layer.to(device)
+        for gi, names in enumerate(get_sequenced_groups(layer)):
+            logging.info(f"[Layer {i + 1}/{len(layers)}] Group {gi + 1}: {', '.join(names)}")
+            cur_eps = adaptive_eps(names[0], eps) if use_adaptive_eps else eps
+            first = _submodule(layer, names[0])
+            acc = HessianAccumulator(first.weight.shape[1], device=device)
+            hook = first.register_forward_hook(lambda m, a, o: acc.add_batch(a[0].detach()))
+            try:
+                run_layer(layer, None)
+            finally:
+                hook.remove()
+            H = acc.get_hessian()
+            del acc
+            if mode == "eigh":
+                R, R_x, perm = process_hessian_alt(H, threshold=cur_eps,
+                                                   threshold_method=threshold_method)
+            else:
+                R, perm = process_hessian(H, actorder=actorder, damp_percent=damp_percent)
+                R_x = None
+            del H
+            for name in names:
+                sub = _submodule(layer, name)
+                q = Quantizer(w_bits=w_bits, group_size=group_size, sym=sym)
+                t0 = time.time()
+                Wq, rank = gptq_fwrd(sub.weight.data.float(), R, q, perm, block_size=block_size,
+                                     use_triton=(mode == "eigh"), R_x=R_x)
+                sub.weight.copy_(Wq)
+                full = f"layer_{i}.{name}"
+                if pack:
+                    qw, qz, sc = pack_quantized(q)
+                    packed[qual.get(id(sub), full)] = dict(qweight=qw, qzeros=qz, scales=sc)
+                dt = time.time() - t0
+                used = rank if mode == "eigh" else "N/A"
+                logging.info(f"   {name: <15} | Rank: {str(used): <4} | Time: {dt:.2f}s")
+                stats.append({"name": full, "rank": used, "time": dt})
+            del R, R_x, perm
+        run_layer(layer, outs)
+        inps, outs = outs, inps
+        if offload:
+            layers[i] = layer.to("cpu")
+        logging.info(f"[*] Layer {i + 1}/{len(layers)} completed in {time.time() - t_layer:.2f}s")
+    torch.cuda.synchronize()
+    return {"layer_stats": stats, "total_time": time.time() - t_start, "packed": packed}
