@@ -92,19 +92,20 @@ struct RowMap {
 // row_mirror), lane^7 (row_half_mirror), lane^3, lane^1 (quad_perm).
 // Each pairing flips a new bit (32, 16, 8 via 15, 4 via 7, 2 via 3, 1), so a
 // butterfly over them in this order is a full reduction / reduce-scatter.
-__device__ inline double xchg32(double x) {
+// Half-wave sums without selects: v_permlane{32,16}_swap(x, x) leaves the
+// lower half's x in one register and the upper half's in the other, lane
+// aligned, so their sum is x[l] + x[l ^ 32] (x[l] + x[l ^ 16]) in every lane.
+__device__ inline double hsum32(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
   const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  const bool up = (threadIdx.x & 32) != 0;
-  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
 }
-__device__ inline double xchg16(double x) {
+__device__ inline double hsum16(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
   const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const bool up = (threadIdx.x & 16) != 0;
-  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
 }
 template <int CTRL>
 __device__ inline double xdpp(double x) {
@@ -115,8 +116,8 @@ __device__ inline double xdpp(double x) {
 constexpr int DPP_MIRROR = 0x140, DPP_HALF_MIRROR = 0x141, DPP_XOR3 = 0x1B, DPP_XOR1 = 0xB1;
 
 __device__ inline double wave_allsum(double s) {
-  s += xchg32(s);
-  s += xchg16(s);
+  s = hsum32(s);
+  s = hsum16(s);
   s += xdpp<DPP_MIRROR>(s);
   s += xdpp<DPP_HALF_MIRROR>(s);
   s += xdpp<DPP_XOR3>(s);
@@ -132,26 +133,32 @@ __device__ inline int rs_col(int lane) {
          ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
 }
 // q_l = v0 r0[l] + v1 r1[l], formed inside the first step.
+// Swap-based reduce-scatter step: v_permlane{32,16}_swap(a, b) exchanges the
+// upper half of `a` with the lower half of `b` (lanes 32-63 / odd 16-lane
+// rows), so afterwards one register holds both halves' `a` values and the
+// other both halves' `b` values, lane-aligned: their sum is the pairwise
+// sum of `a` in the lower half and of `b` in the upper half -- no selects.
+__device__ inline double rs_swap32(double a, double b) {
+  const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+__device__ inline double rs_swap16(double a, double b) {
+  const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+
 __device__ inline double reduce_scatter32(const double (&r0)[32], const double (&r1)[32],
                                           double v0, double v1, int lane) {
   auto qf = [&](int l) { return v0 * r0[l] + v1 * r1[l]; };
   double p[16];
-  {
-    const bool up = (lane & 32) != 0;
+  // lanes 0-31 keep column k, lanes 32-63 column k + 16
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const double recv = xchg32(up ? qf(k) : qf(k + 16));
-      p[k] = (up ? qf(k + 16) : qf(k)) + recv;
-    }
-  }
-  {
-    const bool up = (lane & 16) != 0;
+  for (int k = 0; k < 16; ++k) p[k] = rs_swap32(qf(k), qf(k + 16));
+  // even 16-lane rows keep p[k], odd rows p[k + 8]
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const double recv = xchg16(up ? p[k] : p[k + 8]);
-      p[k] = (up ? p[k + 8] : p[k]) + recv;
-    }
-  }
+  for (int k = 0; k < 8; ++k) p[k] = rs_swap16(p[k], p[k + 8]);
   {
     const bool up = (lane & 8) != 0;
 #pragma unroll
@@ -226,7 +233,6 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
                                                      unsigned long long *__restrict__ qst) {
   __shared__ double prow[SB_B];
   uint64_t ph[5] = {0, 0, 0, 0, 0};
-  __shared__ double nrm[QT / 64];
   __shared__ double red[QT / 64][SB_B];
   __shared__ double qw[SB_B], taus[SB_B];
   __shared__ double Ts[SB_B][SB_B + 1];
@@ -248,6 +254,10 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
   load_row(tid + QT, r1);
   for (int idx = tid; idx < SB_B * (SB_B + 1); idx += QT) (&Ts[0][0])[idx] = 0.0;
   const int mycol = rs_col(lane);
+  // One reduction per column: with the raw column x as weights,
+  // d_l = sum_{i>j} x_i P[i][l] gives both the squared norm (l = j) and,
+  // since v = (x_i scal)_{i>j} with v_j = 1, every v^T P[:, l] =
+  // P[j][l] + scal d_l (l > j: the update, l < j: the T recurrence input).
   auto step = [&](auto jc) {
     constexpr int j = decltype(jc)::value;
     const uint64_t p0 = __builtin_amdgcn_s_memrealtime();
@@ -256,11 +266,12 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
 #pragma unroll
       for (int l = 0; l < SB_B; ++l) prow[l] = r0[l];
     }
-    const double s_w = wave_allsum(((tid > j) ? x0 * x0 : 0.0) + x1 * x1);
-    if (lane == 0) nrm[wid] = s_w;
-    __syncthreads();
+    const double d = reduce_scatter32(r0, r1, (tid > j) ? x0 : 0.0, x1, lane);
     const uint64_t p1 = __builtin_amdgcn_s_memrealtime();
-    const double s = (nrm[0] + nrm[1]) + (nrm[2] + nrm[3]);
+    if ((lane & 1) == 0) red[wid][mycol] = d;
+    __syncthreads();
+    const uint64_t p2 = __builtin_amdgcn_s_memrealtime();
+    const double s = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
     const double alpha = prow[j];
     double tau = 0.0, scal = 0.0, beta = alpha;
     if (s != 0.0) {
@@ -268,22 +279,18 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
       tau = (beta - alpha) / beta;
       scal = 1.0 / (alpha - beta);
     }
-    const double v0 = (tid > j) ? x0 * scal : (tid == j ? 1.0 : 0.0);
-    const double v1 = x1 * scal;
-    // q_l = sum_i v_i P[i][l]: l > j -> w_l, l < j -> (Y^T v)_l (q_j is never used)
-    const double q = reduce_scatter32(r0, r1, v0, v1, lane);
-    const uint64_t p2 = __builtin_amdgcn_s_memrealtime();
-    if ((lane & 1) == 0) red[wid][mycol] = q;
-    __syncthreads();
     const uint64_t p3 = __builtin_amdgcn_s_memrealtime();
     if (tid < SB_B) {
-      const double a = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+      const double dl = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+      const double a = prow[tid] + scal * dl;
       qw[tid] = a;
       Gs[tid][j] = tid < j ? a : 0.0;  // (Y^T v_j)_tid, the T recurrence input
     }
     if (tid == 0) taus[j] = tau;
     __syncthreads();
     const uint64_t p4 = __builtin_amdgcn_s_memrealtime();
+    const double v0 = (tid > j) ? x0 * scal : (tid == j ? 1.0 : 0.0);
+    const double v1 = x1 * scal;
     const double tv0 = tau * v0, tv1 = tau * v1;
 #pragma unroll
     for (int l = j + 1; l < SB_B; ++l) {
@@ -368,7 +375,7 @@ hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int 
     atexit([] {
       unsigned long long h[8];
       (void)hipMemcpy(h, qst, sizeof(h), hipMemcpyDeviceToHost);
-      fprintf(stderr, "qr per column (us): norm+bar %.2f  scal+rs %.2f  red+bar %.2f  qv+bar %.2f  upd+T %.2f (WGs %llu)\n",
+      fprintf(stderr, "qr per column (us): rs %.2f  red+bar %.2f  scal %.2f  qv+bar %.2f  upd %.2f (WGs %llu)\n",
               h[0] / 100.0 / h[5] / 32, h[1] / 100.0 / h[5] / 32, h[2] / 100.0 / h[5] / 32,
               h[3] / 100.0 / h[5] / 32, h[4] / 100.0 / h[5] / 32, h[5]);
     });

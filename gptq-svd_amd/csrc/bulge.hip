@@ -29,19 +29,20 @@ namespace {
 using tg::SB_B;
 constexpr int LDB = 2 * SB_B;
 
-__device__ inline double xchg32(double x) {
+// Half-wave sums without selects: v_permlane{32,16}_swap(x, x) leaves the
+// lower half's x in one register and the upper half's in the other, lane
+// aligned, so their sum is x[l] + x[l ^ 32] (x[l] + x[l ^ 16]) in every lane.
+__device__ inline double hsum32(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
   const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  const bool up = (threadIdx.x & 32) != 0;
-  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
 }
-__device__ inline double xchg16(double x) {
+__device__ inline double hsum16(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
   const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  const bool up = (threadIdx.x & 16) != 0;
-  return __hiloint2double(up ? h[0] : h[1], up ? l[0] : l[1]);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
 }
 template <int CTRL>
 __device__ inline double xdpp(double x) {
@@ -53,8 +54,8 @@ __device__ inline double xdpp(double x) {
 // lane^16 (permlane swaps), lane^15 / lane^7 (DPP row mirrors), lane^3,
 // lane^1 (quad_perm) flip a new bit each.
 __device__ inline double wsum(double s) {
-  s += xchg32(s);
-  s += xchg16(s);
+  s = hsum32(s);
+  s = hsum16(s);
   s += xdpp<0x140>(s);
   s += xdpp<0x141>(s);
   s += xdpp<0x1B>(s);
@@ -212,7 +213,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       u3 += e[q + 3] * vk[q + 3];
     }
     double u = (u0 + u1) + (u2 + u3);
-    u += xchg32(u);
+    u = hsum32(u);
     const double tu = tau * u;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -241,7 +242,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       w3 += vk[q + 3] * e[q + 3];
     }
     double wc = (w0 + w1) + (w2 + w3);
-    wc += xchg32(wc);
+    wc = hsum32(wc);
     if (FULL || li < nl) {
       const int c = li;
       double *Ac = Rf + at(lo + c, r1 - lo - c);
@@ -266,7 +267,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
     }
     double p = (p0 + p1) + (p2 + p3);
     PH(1)
-    p += xchg32(p);
+    p = hsum32(p);
     p *= tau;
     const double pv = wsum(hf == 0 ? p * v : 0.0);
     const double w = p - 0.5 * tau * pv * v;
