@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -52,6 +53,7 @@ struct PivWs {
   unsigned *flag;
 };
 constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
+static_assert(PGMAX * PPS % 256 == 0, "slot copy assumes whole rounds of 256 threads");
 
 template <class A>
 void piv_layout(A &ar, int n, int k, PivWs *p) {
@@ -230,11 +232,70 @@ __device__ inline void st1i(int32_t *p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+
+// Wave argmax without the LDS crossbar: partner values through
+// v_permlane{32,16}_swap (lane ^ 32, ^ 16) and DPP row mirrors / quad perms
+// (lane ^ 15, ^ 7, ^ 3, ^ 1); each pairing flips a new lane bit, so after the
+// six stages every lane holds the maximum of the strict total order used.
+__device__ inline int part32(int x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ inline int part16(int x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return (threadIdx.x & 16) ? r[0] : r[1];
+}
+template <int CTRL>
+__device__ inline int partdpp(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+template <int S>
+__device__ inline int partner(int x) {
+  if constexpr (S == 0) return part32(x);
+  else if constexpr (S == 1) return part16(x);
+  else if constexpr (S == 2) return partdpp<0x140>(x);  // row_mirror: lane ^ 15
+  else if constexpr (S == 3) return partdpp<0x141>(x);  // row_half_mirror: lane ^ 7
+  else if constexpr (S == 4) return partdpp<0x1B>(x);   // quad_perm [3,2,1,0]: lane ^ 3
+  else return partdpp<0xB1>(x);                         // quad_perm [1,0,3,2]: lane ^ 1
+}
+// (value desc, then p asc, then g asc): the dgeqp3 pivot rule with a
+// deterministic workgroup tie-break
+template <int S>
+__device__ inline void argmax_stage(double &v, int &p, int &g) {
+  const double ov = __hiloint2double(partner<S>(__double2hiint(v)), partner<S>(__double2loint(v)));
+  const int op = partner<S>(p), og = partner<S>(g);
+  if (ov > v || (ov == v && (op < p || (op == p && og < g)))) {
+    v = ov;
+    p = op;
+    g = og;
+  }
+}
+__device__ inline void wave_argmax(double &v, int &p, int &g) {
+  argmax_stage<0>(v, p, g);
+  argmax_stage<1>(v, p, g);
+  argmax_stage<2>(v, p, g);
+  argmax_stage<3>(v, p, g);
+  argmax_stage<4>(v, p, g);
+  argmax_stage<5>(v, p, g);
+}
+
 // Worker selection: the launch has at least 8 (G - 1) + 1 workgroups; each
 // takes a ticket on its XCD (HW_REG_XCC_ID) and the first XCD to hand out G
 // tickets becomes the worker set (pigeonhole: one always does); the others
 // exit.  Workers then hand data over through that XCD's L2: plain stores +
 // vmcnt(0) + agent atomic ticket, sc1 (L1-bypassing) loads.
+#ifdef TG_PIV_PHASES
+__device__ unsigned long long g_pivph[8];
+#define PVT(i)                                                                 \
+  {                                                                            \
+    const uint64_t tt = __builtin_amdgcn_s_memrealtime();                      \
+    if (i > 0 && tid == 0 && me == 0) atomicAdd(g_pivph + i - 1, tt - pvt_last); \
+    pvt_last = tt;                                                             \
+  }
+#else
+#define PVT(i)
+#endif
+
 template <int RPT>
 __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, int pe, int G,
                                                         unsigned base, PivWs w) {
@@ -242,6 +303,8 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
   __shared__ double sv[4], lrow[PB + 1];
   __shared__ int spos[4], swin[4], s_g, s_me;
   __shared__ double s_best;
+  __shared__ double slotc[PGMAX * PPS];
+  __shared__ double wrow[4][PB + 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) {
     unsigned x;
@@ -285,11 +348,18 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
   __syncthreads();
   int piv = permL[ps];
   double dpiv = w.dsc[piv];
+  // H_k[piv][row] for the next step, loaded as soon as the pivot is known
+  double hv[RPT];
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) hv[u] = w.Hk[size_t(piv) * n + min(rows[u], n - 1)];
+#ifdef TG_PIV_PHASES
+  uint64_t pvt_last = 0;
+#endif
   for (int i = ps; i < pe; ++i) {
     const int t = i - ps;
+    PVT(0)
     const double ljj = sqrt(fmax(dpiv, 0.0));
     const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
-    const double *hrow = w.Hk + size_t(piv) * n;
     double bv = -INFINITY;
     int bp = n, bu = -1;
 #pragma unroll
@@ -297,20 +367,16 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
       const int r = rows[u];
       if (r >= n) continue;
       if (r == piv) {  // the pivot row itself
-        w.L[size_t(r) * k + i] = ljj;
-        w.LT[size_t(t) * n + r] = ljj;
 #pragma unroll
         for (int l = 0; l < PB; ++l)
           if (l == t) lr[u][l] = ljj;
         continue;
       }
       if (posr[u] <= i) continue;
-      double v = hrow[r];
+      double v = hv[u];
 #pragma unroll
       for (int l = 0; l < PB; ++l) v -= l < t ? lr[u][l] * lrow[l] : 0.0;
       const double lv = v * inv;
-      w.L[size_t(r) * k + i] = lv;
-      w.LT[size_t(t) * n + r] = lv;
 #pragma unroll
       for (int l = 0; l < PB; ++l)
         if (l == t) lr[u][l] = lv;
@@ -321,47 +387,41 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
         bu = u;
       }
     }
+    PVT(1)
     if (i + 1 >= k) break;  // dgeqp3 stops after k steps: no swap into position k
-    // workgroup candidate (largest diagonal, first dgeqp3 position)
+    // workgroup candidate (largest diagonal, first dgeqp3 position); each
+    // wave's winning lane stages its row and L row in LDS
     int bw = tid;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(bv, off);
-      const int op = __shfl_xor(bp, off), ow = __shfl_xor(bw, off);
-      if (ov > bv || (ov == bv && op < bp)) {
-        bv = ov;
-        bp = op;
-        bw = ow;
-      }
-    }
+    wave_argmax(bv, bp, bw);
     if (lane == 0) {
       sv[wid] = bv;
       spos[wid] = bp;
       swin[wid] = bw;
     }
+    if (tid == bw && bu >= 0) {
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        if (u == bu) {
+          wrow[wid][0] = double(rows[u]);
+#pragma unroll
+          for (int l = 0; l < PB; ++l) wrow[wid][1 + l] = lr[u][l];
+        }
+    }
     __syncthreads();
+    PVT(2)
     int wq = 0;
 #pragma unroll
     for (int q = 1; q < 4; ++q)
       if (sv[q] > sv[wq] || (sv[q] == sv[wq] && spos[q] < spos[wq])) wq = q;
     // publish: value, position, row, the row's L panel (slot parity = step parity)
     double *mine = w.pp + (size_t(i & 1) * PGMAX + me) * PPS;
-    if (tid == swin[wq] && bu >= 0) {
-#pragma unroll
-      for (int u = 0; u < RPT; ++u)
-        if (u == bu) {
-          mine[2] = double(rows[u]);
-#pragma unroll
-          for (int l = 0; l < PB; ++l)
-            if (l <= t) mine[8 + l] = lr[u][l];
-        }
+    if (wid == 0) {  // one parallel store: [0] value, [1] position, [2] row, [8 + l] L row
+      if (lane < 3) mine[lane] = lane == 0 ? sv[wq] : (lane == 1 ? double(spos[wq]) : wrow[wq][0]);
+      else if (lane >= 8 && lane - 8 <= t) mine[lane] = wrow[wq][lane - 7];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (tid == 0) {
-      mine[0] = sv[wq];
-      mine[1] = double(spos[wq]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    PVT(3)
     // all-to-all: wait for every workgroup's candidate of this step
     if (tid == 0) {
       __hip_atomic_fetch_add(w.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -379,24 +439,34 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
     }
     __syncthreads();
     if (s_me < 0) return;
+    PVT(4)
+    // every workgroup's record (value, position, row, L row) in one round of
+    // parallel sc1 loads, so the winner's L row needs no second round trip
     const double *slots = w.pp + size_t(i & 1) * PGMAX * PPS;
+    {
+      const int nrec = G * PPS;
+      double tmp[PGMAX * PPS / 256];
+#pragma unroll
+      for (int u = 0; u < PGMAX * PPS / 256; ++u) {
+        const int x = tid + u * 256;
+        tmp[u] = x < nrec ? ld1(slots + x) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < PGMAX * PPS / 256; ++u) {
+        const int x = tid + u * 256;
+        if (x < nrec) slotc[x] = tmp[u];
+      }
+    }
+    __syncthreads();
+    PVT(5)
     if (wid == 0) {
       double v = -INFINITY;
       int p2 = n, g = lane;
       if (lane < G) {
-        v = ld1(slots + size_t(lane) * PPS);
-        p2 = int(ld1(slots + size_t(lane) * PPS + 1));
+        v = slotc[lane * PPS];
+        p2 = int(slotc[lane * PPS + 1]);
       }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(v, off);
-        const int op = __shfl_xor(p2, off), og = __shfl_xor(g, off);
-        if (ov > v || (ov == v && (op < p2 || (op == p2 && og < g)))) {
-          v = ov;
-          p2 = op;
-          g = og;
-        }
-      }
+      wave_argmax(v, p2, g);
       if (lane == 0) {
         s_best = v;
         s_g = g;
@@ -405,13 +475,14 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
     }
     __syncthreads();
     const int g = min(max(s_g, 0), G - 1), q = min(max(spos[0], i + 1), n - 1);
-    const double *win = slots + size_t(g) * PPS;
-    if (tid <= t) lrow[tid] = ld1(win + 8 + tid);
-    if (tid == 64) sv[0] = ld1(win + 2);
-    __syncthreads();
-    const int rowb = min(max(int(sv[0]), 0), n - 1);
+    const double *win = slotc + g * PPS;
+    if (tid <= t) lrow[tid] = win[8 + tid];
+    const int rowb = min(max(int(win[2]), 0), n - 1);
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) hv[u] = w.Hk[size_t(rowb) * n + min(rows[u], n - 1)];
     const int a = permL[i + 1];
     __syncthreads();
+    PVT(6)
     if (tid == 0 && q != i + 1) {  // dgeqp3 swap of positions i+1 and q (every copy)
       permL[i + 1] = rowb;
       permL[q] = a;
@@ -430,10 +501,23 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
     dpiv = s_best;
     piv = rowb;
     __syncthreads();
+    PVT(7)
   }
+  // the panel's L columns, once: row-contiguous into L, coalesced into LT
+  const int pw = min(pe, k) - ps;
 #pragma unroll
-  for (int u = 0; u < RPT; ++u)
-    if (rows[u] < n) w.dsc[rows[u]] = dsr[u];
+  for (int u = 0; u < RPT; ++u) {
+    const int r = rows[u];
+    if (r >= n) continue;
+    w.dsc[r] = dsr[u];
+#pragma unroll
+    for (int l = 0; l < PB; ++l) {
+      if (l < pw) {
+        w.L[size_t(r) * k + ps + l] = lr[u][l];
+        w.LT[size_t(l) * n + r] = lr[u][l];
+      }
+    }
+  }
 }
 
 // Rx[t][j] = L[perm[j]][t] for j >= t (upper trapezoidal), perm64 = perm.
@@ -743,6 +827,23 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
   const int G = std::max(1, std::min(PGMAX, tg::cdiv(n, 256)));
   const int rpt = tg::cdiv(n, G * 256);
   const bool persistent = rpt <= 2 && n <= 32768 && getenv("TG_PIVOT_STEPWISE") == nullptr;
+#ifdef TG_PIV_PHASES
+  static bool reg = false;
+  if (!reg) {
+    reg = true;
+    atexit([] {
+      unsigned long long h[8];
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pivph), sizeof(h));
+      double tot = 0;
+      for (int q = 0; q < 7; ++q) tot += h[q];
+      fprintf(stderr, "pivot phases (share of step time, workgroup 0):");
+      const char *nm[7] = {"local", "wgargmax", "publish", "poll", "slotcopy", "argmax+lrow",
+                           "swap"};
+      for (int q = 0; q < 7; ++q) fprintf(stderr, " %s %.2f", nm[q], h[q] / tot);
+      fprintf(stderr, "\n");
+    });
+  }
+#endif
   if (persistent && n * sizeof(int) > 64 * 1024) {
     TG_HIP(hipFuncSetAttribute((const void *)piv_panel_kernel<1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(n * sizeof(int))));
