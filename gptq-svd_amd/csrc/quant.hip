@@ -269,16 +269,128 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
 // A10: cross-block update W[:, i2:] -= E @ SM with FP32 MFMA (32x32x2).
 // acc starts at +0 and walks k in ascending order through one accumulator
 // per output element, so each output is the k-ordered fmaf chain.
-// Tile 128x128 per workgroup, 4 waves each 64x64 (2x2 MFMA tiles), K-step 32.
+// Tile 128x128 per workgroup, 4 waves each 64x64 (2x2 MFMA tiles), K-tile 32.
+// Staging: 16-B global loads with clamped addresses (out-of-range k -> 0 by
+// select; out-of-range rows/columns only feed masked outputs), the next
+// K-tile prefetched into registers while the current one is multiplied.
+// LDS keeps even and odd k apart (A: [k & 1][row][k / 2], B: [k & 1][col][k / 2],
+// runs of 20 floats: the 16-lane passes of a 16-B read hit distinct banks) so
+// one 16-B LDS read gives a lane its operands for four consecutive MFMAs
+// (lane half h = l >> 5 supplies k = kk + h).
+// Requires lde % 4 == 0 and ldsm % 4 == 0 (host falls back otherwise).
 // ---------------------------------------------------------------------------
 constexpr int GM = 128, GN = 128, GK = 32;
+constexpr int KH = GK / 2 + 4;  // floats per (k parity, row) run, padded
 
 __global__ __launch_bounds__(256) void cross_gemm_kernel(const float *__restrict__ E, int lde,
                                                          const float *__restrict__ SM, int ldsm,
                                                          float *__restrict__ W, int ldw, int m,
                                                          int nc, int K) {
+  __shared__ float As[2][GM][KH];
+  __shared__ float Bs[2][GN][KH];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, h = lane >> 5, l32 = lane & 31;
+  const int tm = blockIdx.y * GM, tn = blockIdx.x * GN;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // A: thread -> rows (tid >> 3) + 32u, k quad (tid & 7);
+  // B: k row (tid & 31), column quads (tid >> 5) + 8u
+  const int aq = tid & 7, ar = tid >> 3, br = tid & 31, bq0 = tid >> 5;
+  float4 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gi = min(tm + ar + 32 * u, m - 1);
+      const int gk = k0 + 4 * aq;  // < roundup32(K) <= lde
+      float4 v = *reinterpret_cast<const float4 *>(E + size_t(gi) * lde + gk);
+      v.x = gk < K ? v.x : 0.0f;
+      v.y = gk + 1 < K ? v.y : 0.0f;
+      v.z = gk + 2 < K ? v.z : 0.0f;
+      v.w = gk + 3 < K ? v.w : 0.0f;
+      ra[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gk = k0 + br;
+      const int gkc = min(gk, K - 1);
+      const int gj = min(tn + 4 * (bq0 + 8 * u), ldsm - 4);
+      float4 v = *reinterpret_cast<const float4 *>(SM + size_t(gkc) * ldsm + gj);
+      if (gk >= K) v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      rb[u] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = ar + 32 * u;  // k = 4 aq .. 4 aq + 3: even (4aq, 4aq+2), odd (4aq+1, 4aq+3)
+      *reinterpret_cast<float2 *>(&As[0][row][2 * aq]) = make_float2(ra[u].x, ra[u].z);
+      *reinterpret_cast<float2 *>(&As[1][row][2 * aq]) = make_float2(ra[u].y, ra[u].w);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c0 = 4 * (bq0 + 8 * u), kp = br & 1, kh = br >> 1;
+      Bs[kp][c0 + 0][kh] = rb[u].x;
+      Bs[kp][c0 + 1][kh] = rb[u].y;
+      Bs[kp][c0 + 2][kh] = rb[u].z;
+      Bs[kp][c0 + 3][kh] = rb[u].w;
+    }
+  };
+  gload(0);
+  for (int k0 = 0; k0 < K; k0 += GK) {
+    lstore();
+    __syncthreads();
+    if (k0 + GK < K) gload(k0 + GK);  // in flight during the MFMAs below
+#pragma unroll
+    for (int c = 0; c < GK / 8; ++c) {  // four MFMA k-steps (kk = 8c .. 8c + 6) per 16-B read
+      float4 av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        av[i] = *reinterpret_cast<const float4 *>(&As[h][wm * 64 + i * 32 + l32][4 * c]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bv[j] = *reinterpret_cast<const float4 *>(&Bs[h][wn * 64 + j * 32 + l32][4 * c]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][e], bv[j][e], acc[i][j], 0, 0,
+                                                             0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int gi = tm + wm * 64 + i * 32 + row;
+        const int gj = tn + wn * 64 + j * 32 + l32;
+        if (gi < m && gj < nc) {
+          float *p = W + size_t(gi) * ldw + gj;
+          *p = *p - acc[i][j][r];  // W[:, i2:] -= Global_delta   (:545)
+        }
+      }
+}
+
+// Generic fallback (unaligned leading dimensions): scalar staging.
+__global__ __launch_bounds__(256) void cross_gemm_scalar_kernel(const float *__restrict__ E,
+                                                                int lde,
+                                                                const float *__restrict__ SM,
+                                                                int ldsm, float *__restrict__ W,
+                                                                int ldw, int m, int nc, int K) {
   __shared__ float As[GM][GK + 1];
-  __shared__ float Bs[GK][GN];
+  __shared__ float Bs[GK][GN + 32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tm = blockIdx.y * GM, tn = blockIdx.x * GN;
@@ -289,24 +401,25 @@ __global__ __launch_bounds__(256) void cross_gemm_kernel(const float *__restrict
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
   for (int k0 = 0; k0 < K; k0 += GK) {
-    {  // A tile: 128 rows x 32 k
+    {
       const int row = tid >> 1, kb = (tid & 1) * 16;
-      const int gi = tm + row;
+      const int gi = min(tm + row, m - 1);
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
         const int gk = k0 + kb + t;
-        As[row][kb + t] = (gi < m && gk < K) ? E[size_t(gi) * lde + gk] : 0.0f;
+        const float v = E[size_t(gi) * lde + min(gk, K - 1)];
+        As[row][kb + t] = gk < K ? v : 0.0f;
       }
     }
-    {  // B tile: 32 k x 128 cols
+    {
       const int kr = tid >> 3, cb = (tid & 7) * 16;
-      const int gk = k0 + kr;
+      const int gk = k0 + kr, gkc = min(gk, K - 1);
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
-        const int gj = tn + cb + t;
-        Bs[kr][cb + t] = (gk < K && gj < nc) ? SM[size_t(gk) * ldsm + gj] : 0.0f;
+        const int gj = min(tn + cb + t, nc - 1);
+        const float v = SM[size_t(gkc) * ldsm + gj];
+        Bs[kr][cb + t] = gk < K ? v : 0.0f;
       }
     }
     __syncthreads();
@@ -336,7 +449,7 @@ __global__ __launch_bounds__(256) void cross_gemm_kernel(const float *__restrict
         const int gj = tn + wn * 64 + j * 32 + (lane & 31);
         if (gi < m && gj < nc) {
           float *p = W + size_t(gi) * ldw + gj;
-          *p = *p - acc[i][j][r];  // W[:, i2:] -= Global_delta   (:545)
+          *p = *p - acc[i][j][r];
         }
       }
 }
@@ -578,8 +691,12 @@ static int gptq_quantize_impl(bool loop, void *stream, const float *W, int m, in
       auto gtok = tg::prof_begin(st, tg::PROF_CROSS_GEMM,
                                  4.0 * (double(m) * bw + double(bw) * nc + 2.0 * double(m) * nc),
                                  2.0 * double(m) * bw * nc);
-      hipLaunchKernelGGL(cross_gemm_kernel, dim3(tg::cdiv(nc, GN), tg::cdiv(m, GM)), dim3(256), 0,
-                         st, q.E, bp, q.SM, n, q.Wp + i2, n, m, nc, bw);
+      if (bp % 4 == 0 && n % 4 == 0 && n >= 4)
+        hipLaunchKernelGGL(cross_gemm_kernel, dim3(tg::cdiv(nc, GN), tg::cdiv(m, GM)), dim3(256),
+                           0, st, q.E, bp, q.SM, n, q.Wp + i2, n, m, nc, bw);
+      else
+        hipLaunchKernelGGL(cross_gemm_scalar_kernel, dim3(tg::cdiv(nc, GN), tg::cdiv(m, GM)),
+                           dim3(256), 0, st, q.E, bp, q.SM, n, q.Wp + i2, n, m, nc, bw);
       tg::prof_end(st, gtok);
       TG_LAUNCHED();
     }
