@@ -549,54 +549,69 @@ __global__ void gather_scale_kernel(const double *__restrict__ Vh, int ldv, cons
 // rows become one MFMA GEMM U12 = W G12.  X = U11^-1 by back substitution,
 // one column per thread group.
 constexpr int NU = 64;
+// Cholesky: thread (column c = tid & 63, rows r0 = tid >> 6 mod 4) updates
+// a[r][c] -= U[j][r] U[j][c] for j < r <= c; the scaled row U[j][:] goes to a
+// separate matrix (row j of `a` is only read in step j), so one barrier per
+// column suffices.  Inverse X = U11^-1: four lanes of one wave per column,
+// partial sums combined by DPP quad permutes, x[i][c] handed on through LDS
+// with wave-level ordering only (no workgroup barrier).
+template <int CTRL>
+__device__ inline double dpp_d(double x) {
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
+}
 __global__ __launch_bounds__(256) void potrf_inv_kernel(double *__restrict__ U, int ldu, int p,
                                                         int pb, double *__restrict__ Wout,
                                                         int *__restrict__ info) {
   __shared__ double a[NU][NU + 1];
-  __shared__ double x[NU][NU + 1];
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
-    const int r = idx / NU, c = idx % NU;
-    a[r][c] = (r < pb && c < pb) ? U[size_t(p + r) * ldu + p + c] : (r == c ? 1.0 : 0.0);
+  __shared__ double u[NU][NU + 1];
+  const int tid = threadIdx.x, c = tid & 63, r0 = tid >> 6;
+  {
+    const double *col = U + size_t(p) * ldu + p + min(c, pb - 1);
+#pragma unroll
+    for (int q = 0; q < NU / 4; ++q) {
+      const int r = r0 + 4 * q;
+      const double v = col[size_t(min(r, pb - 1)) * ldu];  // clamped: no guarded loads
+      a[r][c] = (r < pb && c < pb) ? v : (r == c ? 1.0 : 0.0);
+    }
   }
   __syncthreads();
+  int bad = 0;
   for (int j = 0; j < NU; ++j) {
     const double djj = a[j][j];
     const double piv = sqrt(djj);
-    if (tid == 0 && !(djj > 0.0) && j < pb) atomicAdd(info, 1);
-    __syncthreads();
-    for (int c = j + 1 + tid; c < NU; c += blockDim.x) a[j][c] /= piv;
-    __syncthreads();
-    if (tid == 0) a[j][j] = piv;
-    const int m = NU - j - 1;
-    for (int idx = tid; idx < m * m; idx += blockDim.x) {
-      const int r = j + 1 + idx / m, c = j + 1 + idx % m;
-      if (c >= r) a[r][c] -= a[j][r] * a[j][c];
-    }
+    const double inv = 1.0 / piv;
+    bad |= !(djj > 0.0) && j < pb;
+    const double ujc = a[j][c] * inv;
+    if (r0 == 0) u[j][c] = c > j ? ujc : (c == j ? piv : 0.0);
+    for (int r = j + 1 + r0; r <= c; r += 4) a[r][c] -= (a[j][r] * inv) * ujc;
     __syncthreads();
   }
-  // X = U11^-1 (upper): column c by back substitution, 4 threads per column
-  // splitting each inner sum (fixed order: partials combined 0+1, 2+3, then).
+  if (tid == 0 && bad) atomicAdd(info, 1);
+  // X = U^-1 (upper) into `a` (dead now): column cc by 4 lanes, part = lane & 3
   {
-    const int c = tid >> 2, part = tid & 3;
+    const int cc = tid >> 2, part = tid & 3;
     for (int i = NU - 1; i >= 0; --i) {
-      double sacc = 0.0;
-      if (i < c)
-        for (int l = i + 1 + part; l <= c; l += 4) sacc += a[i][l] * x[l][c];
-      sacc += __shfl_xor(sacc, 1);
-      sacc += __shfl_xor(sacc, 2);
-      if (part == 0) x[i][c] = i > c ? 0.0 : ((i == c ? 1.0 : 0.0) - sacc) / a[i][i];
-      __syncthreads();
+      double s = 0.0;
+      if (i < cc)
+        for (int l = i + 1 + part; l <= cc; l += 4) s += u[i][l] * a[l][cc];
+      s += dpp_d<0xB1>(s);  // lane ^ 1
+      s += dpp_d<0x4E>(s);  // lane ^ 2
+      if (part == 0) a[i][cc] = i > cc ? 0.0 : ((i == cc ? 1.0 : 0.0) - s) / u[i][i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  for (int idx = tid; idx < pb * pb; idx += blockDim.x) {
-    const int r = idx / pb, c = idx % pb;
-    U[size_t(p + r) * ldu + p + c] = c >= r ? a[r][c] : 0.0;
+  __syncthreads();
+  for (int idx = tid; idx < pb * NU; idx += blockDim.x) {
+    const int r = idx / NU, cc = idx % NU;
+    if (cc < pb) U[size_t(p + r) * ldu + p + cc] = cc >= r ? u[r][cc] : 0.0;
   }
   // W = X^T (lower), NU x NU, row stride NU
   for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
-    const int r = idx / NU, c = idx % NU;
-    Wout[idx] = (r < pb && c < pb) ? x[c][r] : 0.0;
+    const int r = idx / NU, cc = idx % NU;
+    Wout[idx] = (r < pb && cc < pb) ? a[cc][r] : 0.0;
   }
 }
 
