@@ -7,12 +7,16 @@
 // r1 = j + 1 + s b, annihilating column j (s = 0) or the first bulge column
 // r1 - b (s > 0), and applies it two-sided to the window [r1 - b, r1 + 2b):
 //   B[R, Lft] <- H B[R, Lft],  B[R, R] <- H B[R, R] H,  B[Rgt, R] <- B[Rgt, R] H.
-// Task (j, s) overlaps sweep j-1's tasks s-1 .. s+2 only, so sweeps run as a
-// pipeline with a lag of 3 tasks.  GPU mapping: one wave per task; a
+// Task (j, s) overlaps sweep j-1's tasks s-1 .. s+2, but its overlap with
+// (j-1, s+2) is the single element B[r1 + 2b - 1][r1 + b - 1], the pivot of
+// (j-1, s+2), whose final value (beta, zeros below) is known one task early:
+// the wave that forms a reflector writes its pivot column at once (the G wave
+// of (j, s-1) for s > 0, first_refl for s = 0) and the left-block wave skips
+// it.  So sweeps run as a pipeline with a lag of LAG = 2 tasks (3 if every
+// write stayed with its task).  GPU mapping: three waves per task; a
 // workgroup owns G_SW consecutive sweeps and advances them in lock-step
-// (wave q runs task t - 3q at step t; the tasks of one step are disjoint).
-// Workgroups hand over through a per-group step counter, published with an
-// agent-scope release every PUB steps and read with an acquire.
+// (pair q runs task t - LAG q at step t; the tasks of one step are disjoint).
+// Workgroups hand over through a per-group step counter.
 //
 // Band storage (lower, with bulge room): Bst[c * LDB + d] = B[c + d][c],
 // d < 2b.  Reflectors of (j, s): V2[(j * smax + s) * b + i], tau2[j * smax + s].
@@ -67,8 +71,8 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 
 // ---------------------------------------------------------------------------
 // LDS-resident pipeline.  A workgroup owns G_SW consecutive sweeps; at step t
-// wave q runs task t - 3q.  The band columns the group touches at step t span
-// [low(t), high(t)) with high(t) - low(t) < 8b, so the group keeps them in an
+// pair q runs task t - LAG q.  The band columns the group touches at step t
+// span [low(t), high(t)) with high(t) - low(t) < 8b, so the group keeps them in an
 // LDS ring of RING band columns (64 doubles each): each step it prefetches the
 // b columns step t+1 adds, and writes back the columns no later task of the
 // group touches.  Hand-off to the next group: the write-backs are plain stores
@@ -80,7 +84,8 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // workers take sweep groups from a queue in increasing order (dependencies
 // point only to lower groups, so any number of resident workers is safe).
 // ---------------------------------------------------------------------------
-constexpr int G_SW = 2;              // sweeps per group (waves per workgroup)
+constexpr int G_SW = 2;              // sweeps per group (wave triples per workgroup)
+constexpr int LAG = 2;               // pipeline lag between consecutive sweeps (tasks)
 constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
 constexpr int NCW = 3 * G_SW;        // compute waves (three per sweep: left, diagonal, lower block)
 constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
@@ -129,14 +134,16 @@ __device__ __forceinline__ void make_refl(double x, int li, int hf, double &v, d
   v = (li == 0) ? 1.0 : x * scal;
 }
 
-// Reflector of task (j, 0) (x = B[j+1 .. j+b, j], final once task (j-1, 1)
-// has run), formed one step ahead by one wave.
-__device__ __forceinline__ void first_refl(const double (*R)[LDB], int n, int j, Refl &out) {
+// Reflector of task (j, 0) (x = B[j+1 .. j+b, j], final once task (j-1, 0)
+// has run: its G wave wrote B[j+b][j]), formed one step ahead by one wave,
+// which also writes the annihilated column (beta, 0, ..., 0).
+__device__ __forceinline__ void first_refl(double (*R)[LDB], int n, int j, Refl &out) {
   const int lane = threadIdx.x & 63, li = lane & 31, hf = lane >> 5;
   const int r1 = j + 1, L = min(SB_B, n - r1);
   const double x = R[rslot(j)][1 + min(li, L - 1)];
   double v, tau, beta;
   make_refl(li < L ? x : 0.0, li, hf, v, tau, beta);
+  if (hf == 0 && li < L) R[rslot(j)][1 + li] = (li == 0) ? beta : 0.0;
   if (hf == 0) out.v[li] = v;
   if (lane == 0) {
     out.tau = tau;
@@ -165,6 +172,13 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
   const int ng = FULL ? SB_B : min(SB_B, n - (r1 + L));
   double *Rf = &R[0][0];
   auto at = [&](int c, int d) { return rslot(c) * LDB + d; };
+  if (role == 0 && s == 0) {
+    // the left block of (j, 0) is column j (written by first_refl) next to
+    // columns that are already tridiagonal (zero in rows R): nothing to apply
+    if (hf == 0) V2[(int64_t(j) * smax) * SB_B + li] = rin.v[li];
+    if (lane == 0) tau2[int64_t(j) * smax] = rin.tau;
+    return;
+  }
   PH(0)
   // block loads (issued before the reflector is needed)
   double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li,
@@ -198,7 +212,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       }
     }
   }
-  const double v = rin.v[li], tau = rin.tau, beta = rin.beta;
+  const double v = rin.v[li], tau = rin.tau;
   double vk[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) vk[q] = rin.v[hf + 2 * q];
@@ -216,20 +230,25 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
     u = hsum32(u);
     const double tu = tau * u;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int k = hf + 2 * q;
-      e[q] = e[q] - tu * vk[q];
-      if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = e[q];
-    }
+    for (int q = 0; q < 16; ++q) e[q] = e[q] - tu * vk[q];
     if (has_next) {
-      // next reflector: x = updated column 0 of G (lanes hf == 0 hold G[li][0])
+      // next reflector: x = updated column 0 of G (lanes hf == 0 hold G[li][0]);
+      // that column is stored as its final (beta, 0, ..., 0) right away
       double vn, tn, bn;
       make_refl((FULL || li < ng) ? e[0] : 0.0, li, hf, vn, tn, bn);
-      if (hf == 0) rout.v[li] = vn;
+      if (hf == 0) {
+        rout.v[li] = vn;
+        e[0] = (li == 0) ? bn : 0.0;
+      }
       if (lane == 0) {
         rout.tau = tn;
         rout.beta = bn;
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = e[q];
     }
   } else if (role == 0) {
     // left block: w_c = sum_i v_i A[i][c]
@@ -243,15 +262,16 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
     }
     double wc = (w0 + w1) + (w2 + w3);
     wc = hsum32(wc);
-    if (FULL || li < nl) {
+    // the pivot column (lo + c == col, s > 0) was written by the G wave of
+    // (j, s-1) when it formed this reflector
+    if ((FULL || li < nl) && lo + li != col) {
       const int c = li;
       double *Ac = Rf + at(lo + c, r1 - lo - c);
-      const bool piv = (lo + c == col);
       const double twc = tau * wc;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = hf + 2 * q;
-        if (FULL || i < L) Ac[i] = piv ? (i == 0 ? beta : 0.0) : e[q] - twc * vk[q];
+        if (FULL || i < L) Ac[i] = e[q] - twc * vk[q];
       }
     }
     if (hf == 0) V2[(int64_t(j) * smax + s) * SB_B + li] = v;
@@ -304,22 +324,27 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
 __device__ inline int group_steps(int n, int nsw, int G) {
   const int j0 = G * G_SW;
   const int g = min(G_SW, nsw - j0);
-  return 3 * (g - 1) + ntasks(n, j0);
+  return LAG * (g - 1) + ntasks(n, j0);
 }
 
-// Lowest column any task of the group touches at step >= t (n if none).
+// Lowest column any task of the group touches at step >= t (n if none):
+// sweep j touches column j in first_refl (s = -1), columns >= r1 = j + 1 in
+// task 0, and columns >= r1 - b + 1 in task s > 0 (the pivot column r1 - b
+// is final before the task starts).
 __device__ inline int group_low(int n, int nsw, int j0, int g, int t) {
   int lowc = n;
   for (int q = 0; q < g; ++q) {
     const int j = j0 + q;
-    int s = t - 3 * q;
-    if (s < 0) s = 0;
+    const int s = t - LAG * q;
     if (s >= ntasks(n, j)) continue;
-    const int r1 = j + 1 + s * SB_B;
-    lowc = min(lowc, max(0, r1 - SB_B));
+    const int c = (s < 0) ? j : (s == 0) ? j + 1 : j + 2 + (s - 1) * SB_B;
+    lowc = min(lowc, c);
   }
   return lowc;
 }
+// Producer step the consumer group needs before it may load the columns of
+// its step t: low_{G-1}(T) >= high_G(t) for T >= t + 2 + LAG (G_SW - 1).
+__device__ inline int group_need(int t) { return t + 2 + LAG * (G_SW - 1); }
 // One past the highest column any task of the group touches at steps <= t.
 __device__ inline int group_high(int n, int j0, int t) {
   return min(n, j0 + 1 + (t + 1) * SB_B);
@@ -424,8 +449,8 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
       }
     };
     // initial window: [low(0), high(0))
-    int ld = max(0, j0 + 1 - SB_B), wb = ld;
-    wait_for(3 * G_SW);
+    int ld = j0, wb = ld;
+    wait_for(group_need(0));
     for (int c0 = ld; c0 < group_high(n, j0, 0); c0 += SB_B) {
       const int c1 = min(c0 + SB_B, group_high(n, j0, 0));
       load_cols(c0, c1);
@@ -440,7 +465,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
       const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
       if (wid < NCW) {
         const int pair = wid / 3, role = wid % 3;
-        const int s = t - 3 * pair;
+        const int s = t - LAG * pair;
         if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
           const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
           const bool nx = s + 1 < ntasks(n, jj);
@@ -474,7 +499,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
         // loader: columns step t + 1 adds
         const int nh = group_high(n, j0, t + 1);
         if (t + 1 < total && nh > ld) {
-          const int need = min(t + 1 + 3 * G_SW, ptotal + 1);
+          const int need = min(group_need(t + 1), ptotal + 1);
           if (G > 0 && known < need) {
             if (wlane == 0) {
               const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
