@@ -119,20 +119,38 @@ def phases(g, H, W, args):
     call("tg_truncation_rank", stream(), ptr(w), n, args.eps, 1, ptr(S), ptr(kd))
     k = int(kd.item())
     t = tick("rank", t)
-    Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
-    call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
-    t = tick("eigh_vectors", t)
-    del ws, A
+    nc, lam_k = g._complement_count(w, k)
+    path = g.spectral_path(n, k, nc, lam_k)
+    phases.path = f"{path} (nc={nc})"
+    t = time.perf_counter()
     perm = torch.empty(n, dtype=torch.int64, device=dev)
     Rx = torch.empty((k, n), dtype=torch.float64, device=dev)
-    ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
-    call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(Rx), n, ptr(ws),
-         ws.numel())
-    t = tick("pivot_order_Rx", t)
     U = torch.empty((k, n), dtype=torch.float64, device=dev)
-    ws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
-    call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n, ptr(ws),
-         ws.numel())
+    if path == "kept":
+        Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
+        call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
+        t = tick("eigh_vectors", t)
+        del ws, A
+        ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+        call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(Rx), n,
+             ptr(ws), ws.numel())
+        t = tick("pivot_order_Rx", t)
+        ws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
+        call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n, ptr(ws),
+             ws.numel())
+    else:
+        Vc = torch.empty((max(nc, 1), n), dtype=torch.float64, device=dev)
+        if nc:
+            call("tg_eigh_vectors_range", stream(), n, ptr(w), k, nc, ptr(Vc), n, ptr(ws),
+                 ws.numel())
+        t = tick("eigh_vectors", t)
+        del ws, A
+        ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+        call("tg_pivoted_factor_complement", stream(), ptr(H), n, ptr(Vc), n,
+             ptr(S[k:]) if nc else None, nc, n, k, ptr(perm), ptr(Rx), n, ptr(ws), ws.numel())
+        t = tick("pivot_order_Rx", t)
+        ws = workspace(_lib.lib.tg_ufactor_rx_workspace_size(n, k), dev)
+        call("tg_u_factor_rx", stream(), ptr(Rx), n, n, k, ptr(U), n, ptr(ws), ws.numel())
     t = tick("u_factor", t)
     q = g.Quantizer(args.bits, args.group, args.sym)
     g.gptq_fwrd(W, U, q, perm, block_size=args.block)
@@ -295,6 +313,7 @@ def main():
     if rank == 0:
         ph, _ = phases(g, H, W, args)
         extra["phases_ms"] = ph
+        extra["spectral_path"] = phases.path
         extra["kernel_ms_per_step"] = shares
         if not args.no_syrk:
             extra["syrk"] = syrk_bench(g, args, device)

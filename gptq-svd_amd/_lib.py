@@ -39,11 +39,16 @@ _SIGS = {
     "tg_eigh_workspace_size": ([_i], _sz),
     "tg_eigh_values": ([_vp, _vp, _i, _i, _vp, _vp, _sz], _i),
     "tg_eigh_vectors": ([_vp, _i, _vp, _i, _vp, _i, _vp, _sz], _i),
+    "tg_eigh_vectors_range": ([_vp, _i, _vp, _i, _i, _vp, _i, _vp, _sz], _i),
     "tg_truncation_rank": ([_vp, _vp, _i, _d, _i, _vp, _vp], _i),
     "tg_pivot_workspace_size": ([_i, _i], _sz),
     "tg_pivoted_factor": ([_vp, _vp, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _sz], _i),
     "tg_ufactor_workspace_size": ([_i, _i], _sz),
     "tg_u_factor": ([_vp, _vp, _i, _vp, _vp, _i, _i, _vp, _i, _vp, _sz], _i),
+    "tg_pivoted_factor_complement": ([_vp, _vp, _i, _vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp,
+                                      _sz], _i),
+    "tg_ufactor_rx_workspace_size": ([_i, _i], _sz),
+    "tg_u_factor_rx": ([_vp, _vp, _i, _i, _i, _vp, _i, _vp, _sz], _i),
     "tg_group_params": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp], _i),
     "tg_process_block_workspace_size": ([_i], _sz),
     "tg_process_block": ([_vp, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _i,

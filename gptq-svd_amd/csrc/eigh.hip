@@ -595,13 +595,16 @@ constexpr int BCH = 16;  // backward-sweep chunk
 
 __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
                                                    const double *__restrict__ e, int n, int k,
+                                                   int first,
                                                    const double *__restrict__ w_asc,
                                                    const double *__restrict__ bnd, int iters,
                                                    Tri w) {
+  // vector jj (column of Z) is the eigenvector of the (first + jj)-th largest eigenvalue
   const int jj = blockIdx.x * blockDim.x + threadIdx.x;
   if (jj >= k) return;
-  const double lam = w_asc[n - 1 - jj];
-  const int sl = w.slot[n - 1 - jj];
+  const int gi = n - 1 - (first + jj);  // ascending index
+  const double lam = w_asc[gi];
+  const int sl = w.slot[gi];
   const int b0 = w.bs[sl], b1 = w.be[sl];
   const double tol = fmax(DBL_EPSILON * bnd[2], 1e-300);
   const size_t K = size_t(k);
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
   n = b1 - b0;
   auto at = [&](int i) { return size_t(i) * K + jj; };
   auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
-  for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(b0 + i), uint32_t(jj)) + 0.25;
+  for (int i = 0; i < n; ++i) x[at(i)] = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
   for (int it = 0; it < iters; ++it) {
     // fused LU (dgttrf pattern) + forward substitution with the row interchanges
     double cur_d = d[0] - lam, cur_u = n > 1 ? e[0] : 0.0, xi = x[at(0)];
@@ -722,16 +725,19 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 }
 
 // Re-orthogonalise clusters of (near-)equal eigenvalues (gap <= reltol*||T||)
-// by modified Gram-Schmidt, one workgroup walking the k columns.
+// by modified Gram-Schmidt, one workgroup walking the k columns (column jj =
+// eigenvalue first + jj in descending order).
 __global__ __launch_bounds__(256) void cluster_mgs_kernel(const double *__restrict__ w_asc, int n,
-                                                          int k, const double *__restrict__ bnd,
+                                                          int k, int first,
+                                                          const double *__restrict__ bnd,
                                                           double reltol, double *__restrict__ Z) {
   __shared__ double scratch[8];
   const double gap = reltol * bnd[2];
+  const double *wd = w_asc + (n - 1 - first);  // wd[-jj] = eigenvalue of column jj
   int start = 0;
   while (start < k) {
     int end = start + 1;
-    while (end < k && fabs(w_asc[n - 1 - (end - 1)] - w_asc[n - 1 - end]) <= gap) ++end;
+    while (end < k && fabs(wd[-(end - 1)] - wd[-end]) <= gap) ++end;
     for (int c = start; c < end && end - start > 1; ++c) {
       for (int pass = 0; pass < 2; ++pass)  // MGS twice ("twice is enough")
       for (int b = start; b < c; ++b) {
@@ -950,11 +956,17 @@ extern "C" int tg_truncation_rank(void *stream, const double *w_asc, int n, doub
 
 extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, double *Vh, int ldv,
                                void *ws, size_t ws_bytes) {
+  return tg_eigh_vectors_range(stream, n, w_asc, 0, k, Vh, ldv, ws, ws_bytes);
+}
+
+extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, int first, int k,
+                                     double *Vh, int ldv, void *ws, size_t ws_bytes) {
   TG_ARG(n >= 1, 2, "n < 1");
   TG_ARG(w_asc, 3, "null w");
-  TG_ARG(k >= 1 && k <= n, 4, "k must be in [1, n]");
-  TG_ARG(Vh, 5, "null Vh");
-  TG_ARG(ldv >= n, 6, "ldv < n");
+  TG_ARG(first >= 0 && first < n, 4, "first must be in [0, n)");
+  TG_ARG(k >= 1 && first + k <= n, 5, "count must be in [1, n - first]");
+  TG_ARG(Vh, 6, "null Vh");
+  TG_ARG(ldv >= n, 7, "ldv < n");
   hipStream_t st = (hipStream_t)stream;
   tg::Arena ar(ws, ws_bytes);
   Tri w{};
@@ -967,11 +979,12 @@ extern "C" int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, 
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
   const char *ie = getenv("TG_INVIT_ITERS");
   const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
-  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k, w_asc,
-                     bnd, iters, w);
+  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k, first,
+                     w_asc, bnd, iters, w);
   tg::prof_end(st, itok);
   TG_LAUNCHED();
-  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, bnd, 1e-9, w.Z);
+  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, first, bnd, 1e-9,
+                     w.Z);
   TG_LAUNCHED();
   // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
   const bool ts = two_stage(n);

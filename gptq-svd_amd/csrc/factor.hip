@@ -815,27 +815,8 @@ extern "C" size_t tg_pivot_workspace_size(int n, int k) {
   return s.off + 256;
 }
 
-extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const double *S, int n,
-                                 int k, int64_t *perm, double *Rx, int ldr, void *ws,
-                                 size_t ws_bytes) {
-  TG_ARG(Vh, 2, "null Vh");
-  TG_ARG(ldv >= n, 3, "ldv < n");
-  TG_ARG(S, 4, "null S");
-  TG_ARG(n >= 1, 5, "n < 1");
-  TG_ARG(k >= 1 && k <= n, 6, "k must be in [1, n]");
-  TG_ARG(perm, 7, "null perm");
-  TG_ARG(!Rx || ldr >= n, 9, "ldr < n");
-  hipStream_t st = (hipStream_t)stream;
-  tg::Arena ar(ws, ws_bytes);
-  PivWs w{};
-  piv_layout(ar, n, k, &w);
-  TG_WS(ar);
-  TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
-  TG_HIP(hipMemsetAsync(w.LT, 0, sizeof(double) * PB * size_t(n), st));
-  hipLaunchKernelGGL(scale_rows_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
-                     dim3(256), 0, st, Vh, ldv, S, n, k, w.B);
-  TG_LAUNCHED();
-  TG_HIP(tg::dsyrk_tn(st, n, k, 1.0, w.B, n, 0.0, w.Hk, n));  // H_k = H_sqrt^T H_sqrt
+// Greedy diagonal pivoting on w.Hk (filled by the caller) -> perm, R_x.
+static int pivot_core(hipStream_t st, PivWs &w, int n, int k, int64_t *perm, double *Rx, int ldr) {
   const int g0 = std::min(PGMAX, tg::cdiv(n, 256));
   hipLaunchKernelGGL(piv_init_kernel, dim3(g0), dim3(256), 0, st, n, w);
   TG_LAUNCHED();
@@ -900,6 +881,66 @@ extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const 
   return 0;
 }
 
+extern "C" int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const double *S, int n,
+                                 int k, int64_t *perm, double *Rx, int ldr, void *ws,
+                                 size_t ws_bytes) {
+  TG_ARG(Vh, 2, "null Vh");
+  TG_ARG(ldv >= n, 3, "ldv < n");
+  TG_ARG(S, 4, "null S");
+  TG_ARG(n >= 1, 5, "n < 1");
+  TG_ARG(k >= 1 && k <= n, 6, "k must be in [1, n]");
+  TG_ARG(perm, 7, "null perm");
+  TG_ARG(!Rx || ldr >= n, 9, "ldr < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  PivWs w{};
+  piv_layout(ar, n, k, &w);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
+  TG_HIP(hipMemsetAsync(w.LT, 0, sizeof(double) * PB * size_t(n), st));
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
+                     dim3(256), 0, st, Vh, ldv, S, n, k, w.B);
+  TG_LAUNCHED();
+  TG_HIP(tg::dsyrk_tn(st, n, k, 1.0, w.B, n, 0.0, w.Hk, n));  // H_k = H_sqrt^T H_sqrt
+  return pivot_core(st, w, n, k, perm, Rx, ldr);
+}
+
+// Complement form: H_k = H - B_c^T B_c with B_c = diag(S_c) Vc, the nc
+// dropped eigenpairs that are not at rounding level (k < j < k + nc in
+// descending order).  Equal to V_k L_k V_k^T up to the dropped eigenvalues
+// below the rounding threshold; nc may be 0.
+extern "C" int tg_pivoted_factor_complement(void *stream, const double *H, int ldh,
+                                            const double *Vc, int ldvc, const double *Sc, int nc,
+                                            int n, int k, int64_t *perm, double *Rx, int ldr,
+                                            void *ws, size_t ws_bytes) {
+  TG_ARG(H, 2, "null H");
+  TG_ARG(ldh >= n, 3, "ldh < n");
+  TG_ARG(nc == 0 || Vc, 4, "null Vc");
+  TG_ARG(nc == 0 || ldvc >= n, 5, "ldvc < n");
+  TG_ARG(nc == 0 || Sc, 6, "null Sc");
+  TG_ARG(nc >= 0 && nc <= k && k + nc <= n, 7, "nc must be in [0, min(k, n - k)]");
+  TG_ARG(n >= 1, 8, "n < 1");
+  TG_ARG(k >= 1 && k <= n, 9, "k must be in [1, n]");
+  TG_ARG(perm, 10, "null perm");
+  TG_ARG(!Rx || ldr >= n, 12, "ldr < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  PivWs w{};
+  piv_layout(ar, n, k, &w);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(w.cnt, 0, 16 * sizeof(unsigned), st));
+  TG_HIP(hipMemsetAsync(w.LT, 0, sizeof(double) * PB * size_t(n), st));
+  TG_HIP(hipMemcpy2DAsync(w.Hk, sizeof(double) * n, H, sizeof(double) * ldh, sizeof(double) * n,
+                          n, hipMemcpyDeviceToDevice, st));
+  if (nc > 0) {
+    hipLaunchKernelGGL(scale_rows_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, nc),
+                       dim3(256), 0, st, Vc, ldvc, Sc, n, nc, w.B);
+    TG_LAUNCHED();
+    TG_HIP(tg::dsyrk_tn(st, n, nc, -1.0, w.B, n, 1.0, w.Hk, n));
+  }
+  return pivot_core(st, w, n, k, perm, Rx, ldr);
+}
+
 extern "C" size_t tg_ufactor_workspace_size(int n, int k) {
   tg::Sizer s;
   s.take<double>(size_t(k) * n);
@@ -931,6 +972,69 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   TG_LAUNCHED();
   // G[:k, :] = A[:, :k]^T A   (k x n) into U
   TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));
+  TG_HIP(chol_upper_rows(st, U, ldu, k, n, Wb, info));
+  hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
+                     dim3(256), 0, st, U, ldu, k);
+  TG_LAUNCHED();
+  return 0;
+}
+
+// U from R_x alone (complement path, no kept eigenvectors):
+// P^T H_k P = L L^T with L = R_x^T (n x k, full column rank), so
+// P^T H_k^+ P = L (L^T L)^-2 L^T = A^T A with A = S^-1 R_x, S = R_x R_x^T.
+// U is the R factor of A (positive diagonal): the first k rows of the upper
+// Cholesky factor of A^T A, as in tg_u_factor.  S = T^T T (Cholesky),
+// Y = T^-1, A = Y (Y^T R_x): all FP64 MFMA GEMMs plus two k x k factorisations.
+template <class Ar>
+static void urx_layout(Ar &ar, int n, int k, double **S, double **Y, double **Bm, double **A,
+                       double **Tt, double **Wb, int **info) {
+  const size_t h = size_t(NU) * ((tg::cdiv(k, NU) + 1) / 2);
+  auto t = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<Ar, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  double *d[6];
+  int *i0;
+  t(S ? *S : d[0], size_t(k) * k);
+  t(Y ? *Y : d[1], size_t(k) * k);
+  t(Bm ? *Bm : d[2], size_t(k) * n);
+  t(A ? *A : d[3], size_t(k) * n);
+  t(Tt ? *Tt : d[4], h * h);
+  t(Wb ? *Wb : d[5], size_t(NU) * NU);
+  t(info ? *info : i0, 16);
+}
+
+extern "C" size_t tg_ufactor_rx_workspace_size(int n, int k) {
+  tg::Sizer s;
+  urx_layout(s, n, k, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U,
+                              int ldu, void *ws, size_t ws_bytes) {
+  TG_ARG(Rx, 2, "null Rx");
+  TG_ARG(ldr >= n, 3, "ldr < n");
+  TG_ARG(n >= 1, 4, "n < 1");
+  TG_ARG(k >= 1 && k <= n, 5, "k must be in [1, n]");
+  TG_ARG(U, 6, "null U");
+  TG_ARG(ldu >= n, 7, "ldu < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  double *S, *Y, *Bm, *A, *Tt, *Wb;
+  int *info;
+  urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  TG_HIP(tg::dsyrk_nt(st, k, n, 1.0, Rx, ldr, 0.0, S, k));        // S = R_x R_x^T
+  TG_HIP(chol_upper_rows(st, S, k, k, k, Wb, info));                // S <- T, T^T T = S
+  TG_HIP(hipMemsetAsync(Y, 0, sizeof(double) * size_t(k) * k, st));
+  hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, S, k, k, Y, k);
+  TG_LAUNCHED();
+  TG_HIP(trinv_offdiag(st, S, k, Y, k, k, Tt));                     // Y = T^-1
+  TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, Y, k, Rx, ldr, 0.0, Bm, n));  // T^-T R_x
+  TG_HIP(tg::dgemm(st, false, false, k, n, k, 1.0, Y, k, Bm, n, 0.0, A, n));    // S^-1 R_x
+  TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));    // G[:k, :]
   TG_HIP(chol_upper_rows(st, U, ldu, k, n, Wb, info));
   hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
                      dim3(256), 0, st, U, ldu, k);

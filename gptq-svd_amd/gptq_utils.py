@@ -73,13 +73,44 @@ class HessianAccumulator:
 # ---------------------------------------------------------------------------
 # A2-A5  (gptq_utils.py:87-126)
 # ---------------------------------------------------------------------------
+def _complement_count(w_asc: torch.Tensor, k: int) -> Tuple[int, float]:
+    """Dropped eigenpairs above the rounding threshold n*eps*lambda_max, and
+    lambda_k (the smallest kept eigenvalue).  One 8n-byte copy; the caller
+    has already synchronised on k."""
+    w = w_asc.double().cpu()
+    n = w.numel()
+    tau = n * 2.220446049250313e-16 * max(float(w[-1]), 0.0)
+    dropped = w[:n - k]
+    return int((dropped > tau).sum()), float(w[n - k])
+
+
+def spectral_path(n: int, k: int, nc: int, lam_k: float) -> str:
+    """'complement' when the dropped eigenpairs that matter are fewer than
+    the kept ones (k > n/2 in practice) and no kept eigenvalue is clamped by
+    sqrt(max(L, 1e-12)) (gptq_utils.py:94); else 'kept'.  TG_SPECTRAL_PATH
+    = kept | complement forces one (complement only where it is exact)."""
+    import os
+    force = os.environ.get("TG_SPECTRAL_PATH", "auto")
+    ok = lam_k >= 1e-12 and nc <= k and k + nc <= n
+    if force == "kept" or not ok:
+        return "kept"
+    if force == "complement":
+        return "complement"
+    return "complement" if nc < k else "kept"
+
+
 def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
                               threshold_method: str = "mean_trimmed", want_rx: bool = True):
     """Native pipeline behind process_hessian_alt.  Returns (U, R_x, perm, S, k).
 
-    eigh (Householder tridiagonalisation + bisection + inverse iteration +
-    blocked back-transform) -> rank rule -> greedy-pivoted factor of
-    H_k = S_k^T S_k (the dgeqp3 pivot order and R_x) -> U.
+    eigh (two-stage reduction + bisection) -> rank rule -> then either
+      kept path:       eigenvectors of the k kept eigenvalues, greedy-pivoted
+                       factor of H_k = S_k^T S_k (the dgeqp3 pivot order and
+                       R_x), U = R(QR(diag(1/S_k) Vh_k P));
+      complement path: eigenvectors of the nc dropped eigenvalues above the
+                       rounding threshold only, H_k = H - B_c^T B_c, the same
+                       pivoting, U = R(QR(S^-1 R_x)), S = R_x R_x^T
+    whichever needs fewer eigenvectors.
     """
     _lib.require_cuda(H, "process_hessian_alt H")
     n = H.shape[0]
@@ -88,7 +119,8 @@ def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
     dev = H.device
     rule = _lib.RULES.get(threshold_method, 0)
     with torch.cuda.device(dev):
-        A = H.to(dtype=torch.float64).contiguous().clone()
+        Hd = H.to(dtype=torch.float64).contiguous()
+        A = Hd.clone()
         ws = workspace(_lib.lib.tg_eigh_workspace_size(n), dev)
         w = torch.empty(n, dtype=torch.float64, device=dev)
         call("tg_eigh_values", stream(), ptr(A), n, n, ptr(w), ptr(ws), ws.numel())
@@ -100,20 +132,38 @@ def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
             raise RuntimeError("process_hessian_alt: truncation rank is 0 "
                                "(threshold keeps no eigenvalue)")
         del A
-        Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
-        call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
-        del ws
+        nc, lam_k = _complement_count(w, k)
+        path = spectral_path(n, k, nc, lam_k)
         perm = torch.empty(n, dtype=torch.int64, device=dev)
-        R_x = torch.empty((k, n), dtype=torch.float64, device=dev) if want_rx else None
-        ws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
-        call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(R_x),
-             n, ptr(ws), ws.numel())
-        del ws
+        R_x = torch.empty((k, n), dtype=torch.float64, device=dev)
         U = torch.empty((k, n), dtype=torch.float64, device=dev)
-        ws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
-        call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n,
-             ptr(ws), ws.numel())
-    return U, R_x, perm, S, k
+        if path == "kept":
+            Vh = torch.empty((k, n), dtype=torch.float64, device=dev)
+            call("tg_eigh_vectors", stream(), n, ptr(w), k, ptr(Vh), n, ptr(ws), ws.numel())
+            del ws
+            pws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+            call("tg_pivoted_factor", stream(), ptr(Vh), n, ptr(S), n, k, ptr(perm), ptr(R_x),
+                 n, ptr(pws), pws.numel())
+            del pws
+            uws = workspace(_lib.lib.tg_ufactor_workspace_size(n, k), dev)
+            call("tg_u_factor", stream(), ptr(Vh), n, ptr(S), ptr(perm), n, k, ptr(U), n,
+                 ptr(uws), uws.numel())
+        else:
+            Vc = torch.empty((max(nc, 1), n), dtype=torch.float64, device=dev)
+            if nc:
+                call("tg_eigh_vectors_range", stream(), n, ptr(w), k, nc, ptr(Vc), n, ptr(ws),
+                     ws.numel())
+            del ws
+            pws = workspace(_lib.lib.tg_pivot_workspace_size(n, k), dev)
+            call("tg_pivoted_factor_complement", stream(), ptr(Hd), n, ptr(Vc), n,
+                 ptr(S[k:]) if nc else None, nc, n, k, ptr(perm), ptr(R_x), n, ptr(pws),
+                 pws.numel())
+            del pws, Vc
+            uws = workspace(_lib.lib.tg_ufactor_rx_workspace_size(n, k), dev)
+            call("tg_u_factor_rx", stream(), ptr(R_x), n, n, k, ptr(U), n, ptr(uws),
+                 uws.numel())
+        truncated_spectral_factor.last_path = (path, nc)
+    return U, (R_x if want_rx else None), perm, S, k
 
 
 def process_hessian_alt(H: torch.Tensor, threshold: float = 0.0005,

@@ -69,6 +69,11 @@ int tg_eigh_values(void *stream, double *A, int n, int lda, double *w_asc, void 
  * `V.T.flip(0)[:k]` (gptq_utils.py:95,110).  Uses the stage-1 workspace. */
 int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, double *Vh, int ldv,
                     void *ws, size_t ws_bytes);
+/* Eigenvectors of the eigenvalues first .. first+count-1 in DESCENDING
+ * order (rows of Vh, count x n).  tg_eigh_vectors(k) = range(0, k).  The
+ * complement path below asks for the dropped eigenpairs k .. k+nc-1. */
+int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, int first, int count,
+                          double *Vh, int ldv, void *ws, size_t ws_bytes);
 
 /* ---- A3: truncation rank (gptq_utils.py:97-108) ---------------------------
  * From ascending eigenvalues: S = sqrt(max(L, 1e-12)) descending, then the
@@ -92,6 +97,21 @@ int tg_pivoted_factor(void *stream, const double *Vh, int ldv, const double *S, 
 size_t tg_ufactor_workspace_size(int n, int k);
 int tg_u_factor(void *stream, const double *Vh, int ldv, const double *S, const int64_t *perm,
                 int n, int k, double *U, int ldu, void *ws, size_t ws_bytes);
+
+/* ---- A4/A5 complement path (same outputs, no kept eigenvectors) ----------
+ * When the dropped eigenpairs above rounding level are fewer than the kept
+ * ones (k > n/2, the usual case: Qwen3-8B keeps ~99.5%), H_k = H - B_c^T B_c
+ * with B_c = diag(S_c) Vc (Vc: nc x n rows = eigenvectors k .. k+nc-1 in
+ * descending order from tg_eigh_vectors_range, S_c = S_desc[k:k+nc]); the
+ * pivot order and R_x come from the same greedy pivoting as
+ * tg_pivoted_factor (workspace: tg_pivot_workspace_size(n, k)), and U from
+ * R_x alone: U = R(QR(S^-1 R_x)), S = R_x R_x^T. */
+int tg_pivoted_factor_complement(void *stream, const double *H, int ldh, const double *Vc,
+                                 int ldvc, const double *Sc, int nc, int n, int k, int64_t *perm,
+                                 double *Rx, int ldr, void *ws, size_t ws_bytes);
+size_t tg_ufactor_rx_workspace_size(int n, int k);
+int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U, int ldu,
+                   void *ws, size_t ws_bytes);
 
 /* ---- A7: Quantizer.find_params (gptq_utils.py:249-266) --------------------
  * W (m x n f32, ld ldw) -> scale, zero (m x n/g f32, ld n/g); g = group or n. */

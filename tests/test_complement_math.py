@@ -1,0 +1,74 @@
+"""CPU check of the complement path's algebra (tg_pivoted_factor_complement,
+tg_u_factor_rx) on the reference's golden vectors, in numpy.
+
+  H_k = H - B_c^T B_c,  B_c = diag(S[k:k+nc]) Vh[k:k+nc]   (nc = dropped
+        eigenpairs above the rounding threshold; the rest are noise)
+  greedy diagonal pivoting on H_k (dgeqp3's rule)  -> perm, R_x
+  U   = R(QR(S^-1 R_x)),  S = R_x R_x^T
+
+must reproduce the reference's perm exactly and its U / R_x (the references
+computed from the kept eigenvectors, gptq_utils.py:109-124).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+RTOL_EIG = 1.0  # threshold = RTOL_EIG * n * eps * lambda_max (as gptq_utils.complement_count)
+
+
+def pivoted_cholesky(Hk, k):
+    """dgeqp3 pivot rule on the Schur diagonal of Hk (largest, first position on ties)."""
+    n = Hk.shape[0]
+    A = Hk.copy()
+    order = np.arange(n)
+    L = np.zeros((n, k))
+    for i in range(k):
+        d = np.diagonal(A)[order[i:]]
+        p = i + int(np.argmax(d))
+        order[[i, p]] = order[[p, i]]
+        c = order[i]
+        piv = np.sqrt(A[c, c])
+        col = A[:, c] / piv
+        L[:, i] = col
+        A = A - np.outer(col, col)
+    Rx = L[order].T  # k x n, upper trapezoidal in pivot order
+    return order, Rx
+
+
+def complement_count(w_desc, k):
+    tau = RTOL_EIG * len(w_desc) * np.finfo(np.float64).eps * max(w_desc[0], 0.0)
+    return int(np.sum(w_desc[k:] > tau))
+
+
+@pytest.mark.parametrize("name", golden_names("p_"))
+def test_complement_path_matches_reference(oracle_mod, name):
+    d = load_golden(name)
+    if "H" in d:
+        H = d["H"]
+    else:
+        acc = oracle_mod.HessianAccumulator(d["X"].shape[1])
+        h = d["X"].shape[0] // 2
+        acc.add_batch(d["X"][:h])
+        acc.add_batch(d["X"][h:])
+        H = acc.get_hessian()
+    L, V = np.linalg.eigh(H)
+    w = L[::-1]
+    Vh = V.T[::-1]
+    S = np.sqrt(np.maximum(w, 1e-12))
+    k = oracle_mod.truncation_rank(S, float(d["eps"]), str(d["method"]))
+    assert k == int(d["k"])
+    nc = complement_count(w, k)
+    Bc = S[k:k + nc, None] * Vh[k:k + nc]
+    Hk = H - Bc.T @ Bc
+    perm, Rx = pivoted_cholesky(Hk, k)
+    assert np.array_equal(perm, d["perm"])
+    Sm = Rx @ Rx.T
+    A = np.linalg.solve(Sm, Rx)
+    _, U = np.linalg.qr(A)
+    U = U * np.sign(np.diagonal(U))[:, None]
+    U_ref = d["U"] if "U" in d else d["U32"]
+    tol = 1e-8 if "U" in d else 1e-6
+    assert np.linalg.norm(U - U_ref) / np.linalg.norm(U_ref) < tol
+    if "Rx" in d:
+        assert np.linalg.norm(Rx - d["Rx"]) / np.linalg.norm(d["Rx"]) < 1e-8

@@ -64,9 +64,12 @@ def test_fullsize_hessian(bench_layer, oracle_mod):
     assert rel(H.cpu().numpy(), acc.get_hessian()) <= 1e-14
 
 
-def test_fullsize_factor(g, bench_layer):
+@pytest.mark.parametrize("path", ["kept", "complement"])
+def test_fullsize_factor(g, bench_layer, path, monkeypatch):
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
     _, H, _, f = bench_layer
     U, R_x, perm, S, k = g.truncated_spectral_factor(H, 1e-4, "energy")
+    assert g.truncated_spectral_factor.last_path[0] == path
     assert k == f.k == 3058
     assert np.array_equal(perm.cpu().numpy(), f.perm)
     assert rel(S.cpu().numpy(), f.S) <= 1e-12
@@ -100,10 +103,13 @@ def test_fullsize_end_to_end(g, bench_layer, oracle_mod):
     assert mism <= 6e-4
 
 
-@pytest.mark.parametrize("n", [8192, 12288, 14336])
-def test_large_n_identities(g, oracle_mod, n):
+@pytest.mark.parametrize("n,path", [(8192, "kept"), (8192, "complement"), (12288, "complement"),
+                                    (14336, "complement"), (14336, "kept")])
+def test_large_n_identities(g, oracle_mod, n, path, monkeypatch):
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
     _, H = wishart(g, n, 3 * n // 4, 1)
     U, R_x, perm, S, k = g.truncated_spectral_factor(H, 1e-4, "energy")
+    assert g.truncated_spectral_factor.last_path[0] == path
     assert 0 < k <= 3 * n // 4 + 1
     assert torch.equal(torch.sort(perm).values, torch.arange(n, device=DEV))
     tr = torch.trace(H).item()

@@ -148,8 +148,11 @@ def test_eigh_one_stage(lib, monkeypatch, kind, n):
     test_eigh(lib, kind, n)
 
 
+@pytest.mark.parametrize("path", ["kept", "complement"])
 @pytest.mark.parametrize("name", golden_names("p_"))
-def test_process_hessian_alt_golden(g, oracle_mod, name):
+def test_process_hessian_alt_golden(g, oracle_mod, name, path, monkeypatch):
+    """Both spectral paths (kept eigenvectors / complement) reproduce the reference."""
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
     d = load_golden(name)
     H = d["H"] if "H" in d else None
     if H is None:
@@ -159,6 +162,7 @@ def test_process_hessian_alt_golden(g, oracle_mod, name):
         acc.add_batch(d["X"][h:])
         H = acc.get_hessian()
     U, R_x, perm, S, k = g.truncated_spectral_factor(t(H), float(d["eps"]), str(d["method"]))
+    assert g.truncated_spectral_factor.last_path[0] == path
     assert k == int(d["k"])
     assert np.array_equal(perm.cpu().numpy(), d["perm"])
     assert rel(S.cpu().numpy(), d["S"]) < 1e-12
@@ -169,9 +173,11 @@ def test_process_hessian_alt_golden(g, oracle_mod, name):
         assert rel(R_x.cpu().numpy(), d["Rx"]) < 1e-8
 
 
+@pytest.mark.parametrize("path", ["kept", "complement"])
 @pytest.mark.parametrize("name", golden_names("p_"))
-def test_end_to_end_golden(g, name):
+def test_end_to_end_golden(g, name, path, monkeypatch):
     """Own H -> own U/perm -> codes, against the reference's codes."""
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
     d = load_golden(name)
     acc = g.HessianAccumulator(d["X"].shape[1], DEV)
     h = d["X"].shape[0] // 2

@@ -49,7 +49,7 @@ def main():
         dg = R_x.diagonal().abs()
         mono = bool((dg[1:] <= dg[:-1] * (1 + 1e-12)).all().item())
         isperm = bool(torch.equal(torch.sort(perm).values, torch.arange(n, device=dev)))
-        print(json.dumps(dict(n=n, k=k, phases_ms=ph, total_ms=round(sum(ph.values()), 1),
+        print(json.dumps(dict(n=n, k=k, path=bench.phases.path, phases_ms=ph, total_ms=round(sum(ph.values()), 1),
                               factor_s=round(t_fact, 3), hk_resid=d1, hk_resid_expected=d1_exp,
                               hnorm=torch.linalg.norm(H).item(), urx_orth=orth,
                               rx_diag_monotone=mono, perm_valid=isperm)), flush=True)
