@@ -11,7 +11,11 @@
 // 16 (k-major images so fragment reads are 16 consecutive doubles).
 // f64 MFMA C/D layout (differs from f32!): col = lane & 15,
 // row = (lane >> 4) + 4 * reg  (MI355X guide §3).
+#include <rocblas/rocblas.h>
+
 #include <algorithm>
+#include <cstdlib>
+#include <unordered_map>
 
 #include "../../include/truncgptq.h"
 #include "common.h"
@@ -29,7 +33,8 @@ template <>
 __device__ inline double to_f64<__hip_bfloat16>(__hip_bfloat16 v) { return double(__bfloat162float(v)); }
 
 constexpr int KC = 16;
-constexpr int PAD = 4;
+constexpr int PAD = 16;  // row pitch = 32 banks mod 64: the two 16-lane row groups of a
+                         // ds_read_b64 half-wave hit disjoint banks
 
 // Staging of an op(X) tile into a k-major LDS image S[KC][W + PAD] covering
 // rows r0..r0+W of op(X) (op(X) is R x K) and k0..k0+KC, split into a
@@ -51,15 +56,17 @@ struct Stg {
       for (int t = 0; t < PER; ++t) v[t] = to_f64(X[int64_t(grc) * ld + min(k0 + kb + t, K - 1)]);
 #pragma unroll
       for (int t = 0; t < PER; ++t) v[t] = (gr < R && k0 + kb + t < K) ? v[t] : 0.0;
-    } else {  // one k, PER consecutive rows
+    } else {  // one k, PER rows strided by TPK (lanes of one k cover consecutive rows:
+              // coalesced loads and conflict-free LDS stores)
       constexpr int TPK = W / PER;
-      const int k = tid / TPK, rb = (tid % TPK) * PER;
+      const int k = tid / TPK, rb = tid % TPK;
       const int gk = k0 + k;
       const int gkc = min(gk, K - 1);
 #pragma unroll
-      for (int t = 0; t < PER; ++t) v[t] = to_f64(X[int64_t(gkc) * ld + min(r0 + rb + t, R - 1)]);
+      for (int t = 0; t < PER; ++t)
+        v[t] = to_f64(X[int64_t(gkc) * ld + min(r0 + rb + t * TPK, R - 1)]);
 #pragma unroll
-      for (int t = 0; t < PER; ++t) v[t] = (gk < K && r0 + rb + t < R) ? v[t] : 0.0;
+      for (int t = 0; t < PER; ++t) v[t] = (gk < K && r0 + rb + t * TPK < R) ? v[t] : 0.0;
     }
   }
   __device__ inline void store(double (*S)[W + PAD]) const {
@@ -71,19 +78,23 @@ struct Stg {
       for (int t = 0; t < PER; ++t) S[kb + t][r] = v[t];
     } else {
       constexpr int TPK = W / PER;
-      const int k = tid / TPK, rb = (tid % TPK) * PER;
+      const int k = tid / TPK, rb = tid % TPK;
 #pragma unroll
-      for (int t = 0; t < PER; ++t) S[k][rb + t] = v[t];
+      for (int t = 0; t < PER; ++t) S[k][rb + t * TPK] = v[t];
     }
   }
 };
 
 // acc += op(A)[tm:tm+BM, kb:ke] op(B)[kb:ke, tn:tn+BN], 4 waves as 2x2.
+// Double-buffered LDS, one barrier per K slab: slab s is read from buffer
+// s & 1 while the registers holding slab s+1 go to the other buffer (last
+// read in slab s-1, released by the previous barrier) and slab s+2's global
+// loads are in flight.
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>
 __device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
                                 const TB_ *__restrict__ B, int64_t ldb, int M, int N, int kb,
-                                int ke, int tm, int tn, double (*As)[BM + PAD],
-                                double (*Bs)[BN + PAD],
+                                int ke, int tm, int tn, double (*As)[KC][BM + PAD],
+                                double (*Bs)[KC][BN + PAD],
                                 doublex4 (&acc)[BM / 32][BN / 32]) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -91,32 +102,41 @@ __device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
   const int wm = wid >> 1, wn = wid & 1;
   Stg<TA_, BM, TA> sa;
   Stg<TB_, BN, !TB> sb;  // op(B) staged as op(B)^T (N x K)
-  if (kb < ke) {
-    sa.load(A, lda, M, ke, tm, kb);
-    sb.load(B, ldb, N, ke, tn, kb);
+  if (kb >= ke) return;
+  sa.load(A, lda, M, ke, tm, kb);
+  sb.load(B, ldb, N, ke, tn, kb);
+  sa.store(As[0]);
+  sb.store(Bs[0]);
+  if (kb + KC < ke) {
+    sa.load(A, lda, M, ke, tm, kb + KC);
+    sb.load(B, ldb, N, ke, tn, kb + KC);
   }
+  __syncthreads();
+  int cur = 0;
   for (int k0 = kb; k0 < ke; k0 += KC) {
-    sa.store(As);
-    sb.store(Bs);
-    __syncthreads();
-    if (k0 + KC < ke) {
-      sa.load(A, lda, M, ke, tm, k0 + KC);
-      sb.load(B, ldb, N, ke, tn, k0 + KC);
-    }
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
       double af[FM], bf[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = As[kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
+      for (int i = 0; i < FM; ++i) af[i] = As[cur][kk + (lane >> 4)][wm * WM + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = Bs[kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
+      for (int j = 0; j < FN; ++j) bf[j] = Bs[cur][kk + (lane >> 4)][wn * WN + j * 16 + (lane & 15)];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+    if (k0 + KC < ke) {
+      sa.store(As[cur ^ 1]);
+      sb.store(Bs[cur ^ 1]);
+      if (k0 + 2 * KC < ke) {
+        sa.load(A, lda, M, ke, tm, k0 + 2 * KC);
+        sb.load(B, ldb, N, ke, tn, k0 + 2 * KC);
+      }
+    }
     __syncthreads();
+    cur ^= 1;
   }
 }
 
@@ -165,8 +185,8 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
                                                     const TB_ *__restrict__ B, int64_t ldb,
                                                     double beta, double *__restrict__ C,
                                                     int64_t ldc, int kchunk, int64_t zstride) {
-  __shared__ double As[KC][BM + PAD];
-  __shared__ double Bs[KC][BN + PAD];
+  __shared__ double As[2][KC][BM + PAD];
+  __shared__ double Bs[2][KC][BN + PAD];
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
   int tm, tn;
@@ -205,8 +225,8 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
                                                             int64_t ldb, double beta,
                                                             double *__restrict__ C,
                                                             int64_t ldc) {
-  __shared__ double As[KC][BM + PAD];
-  __shared__ double Bs[KC][BN + PAD];
+  __shared__ double As[2][KC][BM + PAD];
+  __shared__ double Bs[2][KC][BN + PAD];
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
   const int z = blockIdx.z;
@@ -279,11 +299,51 @@ hipError_t syrk_t(hipStream_t st, const T *X, int64_t rows, int n, int64_t ldx, 
 
 }  // namespace
 
+namespace {
+// Plain (unfused, non-aliasing) large GEMMs go to rocBLAS's Tensile DGEMM
+// (~65 TF/s on MI355X vs ~36-40 TF/s for dgemm_kernel above).  One handle per
+// thread and device, bound to the caller's stream on every call; its device
+// workspace is disabled (size 0), so the library still allocates nothing.
+rocblas_handle blas_handle(hipStream_t st) {
+  thread_local std::unordered_map<int, rocblas_handle> handles;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto it = handles.find(dev);
+  rocblas_handle h = nullptr;
+  if (it == handles.end()) {
+    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    rocblas_set_workspace(h, nullptr, 0);
+    handles.emplace(dev, h);
+  } else {
+    h = it->second;
+  }
+  return rocblas_set_stream(h, st) == rocblas_status_success ? h : nullptr;
+}
+
+bool use_blas(int M, int N, int K, const double *A, const double *B, const double *C) {
+  static const bool off = getenv("TG_NO_ROCBLAS") != nullptr;
+  if (off || K < 32 || double(M) * N * K < double(1 << 28)) return false;
+  // rocBLAS does not allow C to alias an operand (chol_upper_rows' in-place
+  // panel solve does; it stays on dgemm_kernel)
+  return C != A && C != B;
+}
+}  // namespace
+
 namespace tg {
 hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
                  const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                  double *C, int64_t ldc) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  if (use_blas(M, N, K, A, B, C)) {
+    if (rocblas_handle h = blas_handle(st)) {
+      // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
+      const rocblas_status rs = rocblas_dgemm(
+          h, tb ? rocblas_operation_transpose : rocblas_operation_none,
+          ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &alpha, B,
+          rocblas_int(ldb), A, rocblas_int(lda), &beta, C, rocblas_int(ldc));
+      if (rs == rocblas_status_success) return hipSuccess;
+    }
+  }
   if (K <= 0) {
     // C = beta * C (alpha * 0): run with K = 0 -> the kernel writes beta*C
   }
