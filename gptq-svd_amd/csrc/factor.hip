@@ -646,6 +646,89 @@ __global__ __launch_bounds__(256) void potf2_kernel(double *__restrict__ U, int 
   }
 }
 
+// Same contract as potrf_inv_kernel, one wave and no barriers: lane c keeps
+// column c of the block (a[r] = A[r][c]) and of X = U^-1 (x[r]) in registers.
+// Step j of the Cholesky needs row j of U across lanes (U[j][r] lives in lane
+// r): every lane writes its a[j] to an LDS row, then reads the row back as
+// broadcast loads (one address per instruction, no bank conflicts).  Entries
+// below the diagonal are updated too (branch-free) and zeroed at their step.
+// The inverse is the same pattern by rows of U: X[i][c] = (d_ic -
+// sum_{l>i} U[i][l] X[l][c]) / U[i][i].
+__global__ __launch_bounds__(64) void potrf_inv_w_kernel(double *__restrict__ U, int ldu, int p,
+                                                         int pb, double *__restrict__ Wout,
+                                                         int *__restrict__ info) {
+  __shared__ double2 row2[NU / 2];
+  __shared__ double wt[NU][NU + 1];
+  double *row = reinterpret_cast<double *>(row2);
+  const int c = threadIdx.x;
+  double a[NU];
+  double *base = U + size_t(p) * ldu + p;
+  {
+    const int cc = min(c, pb - 1);
+#pragma unroll
+    for (int r = 0; r < NU; ++r) {
+      const double v = base[size_t(min(r, pb - 1)) * ldu + cc];  // clamped: no guarded loads
+      a[r] = (r < pb && c < pb) ? v : (r == c ? 1.0 : 0.0);
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < NU; ++j) {
+    row[c] = a[j];
+    __builtin_amdgcn_wave_barrier();
+    double rv[NU];
+#pragma unroll
+    for (int q = j / 2; q < NU / 2; ++q) {  // 16-B broadcast reads of row j of the update
+      const double2 t = row2[q];
+      rv[2 * q] = t.x;
+      rv[2 * q + 1] = t.y;
+    }
+    const double d = rv[j];
+    const double piv = sqrt(d);
+    const double inv = 1.0 / piv;
+    bad |= !(d > 0.0) && j < pb;
+    const double ujc = a[j] * inv;
+    a[j] = c > j ? ujc : (c == j ? piv : 0.0);
+    const double f = ujc * inv;
+#pragma unroll
+    for (int r = j + 1; r < NU; ++r) a[r] -= rv[r] * f;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (c == 0 && bad) atomicAdd(info, 1);
+  // U block (upper) back in place
+#pragma unroll
+  for (int r = 0; r < NU; ++r)
+    if (r < pb && c < pb) base[size_t(r) * ldu + c] = c >= r ? a[r] : 0.0;
+  // X = U^-1 by rows of U: X[i][c] = (d_ic - sum_{l>i} U[i][l] X[l][c]) / U[i][i];
+  // x[] overwrites a[] from the bottom (a[i] is dead once row i is in LDS)
+#pragma unroll
+  for (int i = NU - 1; i >= 0; --i) {
+    row[c] = a[i];  // row i of U
+    __builtin_amdgcn_wave_barrier();
+    double rv[NU];
+#pragma unroll
+    for (int q = i / 2; q < NU / 2; ++q) {
+      const double2 t = row2[q];
+      rv[2 * q] = t.x;
+      rv[2 * q + 1] = t.y;
+    }
+    double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+    for (int l = i + 1; l < NU; l += 2) {
+      s0 -= rv[l] * a[l];
+      if (l + 1 < NU) s1 -= rv[l + 1] * a[l + 1];
+    }
+    a[i] = (s0 + s1) / rv[i];
+    __builtin_amdgcn_wave_barrier();
+  }
+  // W = X^T (lower) through LDS for coalesced rows
+#pragma unroll
+  for (int r = 0; r < NU; ++r) wt[c][r] = (r < pb && c < pb) ? a[r] : 0.0;  // X[r][c]
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < NU; ++r) Wout[r * NU + c] = wt[r][c];
+}
+
 // Row-panel triangular solve: X = Ubb^{-T} G[p:p+pb, c] for c in [c0, n).
 // One thread per column; the column's pb unknowns live in LDS (xs[j][tid]).
 __global__ __launch_bounds__(256) void trsm_rows_kernel(double *__restrict__ U, int ldu, int p, int pb,
@@ -687,7 +770,7 @@ hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, dou
                            int *info) {
   for (int p = 0; p < k; p += NU) {
     const int pb = std::min(NU, k - p);
-    hipLaunchKernelGGL(potrf_inv_kernel, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
+    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, st, U, ldu, p, pb, Wb, info);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int c0 = p + pb;
