@@ -348,15 +348,33 @@ __device__ inline double fdiv(double a, double b) {
   return fma(fma(-b, q, a), r, q);
 }
 
+// Negative pivots of the LDL^T of T - x I (dlaebz's q recurrence).  The
+// division e2/q uses the hardware reciprocal plus one Newton step (relative
+// error ~2^-50, the count of a matrix a few ulps away) to keep the serial
+// chain short; d and e2 are read 8 ahead of the chain.
 __device__ inline int sturm_count(const double *__restrict__ d, const double *__restrict__ e2, int n,
                                   double x, double pivmin) {
   double q = d[0] - x;
   if (fabs(q) <= pivmin) q = -pivmin;
   int c = q < 0.0;
-  for (int k = 1; k < n; ++k) {
-    q = (d[k] - x) - fdiv(e2[k - 1], q);
-    if (fabs(q) <= pivmin) q = -pivmin;
-    c += q < 0.0;
+  for (int k0 = 1; k0 < n; k0 += 8) {
+    double dv[8], ev[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = min(k0 + u, n - 1);
+      dv[u] = d[k] - x;
+      ev[u] = e2[k - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (k0 + u < n) {
+        double r = __builtin_amdgcn_rcp(q);
+        r = fma(fma(-q, r, 1.0), r, r);
+        q = fma(-ev[u], r, dv[u]);
+        if (fabs(q) <= pivmin) q = -pivmin;
+        c += q < 0.0;
+      }
+    }
   }
   return c;
 }
@@ -505,7 +523,8 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
     if (j < n) c = sturm_count(dd + b0, ee2 + b0, b1 - b0, x, pivmin);
     // lanes with count(x) <= jl have x <= lambda_jl
     const unsigned long long m = __ballot(j < n && c <= jl);
-    const int a = __popcll((m >> grp_base) & ((1ull << ML) - 1));
+    const unsigned long long gm = ML == 64 ? ~0ull : ((1ull << (ML & 63)) - 1) << grp_base;
+    const int a = __popcll(m & gm);
     const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
     const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
     const double nlo = a > 0 ? xa1 : lo;
