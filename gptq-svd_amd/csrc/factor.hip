@@ -766,8 +766,83 @@ __global__ void zero_lower_kernel(double *__restrict__ U, int ldu, int k) {
 // diagonal block and its inverse in LDS (potrf_inv_kernel), the panel rows as
 // one MFMA GEMM U12 = U11^-T G12, the trailing update as a second GEMM.
 // info[0] counts non-positive pivots.
+// Low-priority side stream + events for the look-ahead (once per device).
+struct LaStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev_panel = nullptr, ev_rest = nullptr;
+};
+static hipError_t la_stream(LaStream *&out) {
+  static LaStream ls[64];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  LaStream &x = ls[dev & 63];
+  if (!x.s) {
+    int least = 0, greatest = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least)) != hipSuccess)
+      return e;
+    if ((e = hipEventCreateWithFlags(&x.ev_panel, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&x.ev_rest, hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  out = &x;
+  return hipSuccess;
+}
+
+#define LA_CHK(x)                   \
+  do {                              \
+    hipError_t e_ = (x);            \
+    if (e_ != hipSuccess) return e_; \
+  } while (0)
+
+// Look-ahead form (depth 1).  Panel i = rows [p, c0), next panel rows [c0, c1).
+// Main stream: next-panel update TA(i) (rows [c0, c1), K = panel i) ->
+// diagonal factor + panel solve of panel i+1.  Side stream, concurrently: the
+// rest of panel i's trailing update TB(i) (rows [c1, k), columns >= c1; the
+// columns [c0, c1) of those rows are below the diagonal and never read).
+// TA(i+1) writes rows that TB(i) wrote, so the main stream waits for TB(i)
+// there; the critical path per panel is max(TA + factor + solve, TB).
+static hipError_t chol_upper_rows_la(hipStream_t st, LaStream &ls, double *U, int ldu, int k,
+                                     int n, double *Wb, int *info) {
+  auto factor_solve = [&](hipStream_t s, int p) -> hipError_t {
+    const int pb = std::min(NU, k - p), c0 = p + pb;
+    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, s, U, ldu, p, pb, Wb, info);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || c0 >= n) return e;
+    double *P = U + size_t(p) * ldu + c0;
+    return tg::dgemm(s, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
+  };
+  LA_CHK(factor_solve(st, 0));
+  bool pending = false;  // a TB on the side stream the main stream has not waited for
+  for (int p = 0; p < k; p += NU) {
+    const int pb = std::min(NU, k - p), c0 = p + pb;
+    if (c0 >= k) break;
+    const int c1 = std::min(c0 + NU, k);
+    const double *P = U + size_t(p) * ldu + c0;  // panel i rows, columns >= c0
+    if (pending) LA_CHK(hipStreamWaitEvent(st, ls.ev_rest, 0));  // TB(i-1) done
+    pending = false;
+    if (c1 < k) {
+      LA_CHK(hipEventRecord(ls.ev_panel, st));  // panel i solved
+      LA_CHK(hipStreamWaitEvent(ls.s, ls.ev_panel, 0));
+      LA_CHK(tg::dgemm(ls.s, true, false, k - c1, n - c1, pb, -1.0, P + (c1 - c0), ldu,
+                       P + (c1 - c0), ldu, 1.0, U + size_t(c1) * ldu + c1, ldu));
+      LA_CHK(hipEventRecord(ls.ev_rest, ls.s));
+      pending = true;
+    }
+    LA_CHK(tg::dgemm(st, true, false, c1 - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
+                     U + size_t(c0) * ldu + c0, ldu));
+    LA_CHK(factor_solve(st, c0));
+  }
+  if (pending) LA_CHK(hipStreamWaitEvent(st, ls.ev_rest, 0));
+  return hipSuccess;
+}
+
 hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, double *Wb,
                            int *info) {
+  static const bool no_la = getenv("TG_CHOL_NO_LOOKAHEAD") != nullptr;
+  LaStream *ls = nullptr;
+  if (!no_la && k > 2 * NU && la_stream(ls) == hipSuccess)
+    return chol_upper_rows_la(st, *ls, U, ldu, k, n, Wb, info);
   for (int p = 0; p < k; p += NU) {
     const int pb = std::min(NU, k - p);
     hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, st, U, ldu, p, pb, Wb, info);
@@ -1064,10 +1139,24 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
 
 // U from R_x alone (complement path, no kept eigenvectors):
 // P^T H_k P = L L^T with L = R_x^T (n x k, full column rank), so
-// P^T H_k^+ P = L (L^T L)^-2 L^T = A^T A with A = S^-1 R_x, S = R_x R_x^T.
-// U is the R factor of A (positive diagonal): the first k rows of the upper
-// Cholesky factor of A^T A, as in tg_u_factor.  S = T^T T (Cholesky),
-// Y = T^-1, A = Y (Y^T R_x): all FP64 MFMA GEMMs plus two k x k factorisations.
+// P^T H_k^+ P = L (L^T L)^-2 L^T = A^T A with A = S^-1 R_x, S = R_x R_x^T,
+// and U is the R factor of A (positive diagonal).
+//
+// Default (one serial Cholesky).  With R_x = [R11 R12] (R11 k x k upper
+// triangular, invertible) and C = R11^-1 R12:
+//   S = R11 (I + C C^T) R11^T,  Z := R11^-1 S = R11^T + C R12^T,
+//   A = S^-1 R_x = Z^-1 R11^-1 R_x = Z^-1 [I C].
+// With N = Z Z^T = V V^T (V upper triangular, positive diagonal),
+//   A^T A = [I C]^T N^-1 [I C] = (V^-1 [I C])^T (V^-1 [I C]),
+// and V^-1 [I C] is upper trapezoidal with positive diagonal, so by
+// uniqueness of the R factor  U = [V^-1, V^-1 C].  V comes from the upper
+// Cholesky of the reversed N' = J N J = R^T R:  V = J R^T J, V^-1 = J R^-T J.
+// Work: two triangular inverses (parallel recursive GEMMs), four GEMMs and
+// ONE k x k blocked Cholesky, against two Choleskys (one over k x n rows) for
+// the form below (TG_URX_TWOCHOL=1): S = T^T T, Y = T^-1, A = Y (Y^T R_x),
+// U = first k rows of the upper Cholesky of A^T A.
+// N has the conditioning of A[:, :k]^T A[:, :k], the same matrix the second
+// Cholesky of the two-Cholesky form factors.
 template <class Ar>
 static void urx_layout(Ar &ar, int n, int k, double **S, double **Y, double **Bm, double **A,
                        double **Tt, double **Wb, int **info) {
@@ -1086,6 +1175,15 @@ static void urx_layout(Ar &ar, int n, int k, double **S, double **Y, double **Bm
   t(Tt ? *Tt : d[4], h * h);
   t(Wb ? *Wb : d[5], size_t(NU) * NU);
   t(info ? *info : i0, 16);
+}
+
+
+// N'[i][j] = N[k-1-i][k-1-j]
+__global__ void flip_both_kernel(const double *__restrict__ N, int k, double *__restrict__ Np) {
+  const int i = blockIdx.y;
+  const double *src = N + size_t(k - 1 - i) * k + (k - 1);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < k; j += gridDim.x * blockDim.x)
+    Np[size_t(i) * k + j] = src[-j];
 }
 
 extern "C" size_t tg_ufactor_rx_workspace_size(int n, int k) {
@@ -1109,6 +1207,36 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
   urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  static const bool two_chol = getenv("TG_URX_TWOCHOL") != nullptr;
+  if (!two_chol) {
+    const int m = n - k;
+    const dim3 gk(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k);
+    double *Yr = Y, *C = Bm, *ZT = S, *Nm = A;  // C: k x m (ld m)
+    TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
+    hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, Rx, ldr, k, Yr,
+                       k);
+    TG_LAUNCHED();
+    TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));                 // Yr = R11^-1
+    TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr, sizeof(double) * k,
+                            k, hipMemcpyDeviceToDevice, st));         // Z^T = R11 (+ ...)
+    if (m > 0) {
+      TG_HIP(tg::dgemm(st, false, false, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
+      TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));  // + R12 C^T
+    }
+    TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));           // N = Z Z^T
+    hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, ZT);  // N' = J N J
+    TG_LAUNCHED();
+    TG_HIP(chol_upper_rows(st, ZT, k, k, k, Wb, info));               // N' = R^T R
+    TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
+    hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, ZT, k, k, Yr, k);
+    TG_LAUNCHED();
+    TG_HIP(trinv_offdiag(st, ZT, k, Yr, k, k, Tt));                   // Yr = R^-1
+    hipLaunchKernelGGL(flip_transpose_kernel, gk, dim3(256), 0, st, Yr, k, U, int64_t(ldu));
+    TG_LAUNCHED();                                                    // U11 = V^-1 = J R^-T J
+    if (m > 0)
+      TG_HIP(tg::dgemm(st, false, false, k, m, k, 1.0, U, ldu, C, m, 0.0, U + k, ldu));  // V^-1 C
+    return 0;
+  }
   TG_HIP(tg::dsyrk_nt(st, k, n, 1.0, Rx, ldr, 0.0, S, k));        // S = R_x R_x^T
   TG_HIP(chol_upper_rows(st, S, k, k, k, Wb, info));                // S <- T, T^T T = S
   TG_HIP(hipMemsetAsync(Y, 0, sizeof(double) * size_t(k) * k, st));
