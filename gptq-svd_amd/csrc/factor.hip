@@ -839,9 +839,11 @@ static hipError_t chol_upper_rows_la(hipStream_t st, LaStream &ls, double *U, in
 
 hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, double *Wb,
                            int *info) {
-  static const bool no_la = getenv("TG_CHOL_NO_LOOKAHEAD") != nullptr;
+  // measured slower than the single-stream order on MI355X (the cross-stream
+  // event waits cost more than the overlap gains): opt-in only
+  static const bool la = getenv("TG_CHOL_LOOKAHEAD") != nullptr;
   LaStream *ls = nullptr;
-  if (!no_la && k > 2 * NU && la_stream(ls) == hipSuccess)
+  if (la && k > 2 * NU && la_stream(ls) == hipSuccess)
     return chol_upper_rows_la(st, *ls, U, ldu, k, n, Wb, info);
   for (int p = 0; p < k; p += NU) {
     const int pb = std::min(NU, k - p);
@@ -933,22 +935,41 @@ __global__ __launch_bounds__(256) void trinv_diag_kernel(const double *__restric
   }
 }
 
-// Off-diagonal blocks of Y = U^-1 (upper, n = multiple-of-NU split):
-// Y12 = -(Y11 U12) Y22, recursing on halves (diagonal blocks already in Y).
+// Off-diagonal blocks of Y = U^-1 (upper; the NU x NU diagonal blocks are
+// already in Y, everything below the diagonal is zero).  Bottom-up: at block
+// size b = NU, 2NU, ... each pair of adjacent solved blocks merges with
+// Y12 = -(Y11 U12) Y22.  All full-size pairs of a level are independent and
+// go out as two batched GEMMs; a pair whose second block is the ragged tail
+// gets two plain GEMMs.  T holds >= n*n/4 doubles.
 hipError_t trinv_offdiag(hipStream_t st, const double *U, int ldu, double *Y, int ldy, int n,
                          double *T) {
-  if (n <= NU) return hipSuccess;
-  const int nb = tg::cdiv(n, NU);
-  const int h = NU * ((nb + 1) / 2), h2 = n - h;
-  hipError_t e = trinv_offdiag(st, U, ldu, Y, ldy, h, T);
-  if (e == hipSuccess)
-    e = trinv_offdiag(st, U + size_t(h) * ldu + h, ldu, Y + size_t(h) * ldy + h, ldy, h2, T);
-  if (e != hipSuccess) return e;
-  // T = Y11 U12 (h x h2), Y12 = -T Y22
-  e = tg::dgemm(st, false, false, h, h2, h, 1.0, Y, ldy, U + h, ldu, 0.0, T, h2);
-  if (e != hipSuccess) return e;
-  return tg::dgemm(st, false, false, h, h2, h2, -1.0, T, h2, Y + size_t(h) * ldy + h, ldy, 0.0,
-                   Y + h, ldy);
+  for (int b = NU; b < n; b *= 2) {
+    const int nblk = tg::cdiv(n, b), npair = nblk / 2;
+    const bool ragged = npair > 0 && 2 * npair * b > n;
+    const int nfull = ragged ? npair - 1 : npair;
+    hipError_t e = hipSuccess;
+    if (nfull > 0) {
+      const int64_t bb = int64_t(b) * b, dy = int64_t(ldy) + 1, du = int64_t(ldu) + 1;
+      const tg::ChunkSpec c1{2 * b, nfull, 2 * b * nfull, dy, 0, du, 0, 0, bb, b, b, b};
+      e = tg::dgemm_chunked(st, false, false, c1, 1.0, Y, ldy, U + b, ldu, 0.0, T, b);
+      if (e != hipSuccess) return e;
+      const tg::ChunkSpec c2{2 * b, nfull, 2 * b * nfull, 0, bb, dy, 0, dy, 0, b, b, b};
+      e = tg::dgemm_chunked(st, false, false, c2, -1.0, T, b, Y + size_t(b) * ldy + b, ldy, 0.0,
+                            Y + b, ldy);
+      if (e != hipSuccess) return e;
+    }
+    if (ragged) {
+      const size_t s = size_t(2) * (npair - 1) * b;
+      const int b2 = n - int(s) - b;
+      e = tg::dgemm(st, false, false, b, b2, b, 1.0, Y + s * ldy + s, ldy, U + s * ldu + s + b,
+                    ldu, 0.0, T, b2);
+      if (e != hipSuccess) return e;
+      e = tg::dgemm(st, false, false, b, b2, b2, -1.0, T, b2, Y + (s + b) * ldy + s + b, ldy, 0.0,
+                    Y + s * ldy + s + b, ldy);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
 }
 
 // R[i][j] = Y[n-1-j][n-1-i] (j >= i), 0 below the diagonal
