@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/truncgptq.h"
 #include "common.h"
@@ -51,6 +52,11 @@ struct PivWs {
   double *pp;    // PGMAX x PPS  per-workgroup step partials (value, position, row, L row)
   double *bc;    // PPS          last arriver's broadcast (pivot, its L row, swap)
   unsigned *flag;
+  // candidate-set pivoting (piv_sel_kernel / piv_fill_kernel)
+  int32_t *sstate;  // [0] steps done, [1] steps of the last panel
+  int32_t *prow;    // PB  pivot rows of the panel
+  double *pinv;     // PB  1 / L[piv][step]
+  double *Lpp;      // PB x PB  L rows of the panel's pivots (panel columns)
 };
 constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
 static_assert(PGMAX * PPS % 256 == 0, "slot copy assumes whole rounds of 256 threads");
@@ -76,6 +82,10 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.perm, n);
   take(q.pos, n);
   take(q.cnt, 16);
+  take(q.sstate, 16);
+  take(q.prow, PB);
+  take(q.pinv, PB);
+  take(q.Lpp, PB * PB);
 }
 
 // B[t][c] = S[t] * Vh[t][c]    (gptq_utils.py:112)
@@ -518,6 +528,404 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Candidate-set pivoting: one workgroup picks a whole panel's pivots.
+//
+// Schur diagonals only decrease.  At the start of a panel the rows with the
+// (about) SEL largest diagonals form the candidate set C; every other
+// unpivoted row stays <= tau = max of their diagonals at panel start.  Step
+// 0 of the panel is a full argmax.  At a later step, if the best candidate
+// (diagonal desc, dgeqp3 position asc) is strictly above tau it is the exact
+// dgeqp3 choice; otherwise the panel ends there (fewer than PB steps) and the
+// next panel re-selects.  Only candidates carry their panel of L (one per
+// thread, in registers), so a step costs one H_k load and two workgroup
+// barriers instead of an all-to-all across workgroups.  piv_fill_kernel then
+// computes the panel's L columns and diagonals of ALL rows with the same
+// operation sequence (explicit fma), so candidates and the rest agree bit
+// for bit.  Selection: two 11-bit radix passes on the diagonal's bit pattern
+// (positive doubles order like their bits), set = rows strictly above the
+// crossing bin (|set| <= SEL).
+constexpr int SEL = 1024;  // candidates (= threads of piv_sel_kernel)
+
+#ifdef TG_SEL_PHASES
+__device__ unsigned long long g_selph[8];
+#define SELT(i)                                                     \
+  {                                                                 \
+    const uint64_t tt = __builtin_amdgcn_s_memtime();               \
+    if (i > 0 && threadIdx.x == 0) atomicAdd(g_selph + i - 1, tt - selt_last); \
+    selt_last = tt;                                                 \
+  }
+#else
+#define SELT(i)
+#endif
+
+__device__ inline unsigned long long dkey(double d) {
+  return d > 0.0 ? static_cast<unsigned long long>(__double_as_longlong(d)) : 0ull;
+}
+
+constexpr int STH = 512;        // threads of piv_sel_kernel (8 waves)
+constexpr int CPT = SEL / STH;  // candidates per thread
+
+// wave argmax of (v desc, p asc) carrying a row id r (positions are unique)
+template <int S>
+__device__ inline void argmax2_stage(double &v, int &p, int &r) {
+  const double ov = __hiloint2double(partner<S>(__double2hiint(v)), partner<S>(__double2loint(v)));
+  const int op = partner<S>(p), orr = partner<S>(r);
+  if (ov > v || (ov == v && op < p)) {
+    v = ov;
+    p = op;
+    r = orr;
+  }
+}
+// block argmax over STH threads; one barrier; the result in every thread
+__device__ inline void block_argmax_sel(double &v, int &p, int &r, double2 *rec) {
+  argmax2_stage<0>(v, p, r);
+  argmax2_stage<1>(v, p, r);
+  argmax2_stage<2>(v, p, r);
+  argmax2_stage<3>(v, p, r);
+  argmax2_stage<4>(v, p, r);
+  argmax2_stage<5>(v, p, r);
+  if ((threadIdx.x & 63) == 0) rec[threadIdx.x >> 6] = make_double2(v, __hiloint2double(p, r));
+  __syncthreads();
+  double2 x = rec[0];
+  v = x.x;
+  p = __double2hiint(x.y);
+  r = __double2loint(x.y);
+#pragma unroll
+  for (int q = 1; q < STH / 64; ++q) {
+    x = rec[q];
+    const int op = __double2hiint(x.y);
+    if (x.x > v || (x.x == v && op < p)) {
+      v = x.x;
+      p = op;
+      r = __double2loint(x.y);
+    }
+  }
+}
+
+// Radix pass over the keys of unpivoted rows (prefix filter (key >> 52) == b1
+// when pass == 2): crossing bin of the `target`-th largest, and the count
+// strictly above it, to out[0..1] (LDS).
+__device__ inline void radix_pass(const double *__restrict__ dsc, const int32_t *__restrict__ pos,
+                                  int n, int ps, int pass, int b1, int target, unsigned *hist,
+                                  int *out) {
+  const int tid = threadIdx.x;
+  for (int x = tid; x < 2048; x += STH) hist[x] = 0u;
+  __syncthreads();
+  for (int r0 = tid; r0 < n; r0 += 4 * STH) {
+    double dv[4];
+    int pv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // one batch of loads in flight
+      const int r = min(r0 + u * STH, n - 1);
+      dv[u] = dsc[r];
+      pv[u] = pos[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (r0 + u * STH >= n || pv[u] < ps) continue;
+      const unsigned long long key = dkey(dv[u]);
+      if (key == 0ull) continue;
+      const int d1 = int(key >> 52);
+      if (pass == 1) atomicAdd(&hist[d1], 1u);
+      else if (d1 == b1) atomicAdd(&hist[int(key >> 41) & 2047], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // lane L covers bins [2047 - 32L - 31, 2047 - 32L], scanned top-down
+    const int top = 2047 - 32 * tid;
+    int sum = 0;
+    for (int b = 0; b < 32; ++b) sum += int(hist[top - b]);
+    int pre = sum;  // inclusive prefix over lanes (top bins first)
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(pre, off);
+      if (tid >= off) pre += o;
+    }
+    int before = pre - sum;
+    if (before < target && pre >= target) {
+      for (int b = 0; b < 32; ++b) {
+        const int c = int(hist[top - b]);
+        if (before + c >= target) {
+          out[0] = top - b;
+          out[1] = before;
+          break;
+        }
+        before += c;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
+  extern __shared__ int permL[];  // n: position -> row
+  __shared__ unsigned hist[2048];
+  __shared__ int cand[SEL];
+  __shared__ double2 rec[STH / 64];
+  __shared__ double sv[STH / 64];
+  __shared__ int scnt[STH / 64];
+  __shared__ int sel[4];
+  __shared__ double lrow[PB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ps = w.sstate[0];
+  if (ps >= k) {
+    if (tid == 0) w.sstate[1] = 0;
+    return;
+  }
+  const int pe = min(ps + PB, k);
+#ifdef TG_SEL_PHASES
+  uint64_t selt_last = 0;
+#endif
+  SELT(0)
+  for (int x = tid; x < n; x += STH) permL[x] = w.perm[x];
+  // --- candidate set ---------------------------------------------------------
+  int valid = 0;
+  for (int r = tid; r < n; r += STH) valid += (w.pos[r] >= ps && dkey(w.dsc[r]) != 0ull);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) valid += __shfl_xor(valid, off);
+  if (lane == 0) scnt[wid] = valid;
+  if (tid == 0) {
+    sel[0] = -1;  // b1 (-1: every positive key is a candidate)
+    sel[2] = -1;  // b2
+  }
+  __syncthreads();
+  valid = 0;
+#pragma unroll
+  for (int q = 0; q < STH / 64; ++q) valid += scnt[q];
+  if (valid > SEL) {
+    radix_pass(w.dsc, w.pos, n, ps, 1, 0, SEL, hist, sel);  // sel[0] = b1, sel[1] = above
+    radix_pass(w.dsc, w.pos, n, ps, 2, sel[0], SEL - sel[1], hist, sel + 2);
+  }
+  const int b1 = sel[0], b2 = sel[2];
+  auto inset = [&](unsigned long long key) {
+    if (key == 0ull) return false;
+    if (b1 < 0) return true;
+    const int d1 = int(key >> 52);
+    return d1 > b1 || (d1 == b1 && (int(key >> 41) & 2047) > b2);
+  };
+  // compaction of the set, tau over the rest, full argmax for step 0
+  int mine = 0;
+  double tau = -INFINITY, bv = -INFINITY;
+  int bp = n, brow = 0;
+  for (int r = tid; r < n; r += STH) {
+    const int pr = w.pos[r];
+    if (pr < ps) continue;
+    const double d = w.dsc[r];
+    if (inset(dkey(d))) ++mine;
+    else tau = fmax(tau, d);
+    if (d > bv || (d == bv && pr < bp)) {
+      bv = d;
+      bp = pr;
+      brow = r;
+    }
+  }
+  {
+    int pre = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(pre, off);
+      if (lane >= off) pre += o;
+    }
+    double t2 = tau;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t2 = fmax(t2, __shfl_xor(t2, off));
+    __syncthreads();  // scnt reuse
+    if (lane == 63) scnt[wid] = pre;
+    if (lane == 0) sv[wid] = t2;
+    __syncthreads();
+    int base = 0;
+    tau = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < STH / 64; ++q) {
+      if (q < wid) base += scnt[q];
+      tau = fmax(tau, sv[q]);
+    }
+    int slot = base + pre - mine;
+    for (int r = tid; r < n; r += STH) {
+      if (w.pos[r] < ps) continue;
+      if (inset(dkey(w.dsc[r]))) cand[slot++] = r;
+    }
+  }
+  __syncthreads();
+  int nset = 0;
+#pragma unroll
+  for (int q = 0; q < STH / 64; ++q) nset += scnt[q];
+  block_argmax_sel(bv, bp, brow, rec);
+  int rc[CPT], posc[CPT];
+  double dc[CPT];
+  bool done[CPT];
+  double lr[CPT][PB];
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int c = tid + u * STH;
+    rc[u] = c < nset ? cand[c] : -1;
+    posc[u] = rc[u] >= 0 ? w.pos[rc[u]] : n;
+    dc[u] = rc[u] >= 0 ? w.dsc[rc[u]] : -INFINITY;
+    done[u] = rc[u] < 0;
+#pragma unroll
+    for (int l = 0; l < PB; ++l) lr[u][l] = 0.0;
+  }
+  int piv = brow, q = bp;
+  double dpiv = bv;
+  int tdone = 0;
+  SELT(1)
+  // steps unrolled: the panel column t is a compile-time register index
+  bool active = true;  // uniform
+  // one instantiation per panel column t: lr[u][t] is a static register index
+  auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
+    const int i = ps + t;
+    active = active && i < pe;
+    if (!active) return;
+    if (t > 0) {  // candidate argmax; exact only above tau
+      double v = -INFINITY;
+      int p = n, r = -1;
+#pragma unroll
+      for (int u = 0; u < CPT; ++u)
+        if (!done[u] && (dc[u] > v || (dc[u] == v && posc[u] < p))) {
+          v = dc[u];
+          p = posc[u];
+          r = rc[u];
+        }
+      SELT(4)
+      block_argmax_sel(v, p, r, rec);
+      SELT(5)
+      active = v > tau;
+      if (!active) return;
+      dpiv = v;
+      q = p;
+      piv = r;
+    }
+    const double ljj = sqrt(fmax(dpiv, 0.0));
+    const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
+    double hv[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
+      hv[u] = (!done[u] && rc[u] != piv) ? w.Hk[size_t(piv) * n + rc[u]] : 0.0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u)
+      if (rc[u] == piv) {
+#pragma unroll
+        for (int l = 0; l < t; ++l) lrow[l] = lr[u][l];
+      }
+    if (tid == 0) {
+      const int a = permL[i];
+      if (q != i) {
+        permL[i] = piv;
+        permL[q] = a;
+      }
+      w.prow[t] = piv;
+      w.pinv[t] = inv;
+    }
+    SELT(2)
+    __syncthreads();
+    SELT(3)
+    if (tid <= t) w.Lpp[t * PB + tid] = tid < t ? lrow[tid] : ljj;
+    double lrw[PB > 1 ? PB : 1];
+#pragma unroll
+    for (int l = 0; l < t; ++l) lrw[l] = lrow[l];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      if (rc[u] == piv) {  // dgeqp3 swap of positions i and q
+        posc[u] = i;
+        lr[u][t] = ljj;
+        done[u] = true;
+      } else if (!done[u]) {
+        if (posc[u] == i && q != i) posc[u] = q;
+        double v = hv[u];
+#pragma unroll
+        for (int l = 0; l < t; ++l) v = fma(-lr[u][l], lrw[l], v);
+        const double lv = v * inv;
+        lr[u][t] = lv;
+        dc[u] = fma(-lv, lv, dc[u]);
+      }
+    }
+    tdone = t + 1;
+  };
+  [&]<int... Ts>(std::integer_sequence<int, Ts...>) __attribute__((always_inline)) {
+    (step(std::integral_constant<int, Ts>{}), ...);
+  }(std::make_integer_sequence<int, PB>{});
+  SELT(6)
+  __syncthreads();
+  for (int x = tid; x < n; x += STH) {
+    const int r = permL[x];
+    w.perm[x] = r;
+    w.pos[r] = x;
+  }
+  if (tid == 0) {
+    w.sstate[0] = ps + tdone;
+    w.sstate[1] = tdone;
+  }
+}
+
+// The last panel's L columns (L row-major, LT panel column-major) and Schur
+// diagonals of every row, with piv_sel_kernel's operation sequence.  Rows
+// pivoted in earlier panels keep LT = 0; LT rows past the panel's steps are 0.
+__global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w) {
+  __shared__ double lpp[PB][PB + 1];
+  __shared__ double pinv[PB];
+  __shared__ int prow[PB];
+  const int tid = threadIdx.x;
+  const int tn = w.sstate[1];
+  if (tn <= 0) return;
+  const int ps = w.sstate[0] - tn;
+  for (int x = tid; x < PB * PB; x += 256) {
+    const int i = x / PB, l = x % PB;
+    lpp[i][l] = (i < tn && l <= i) ? w.Lpp[x] : 0.0;
+  }
+  if (tid < PB) {
+    pinv[tid] = tid < tn ? w.pinv[tid] : 0.0;
+    prow[tid] = tid < tn ? w.prow[tid] : -1;
+  }
+  __syncthreads();
+  const int r = blockIdx.x * 256 + tid;
+  if (r >= n) return;
+  if (w.pos[r] < ps) {  // pivoted in an earlier panel
+#pragma unroll
+    for (int l = 0; l < PB; ++l) w.LT[size_t(l) * n + r] = 0.0;
+    return;
+  }
+  double hv[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? w.Hk[size_t(prow[i]) * n + r] : 0.0;
+  double d = w.dsc[r];
+  double lr[PB];
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    lr[i] = 0.0;
+    if (i >= tn || done) continue;
+    if (prow[i] == r) {
+      lr[i] = lpp[i][i];
+      done = true;
+      continue;
+    }
+    double v = hv[i];
+#pragma unroll
+    for (int l = 0; l < PB; ++l)
+      if (l < i) v = fma(-lr[l], lpp[i][l], v);
+    const double lv = v * pinv[i];
+    lr[i] = lv;
+    d = fma(-lv, lv, d);
+  }
+  w.dsc[r] = d;
+#pragma unroll
+  for (int l = 0; l < PB; ++l) {
+    if (l < tn) w.L[size_t(r) * k + ps + l] = lr[l];
+    w.LT[size_t(l) * n + r] = lr[l];
+  }
+}
+
+// dsc = diag(Hk), perm = pos = identity, no pivot chosen yet.
+__global__ __launch_bounds__(256) void piv_init2_kernel(int n, PivWs w) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    w.dsc[j] = w.Hk[size_t(j) * n + j];
+    w.perm[j] = j;
+    w.pos[j] = j;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 16) w.sstate[threadIdx.x] = 0;
 }
 
 // Rx[t][j] = L[perm[j]][t] for j >= t (upper trapezoidal), perm64 = perm.
@@ -995,7 +1403,67 @@ extern "C" size_t tg_pivot_workspace_size(int n, int k) {
 }
 
 // Greedy diagonal pivoting on w.Hk (filled by the caller) -> perm, R_x.
+// Candidate-set pivot order (piv_sel_kernel + piv_fill_kernel per panel).
+// Panels end early when the candidate bound fails, so the host launches the
+// panels full panels would need, reads the step count once, and continues
+// while steps remain.  The Schur update of a round's last panel is issued
+// only once more steps are known to follow.
+static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
+#ifdef TG_SEL_PHASES
+  static bool reg = false;
+  if (!reg) {
+    reg = true;
+    atexit([] {
+      unsigned long long h[8];
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_selph), sizeof(h));
+      const char *nm[7] = {"select", "head", "barrier2", "compute+wargmax", "blockargmax", "?", "tail"};
+      fprintf(stderr, "sel phases (cycles, thread 0):");
+      for (int q = 0; q < 7; ++q) fprintf(stderr, " %s %.3g", nm[q], double(h[q]));
+      fprintf(stderr, "\n");
+    });
+  }
+#endif
+  hipLaunchKernelGGL(piv_init2_kernel, dim3(std::min(64, tg::cdiv(n, 256))), dim3(256), 0, st, n, w);
+  TG_LAUNCHED();
+  const size_t lds = sizeof(int) * size_t(n);
+  if (lds > 48 * 1024)
+    TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  int done = 0;
+  for (int round = 0;; ++round) {
+    if (round > 4 * (k / PB + 2)) {
+      tg::set_error("pivot order: no progress after %d rounds (%d of %d steps)", round, done, k);
+      return int(hipErrorUnknown);
+    }
+    const int P = tg::cdiv(k - done, PB);
+    for (int p = 0; p < P; ++p) {
+      auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n) * PB * 3, 0.0);
+      hipLaunchKernelGGL(piv_sel_kernel, dim3(1), dim3(STH), lds, st, n, k, w);
+      hipLaunchKernelGGL(piv_fill_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, n, k, w);
+      tg::prof_end(st, tok);
+      TG_LAUNCHED();
+      if (p + 1 < P) TG_HIP(tg::dsyrk_tn(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
+    }
+    int32_t h = 0;
+    TG_HIP(hipMemcpyAsync(&h, w.sstate, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    TG_HIP(hipStreamSynchronize(st));
+    if (h >= k) break;
+    done = h;
+    TG_HIP(tg::dsyrk_tn(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
+  }
+  return 0;
+}
+
 static int pivot_core(hipStream_t st, PivWs &w, int n, int k, int64_t *perm, double *Rx, int ldr) {
+  static const bool old_pivot = getenv("TG_PIVOT_OLD") != nullptr;
+  if (!old_pivot && n <= 32768) {
+    const int e = pivot_core_sel(st, w, n, k);
+    if (e != 0) return e;
+    hipLaunchKernelGGL(rx_gather_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
+                       dim3(256), 0, st, n, k, w, Rx, ldr, perm);
+    TG_LAUNCHED();
+    return 0;
+  }
   const int g0 = std::min(PGMAX, tg::cdiv(n, 256));
   hipLaunchKernelGGL(piv_init_kernel, dim3(g0), dim3(256), 0, st, n, w);
   TG_LAUNCHED();
