@@ -547,7 +547,8 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
 // for bit.  Selection: two 11-bit radix passes on the diagonal's bit pattern
 // (positive doubles order like their bits), set = rows strictly above the
 // crossing bin (|set| <= SEL).
-constexpr int SEL = 1024;  // candidates (= threads of piv_sel_kernel)
+constexpr int SEL = 1024;         // candidates
+constexpr int SEL_LDS_N = 8192;  // n up to which piv_sel_kernel stages diagonals in LDS
 
 #ifdef TG_SEL_PHASES
 __device__ unsigned long long g_selph[8];
@@ -681,9 +682,35 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
 #endif
   SELT(0)
   for (int x = tid; x < n; x += STH) permL[x] = w.perm[x];
+  // Schur diagonals and positions: staged in LDS once for n <= SEL_LDS_N (the
+  // selection passes below read them five times), else read from HBM/L2
+  const bool staged = n <= SEL_LDS_N;
+  double *dsh = reinterpret_cast<double *>(permL + ((n + 1) & ~1));
+  int *posh = reinterpret_cast<int *>(dsh + n);
+  if (staged) {
+    for (int r0 = tid; r0 < n; r0 += 8 * STH) {
+      double dv[8];
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // one batch of loads in flight
+        const int r = min(r0 + u * STH, n - 1);
+        dv[u] = w.dsc[r];
+        pv[u] = w.pos[r];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + u * STH < n) {
+          dsh[r0 + u * STH] = dv[u];
+          posh[r0 + u * STH] = pv[u];
+        }
+    }
+    __syncthreads();
+  }
+  const double *dS = staged ? dsh : w.dsc;
+  const int32_t *pS = staged ? posh : w.pos;
   // --- candidate set ---------------------------------------------------------
   int valid = 0;
-  for (int r = tid; r < n; r += STH) valid += (w.pos[r] >= ps && dkey(w.dsc[r]) != 0ull);
+  for (int r = tid; r < n; r += STH) valid += (pS[r] >= ps && dkey(dS[r]) != 0ull);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) valid += __shfl_xor(valid, off);
   if (lane == 0) scnt[wid] = valid;
@@ -696,8 +723,8 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) valid += scnt[q];
   if (valid > SEL) {
-    radix_pass(w.dsc, w.pos, n, ps, 1, 0, SEL, hist, sel);  // sel[0] = b1, sel[1] = above
-    radix_pass(w.dsc, w.pos, n, ps, 2, sel[0], SEL - sel[1], hist, sel + 2);
+    radix_pass(dS, pS, n, ps, 1, 0, SEL, hist, sel);  // sel[0] = b1, sel[1] = above
+    radix_pass(dS, pS, n, ps, 2, sel[0], SEL - sel[1], hist, sel + 2);
   }
   const int b1 = sel[0], b2 = sel[2];
   auto inset = [&](unsigned long long key) {
@@ -711,9 +738,9 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   double tau = -INFINITY, bv = -INFINITY;
   int bp = n, brow = 0;
   for (int r = tid; r < n; r += STH) {
-    const int pr = w.pos[r];
+    const int pr = pS[r];
     if (pr < ps) continue;
-    const double d = w.dsc[r];
+    const double d = dS[r];
     if (inset(dkey(d))) ++mine;
     else tau = fmax(tau, d);
     if (d > bv || (d == bv && pr < bp)) {
@@ -745,8 +772,8 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
     }
     int slot = base + pre - mine;
     for (int r = tid; r < n; r += STH) {
-      if (w.pos[r] < ps) continue;
-      if (inset(dkey(w.dsc[r]))) cand[slot++] = r;
+      if (pS[r] < ps) continue;
+      if (inset(dkey(dS[r]))) cand[slot++] = r;
     }
   }
   __syncthreads();
@@ -762,8 +789,8 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   for (int u = 0; u < CPT; ++u) {
     const int c = tid + u * STH;
     rc[u] = c < nset ? cand[c] : -1;
-    posc[u] = rc[u] >= 0 ? w.pos[rc[u]] : n;
-    dc[u] = rc[u] >= 0 ? w.dsc[rc[u]] : -INFINITY;
+    posc[u] = rc[u] >= 0 ? pS[rc[u]] : n;
+    dc[u] = rc[u] >= 0 ? dS[rc[u]] : -INFINITY;
     done[u] = rc[u] < 0;
 #pragma unroll
     for (int l = 0; l < PB; ++l) lr[u][l] = 0.0;
@@ -1425,7 +1452,8 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
 #endif
   hipLaunchKernelGGL(piv_init2_kernel, dim3(std::min(64, tg::cdiv(n, 256))), dim3(256), 0, st, n, w);
   TG_LAUNCHED();
-  const size_t lds = sizeof(int) * size_t(n);
+  const size_t lds = sizeof(int) * size_t((n + 1) & ~1) +
+                     (n <= SEL_LDS_N ? (sizeof(double) + sizeof(int)) * size_t(n) : 0);
   if (lds > 48 * 1024)
     TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
