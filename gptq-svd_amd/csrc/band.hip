@@ -224,6 +224,9 @@ __device__ inline void usets(double (&a)[32], double (&b)[32], int j, double x, 
 // w = v^T P (trailing columns) and Y^T v (the new T column), and thread a of
 // wave 0 extends row a of T in registers: T[a][j] = -tau_j sum_c T[a][c] q_c.
 constexpr int QT = 256;
+// STATS: per-phase s_memrealtime stamps (TG_QR_STATS); off in production, the
+// stamps wait on lgkmcnt and lengthen the serial column chain.
+template <bool STATS>
 __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ src, int64_t ld,
                                                      int c, int nc, int m,
                                                      double *__restrict__ Yo,
@@ -260,17 +263,17 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
   // P[j][l] + scal d_l (l > j: the update, l < j: the T recurrence input).
   auto step = [&](auto jc) {
     constexpr int j = decltype(jc)::value;
-    const uint64_t p0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t p0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     const double x0 = r0[j], x1 = r1[j];
     if (tid == j) {
 #pragma unroll
       for (int l = 0; l < SB_B; ++l) prow[l] = r0[l];
     }
     const double d = reduce_scatter32(r0, r1, (tid > j) ? x0 : 0.0, x1, lane);
-    const uint64_t p1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t p1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if ((lane & 1) == 0) red[wid][mycol] = d;
     __syncthreads();
-    const uint64_t p2 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t p2 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     const double s = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
     const double alpha = prow[j];
     double tau = 0.0, scal = 0.0, beta = alpha;
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
       tau = (beta - alpha) / beta;
       scal = 1.0 / (alpha - beta);
     }
-    const uint64_t p3 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t p3 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (tid < SB_B) {
       const double dl = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
       const double a = prow[tid] + scal * dl;
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     }
     if (tid == 0) taus[j] = tau;
     __syncthreads();
-    const uint64_t p4 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t p4 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     const double v0 = (tid > j) ? x0 * scal : (tid == j ? 1.0 : 0.0);
     const double v1 = x1 * scal;
     const double tv0 = tau * v0, tv1 = tau * v1;
@@ -300,13 +303,15 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     }
     r0[j] = (tid > j) ? v0 : (tid == j ? beta : x0);
     r1[j] = v1;
-    const uint64_t p5 = __builtin_amdgcn_s_memrealtime();
-    ph[0] += p1 - p0; ph[1] += p2 - p1; ph[2] += p3 - p2; ph[3] += p4 - p3; ph[4] += p5 - p4;
+    const uint64_t p5 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+    if constexpr (STATS) {
+      ph[0] += p1 - p0; ph[1] += p2 - p1; ph[2] += p3 - p2; ph[3] += p4 - p3; ph[4] += p5 - p4;
+    }
   };
   [&]<int... J>(std::integer_sequence<int, J...>) {
     (step(std::integral_constant<int, J>{}), ...);
   }(std::make_integer_sequence<int, SB_B>{});
-  if (qst && tid == 0) {
+  if (STATS && qst && tid == 0) {
     for (int k = 0; k < 5; ++k) atomicAdd(qst + k, (unsigned long long)ph[k]);
     atomicAdd(qst + 5, 1ull);
   }
@@ -380,8 +385,12 @@ hipError_t launch_qr(hipStream_t st, const double *src, int64_t ld, int nc, int 
               h[3] / 100.0 / h[5] / 32, h[4] / 100.0 / h[5] / 32, h[5]);
     });
   }
-  hipLaunchKernelGGL(tsqr_qr_kernel, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T, R,
-                     YT, qst);
+  if (qst)
+    hipLaunchKernelGGL(tsqr_qr_kernel<true>, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T,
+                       R, YT, qst);
+  else
+    hipLaunchKernelGGL(tsqr_qr_kernel<false>, dim3(nc), dim3(QT), 0, st, src, ld, SB_C, nc, m, Y, T,
+                       R, YT, nullptr);
   tg::prof_end(st, tok);
   return hipGetLastError();
 }
