@@ -545,9 +545,14 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
                                                        int64_t ldx,
                                                        const double *__restrict__ M,
                                                        int64_t ldm) {
-  __shared__ double As[S2K][S2T + S2P];
-  __shared__ double Bs[S2K][S2T + S2P];
-  __shared__ double YS[SB_B][S2T + S2P];   // -(Y_rows S_IJ)^T, k-major
+  // one LDS block: As, Bs, YS during the K loop, then the 64 x 65 tile for the
+  // coalesced mirror stores
+  constexpr int SMN = (2 * S2K + SB_B) * (S2T + S2P);
+  static_assert(SMN >= S2T * (S2T + 1), "mirror tile must fit");
+  __shared__ double sm[SMN];
+  double(*As)[S2T + S2P] = reinterpret_cast<double(*)[S2T + S2P]>(sm);
+  double(*Bs)[S2T + S2P] = reinterpret_cast<double(*)[S2T + S2P]>(sm + S2K * (S2T + S2P));
+  double(*YS)[S2T + S2P] = reinterpret_cast<double(*)[S2T + S2P]>(sm + 2 * S2K * (S2T + S2P));  // -(Y_rows S_IJ)^T, k-major
   __shared__ double Ss[SB_B][SB_B + 1];
   const int b = blockIdx.x;
   int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
@@ -624,21 +629,42 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
     }
     __syncthreads();
   }
+  // old values loaded together (clamped), then the lower tile written and,
+  // for an off-diagonal tile, its transpose written row-contiguous from LDS
+  double old[2][2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int gi = tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
-        const int gj = tn + wn * 32 + j * 16 + (lane & 15);
+        const int gi = min(tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r, m - 1);
+        const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
+        old[i][j][r] = A[int64_t(gi) * lda + gj];
+      }
+  double(*Tt)[S2T + 1] = reinterpret_cast<double(*)[S2T + 1]>(sm);  // K loop done (barrier)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm * 32 + i * 16 + (lane >> 4) + 4 * r, lj = wn * 32 + j * 16 + (lane & 15);
+        const int gi = tm + li, gj = tn + lj;
         if (gi < m && gj < m && gi >= gj) {
-          double *p = A + int64_t(gi) * lda + gj;
-          const double v = *p - acc[i][j][r];
-          *p = v;
-          if (gi != gj) A[int64_t(gj) * lda + gi] = v;
+          const double v = old[i][j][r] - acc[i][j][r];
+          A[int64_t(gi) * lda + gj] = v;
+          if (tm != tn) Tt[li][lj] = v;
+          else if (gi != gj) A[int64_t(gj) * lda + gi] = v;
         }
       }
+  if (tm != tn) {
+    __syncthreads();
+    for (int idx = tid; idx < S2T * S2T; idx += 256) {
+      const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
+      if (tn + lc < m && tm + lr < m) A[int64_t(tn + lc) * lda + tm + lr] = Tt[lr][lc];
+    }
+  }
 }
 
 // dst[s][:] = src[map(s)][:]
