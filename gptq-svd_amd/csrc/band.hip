@@ -668,6 +668,44 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
 }
 
 // dst[s][:] = src[map(s)][:]
+// Both passes of sym_scatter_kernel in one launch: blockIdx.z = pass, each
+// with its own (x, y) extent; the passes write disjoint entries.
+__global__ void sym_scatter2_kernel(double *__restrict__ A, int64_t lda, int m, int nS, RowMap mp,
+                                    const double *__restrict__ U, int gx0, int gx1, int gy1) {
+  if (blockIdx.z == 0) {
+    const int s = blockIdx.y;
+    if (s >= nS || int(blockIdx.x) >= gx0) return;
+    const int r = mp.fwd(s);
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < m; c += gx0 * blockDim.x) {
+      const int t = mp.inv(c);
+      double v = U[int64_t(s) * m + c];
+      if (t >= 0) v = v + U[int64_t(t) * m + r];
+      A[int64_t(r) * lda + c] -= v;
+    }
+  } else {
+    if (int(blockIdx.x) >= gx1 || int(blockIdx.y) >= gy1) return;
+    const int r = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (r >= m || mp.inv(r) >= 0) return;
+    for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < nS; t += gy1 * 4)
+      A[int64_t(r) * lda + mp.fwd(t)] -= U[int64_t(t) * m + r];
+  }
+}
+
+// X[S_s, :] -= 1/2 sum_a Y[s][a] M[z(s) * 32 + a][:]  (z(s) = chunk of level
+// row s), in place through the row map: the level >= 1 W = X - Yd M / 2.
+__global__ void xs_update_kernel(double *__restrict__ X, int w, int rows, int nc, RowMap mp,
+                                 const double *__restrict__ Y, const double *__restrict__ M) {
+  const int s = blockIdx.y, col = blockIdx.x * 64 + threadIdx.x;
+  if (col >= w) return;
+  const int z = min(s / SB_C, nc - 1);
+  const double *yr = Y + int64_t(s) * SB_B;
+  const double *mc = M + int64_t(z) * SB_B * w + col;
+  double acc = 0.0;
+#pragma unroll
+  for (int a = 0; a < SB_B; ++a) acc += yr[a] * mc[int64_t(a) * w];
+  X[int64_t(mp.fwd(s)) * w + col] += -0.5 * acc;
+}
+
 __global__ void gather_rows_kernel(const double *__restrict__ src, int64_t lds, int ncols, int nrows,
                                    RowMap mp, double *__restrict__ dst) {
   const int s = blockIdx.y;
@@ -807,27 +845,24 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
         // X = Gr^T blockdiag(YT)   (m x w)
         ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
         TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w));
-        // Xs = X[S, :]  (rows x w)
-        hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(w, 256), rows), dim3(256), 0, st, b.X,
-                           int64_t(w), w, rows, mp, b.Xs);
-        TG_CHK(hipGetLastError());
-        hipLaunchKernelGGL((ytz_kernel<0, false>), dim3(nc, nc), dim3(512), 0, st, Yl, Tl, b.Xs,
+        // M = T^T Y^T X[S, :]  (the rows S of X read through the row map)
+        hipLaunchKernelGGL((ytz_kernel<0, true>), dim3(nc, nc), dim3(512), 0, st, Yl, Tl, b.X,
                            int64_t(w), w, SB_C, nc, rows, mp, b.M, int64_t(w));
         TG_CHK(hipGetLastError());
-        ChunkSpec cw{SB_C, nc, rows, SB_B, 0, 0, int64_t(SB_B) * w, w, 0, -1, w, SB_B};
-        TG_CHK(dgemm_chunked(st, false, false, cw, -0.5, Yl, SB_B, b.M, w, 1.0, b.Xs, w));
-        hipLaunchKernelGGL(scatter_rows_kernel, dim3(cdiv(w, 256), rows), dim3(256), 0, st, b.Xs,
-                           w, rows, mp, b.X, int64_t(w));
+        // W = X - 1/2 Yd M on the rows S, in place
+        hipLaunchKernelGGL(xs_update_kernel, dim3(cdiv(w, 64), rows), dim3(64), 0, st, b.X, w,
+                           rows, nc, mp, Yl, b.M);
         TG_CHK(hipGetLastError());
         // U = Y_l W^T  (rows x m)
         ChunkSpec cu{SB_C, nc, rows, SB_B, 0, 0, SB_B, m, 0, -1, m, SB_B};
         TG_CHK(dgemm_chunked(st, false, true, cu, 1.0, Yl, SB_B, b.X, w, 0.0, b.U, m));
-        hipLaunchKernelGGL(sym_scatter_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
-                           int64_t(lda), m, rows, mp, b.U, 0);
-        TG_CHK(hipGetLastError());
-        hipLaunchKernelGGL(sym_scatter_kernel, dim3(cdiv(m, 64), std::min(64, cdiv(rows, 4))),
-                           dim3(256), 0, st, A22, int64_t(lda), m, rows, mp, b.U, 1);
-        TG_CHK(hipGetLastError());
+        // A22[S, :] and A22[:, S] -= U, U^T in one launch (disjoint entries)
+        {
+          const int gx0 = cdiv(m, 256), gx1 = cdiv(m, 64), gy1 = std::min(64, cdiv(rows, 4));
+          hipLaunchKernelGGL(sym_scatter2_kernel, dim3(std::max(gx0, gx1), std::max(rows, gy1), 2),
+                             dim3(256), 0, st, A22, int64_t(lda), m, rows, mp, b.U, gx0, gx1, gy1);
+          TG_CHK(hipGetLastError());
+        }
       }
     }
     hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, st, A,
