@@ -772,7 +772,7 @@ namespace tg {
 // Side stream + events for the TSQR levels >= 1 (created once per device).
 struct SideStream {
   hipStream_t s = nullptr;
-  hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
+  hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr}, evj = nullptr;
 };
 static hipError_t side_stream(SideStream *&out) {
   static SideStream ss[64];
@@ -786,6 +786,7 @@ static hipError_t side_stream(SideStream *&out) {
       if ((e = hipEventCreateWithFlags(&x.ev0[i], hipEventDisableTiming)) != hipSuccess) return e;
       if ((e = hipEventCreateWithFlags(&x.ev1[i], hipEventDisableTiming)) != hipSuccess) return e;
     }
+    if ((e = hipEventCreateWithFlags(&x.evj, hipEventDisableTiming)) != hipSuccess) return e;
   }
   out = &x;
   return hipSuccess;
@@ -814,6 +815,14 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
                          b.R[l & 1], b.YTl[l]));
       }
       TG_CHK(hipEventRecord(ss->ev1[ph], ss->s));
+      // R (in R[1] when nl is even) -> the panel's band block, off the main
+      // stream's critical path: it writes A outside every later A22 and
+      // outside the next panels' columns; joined after the last panel
+      if (((P.nl - 1) & 1) == 1) {
+        hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, ss->s, A,
+                           int64_t(lda), P.p, r0, m, b.R[1]);
+        TG_CHK(hipGetLastError());
+      }
     }
     for (int l = 0; l < P.nl; ++l) {
       const SbLevel &L = P.L[l];
@@ -865,11 +874,15 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
         }
       }
     }
-    hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, st, A,
-                       int64_t(lda), P.p, r0, m, b.R[(P.nl - 1) & 1]);
-    TG_CHK(hipGetLastError());
+    if (((P.nl - 1) & 1) == 0) {
+      hipLaunchKernelGGL(write_panel_kernel, dim3(cdiv(m * SB_B, 256)), dim3(256), 0, st, A,
+                         int64_t(lda), P.p, r0, m, b.R[(P.nl - 1) & 1]);
+      TG_CHK(hipGetLastError());
+    }
     ++pi;
   }
+  TG_CHK(hipEventRecord(ss->evj, ss->s));  // side-stream panel writes done
+  TG_CHK(hipStreamWaitEvent(st, ss->evj, 0));
   return hipSuccess;
 }
 
