@@ -128,7 +128,10 @@ __global__ void prep_block_kernel(const float *__restrict__ Ublk, int ldu, int b
 // w_j <- w_j - e_c * corr[c][j] for c = 0, 1, ... (separately rounded mul
 // and sub), so the result is bit-identical to the Triton kernel.
 // ---------------------------------------------------------------------------
-constexpr int RW = 16;  // rows per workgroup
+#ifndef TG_QUANT_RW
+#define TG_QUANT_RW 16
+#endif
+constexpr int RW = TG_QUANT_RW;  // rows per workgroup
 constexpr int P = 32;   // panel width
 
 struct BlockArgs {
