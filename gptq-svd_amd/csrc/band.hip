@@ -852,8 +852,16 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
                            int64_t(lda), m, rows, mp, b.Gr);
         TG_CHK(hipGetLastError());
         // X = Gr^T blockdiag(YT)   (m x w)
-        ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
-        TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w));
+        if (nc == 1) {
+          // one chunk: a tall-skinny Gr^T YT (m x 32, K = rows) has only m/64
+          // output tiles; split K over up to 8 workgroups per tile (scratch:
+          // U, which this level fills only later; ncmax * 32 * n >= 32 m * splits)
+          TG_CHK(dgemm_splitk(st, true, false, m, w, rows, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w,
+                              std::min(8, pl.ncmax), b.U));
+        } else {
+          ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
+          TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w));
+        }
         // M = T^T Y^T X[S, :]  (the rows S of X read through the row map)
         hipLaunchKernelGGL((ytz_kernel<0, true>), dim3(nc, nc), dim3(512), 0, st, Yl, Tl, b.X,
                            int64_t(w), w, SB_C, nc, rows, mp, b.M, int64_t(w));
