@@ -847,18 +847,25 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
         if (P.nl > 1) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));
       } else {
         double *YTl = b.YTl[l];
-        // Gr = A22[S, :]  (rows x m)
-        hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
-                           int64_t(lda), m, rows, mp, b.Gr);
-        TG_CHK(hipGetLastError());
-        // X = Gr^T blockdiag(YT)   (m x w)
+        // X = A22[S, :]^T blockdiag(YT)   (m x w)
         if (nc == 1) {
-          // one chunk: a tall-skinny Gr^T YT (m x 32, K = rows) has only m/64
-          // output tiles; split K over up to 8 workgroups per tile (scratch:
-          // U, which this level fills only later; ncmax * 32 * n >= 32 m * splits)
-          TG_CHK(dgemm_splitk(st, true, false, m, w, rows, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w,
-                              std::min(8, pl.ncmax), b.U));
+          // one chunk (w = 32): the rows S are 32-row blocks of A22 at a
+          // fixed stride, so X = sum_z A22[block z, :]^T YT[32z : 32z + 32, :]
+          // is one chunked GEMM straight from A22 (no gather; nz x 64 output
+          // tiles instead of m/64) and a sum of the nz partials (scratch: U,
+          // which this level fills only later; nz * 32 * m <= ncmax * 32 * n)
+          int stride = SB_C;
+          for (int q = 1; q < l; ++q) stride *= SB_C / SB_B;
+          const int nz = rows / SB_B;
+          ChunkSpec cz{SB_B, nz, rows, int64_t(stride / SB_B) * lda, 0, SB_B, 0, 0,
+                       int64_t(m) * SB_B, m, SB_B, SB_B};
+          TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, YTl, SB_B, 0.0, b.U, SB_B));
+          TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, w));
         } else {
+          // Gr = A22[S, :]  (rows x m)
+          hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(m, 256), rows), dim3(256), 0, st, A22,
+                             int64_t(lda), m, rows, mp, b.Gr);
+          TG_CHK(hipGetLastError());
           ChunkSpec cx{SB_C, nc, rows, m, 0, SB_B, 0, 0, SB_B, m, SB_B, -1};
           TG_CHK(dgemm_chunked(st, true, false, cx, 1.0, b.Gr, m, YTl, SB_B, 0.0, b.X, w));
         }

@@ -16,6 +16,9 @@ size_t dgemm_splitk_scratch(int M, int N, int splits);
 hipError_t dgemm_splitk(hipStream_t st, bool transA, bool transB, int M, int N, int K,
                         double alpha, const double *A, int64_t lda, const double *B, int64_t ldb,
                         double beta, double *C, int64_t ldc, int splits, double *scratch);
+// C = alpha * sum_z P_z + beta * C, P_z = P + z * M * N (M x N, ld N).
+hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, double alpha,
+                        double beta, double *C, int64_t ldc);
 // Symmetric rank-K updates (lower tiles computed, mirrored to the upper triangle).
 hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc);  // C = a X^T X + b C, X: K x n

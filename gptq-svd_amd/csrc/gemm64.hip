@@ -414,6 +414,16 @@ hipError_t dgemm_splitk(hipStream_t st, bool ta, bool tb, int M, int N, int K, d
   return hipGetLastError();
 }
 
+hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, double alpha,
+                        double beta, double *C, int64_t ldc) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int64_t zs = int64_t(M) * N;
+  const int blocks = int(std::min<int64_t>(4096, (zs + 255) / 256));
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, P, nz, zs, M, N, alpha,
+                     beta, C, ldc);
+  return hipGetLastError();
+}
+
 // C = alpha * X^T X + beta * C on lower tiles, mirrored (X is K x n, ld ldx).
 hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc) {
