@@ -181,10 +181,10 @@ __device__ inline void load_sz(const BlockArgs &a, int row, int c, float &s, flo
 template <bool GATHER, bool LOOP>
 __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
   extern __shared__ float smem[];
-  const int bwp = a.bw + 1;           // odd row stride: lane-per-row access is conflict-free
-  float *Wb = smem;                    // [RW][bwp]
-  float *el = Wb + RW * bwp;           // [RW][P+1] panel errors
-  float *cp = el + RW * (P + 1);       // [P][P]   corr panel
+  const int bwp = a.bw + 1;             // odd row stride: lane-per-row access is conflict-free
+  float *Wb = smem;                      // [RW][bwp]
+  float *el = Wb + RW * bwp;             // [2][RW][P+1] panel errors, parity by panel
+  float *cp = el + 2 * RW * (P + 1);     // [P][P]   corr panel
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * RW;
 
@@ -193,15 +193,41 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
     const int row = r0 + rr;
     Wb[rr * bwp + c] = row < a.m ? a.W[size_t(row) * a.ldw + c] : 0.0f;
   }
-
-  for (int p0 = 0; p0 < a.bw; p0 += P) {
-    const int pw = min(P, a.bw - p0);
+  auto load_cp = [&](int q0) {
+    const int qw = min(P, a.bw - q0);
     for (int idx = tid; idx < P * P; idx += blockDim.x) {
       const int cc = idx / P, j = idx % P;
-      cp[idx] = (cc < pw && j < pw) ? a.corr[size_t(p0 + cc) * a.ldcorr + p0 + j] : 0.0f;
+      cp[idx] = (cc < qw && j < qw) ? a.corr[size_t(q0 + cc) * a.ldcorr + q0 + j] : 0.0f;
     }
-    __syncthreads();
+  };
+  // rows rr0, rr0 + rstep, ... of column j get panel q0's errors e, in order
+  auto apply_col = [&](const float *e, int q0, int j, int rr0, int rstep) {
+    float cv[P];
+#pragma unroll
+    for (int cc = 0; cc < P; ++cc) cv[cc] = a.corr[size_t(q0 + cc) * a.ldcorr + j];
+#pragma unroll 2
+    for (int rr = rr0; rr < RW; rr += rstep) {
+      float w = Wb[rr * bwp + j];
+#pragma unroll
+      for (int cc = 0; cc < P; ++cc) {
+        const float d = e[rr * (P + 1) + cc] * cv[cc];
+        w = w - d;
+      }
+      Wb[rr * bwp + j] = w;
+    }
+  };
+  load_cp(0);
+  __syncthreads();
 
+  // Look-ahead: while wave 0 runs panel p's column chain, waves 1-3 apply
+  // panel p-1's errors to the columns after panel p; then all threads apply
+  // panel p's errors to panel p+1's columns.  Every element still receives
+  // the panels' updates in panel order, cc ascending within a panel, so the
+  // result is the same bit for bit.
+  for (int p0 = 0, it = 0; p0 < a.bw; p0 += P, ++it) {
+    const int pw = min(P, a.bw - p0);
+    float *elc = el + (it & 1) * RW * (P + 1);
+    const float *elp = el + ((it + 1) & 1) * RW * (P + 1);
     if (tid < RW) {  // sequential column chain: one lane per row
       const int rr = tid, row = r0 + rr;
       float wv[P], sv[P], zv[P];
@@ -234,7 +260,7 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
             a.E[size_t(row) * a.lde + c] = err;
             if (a.codes) a.codes[size_t(row) * a.ldc + c] = uint8_t(int(qi) + a.code_off);
           }
-          el[rr * (P + 1) + cc] = err;
+          elc[rr * (P + 1) + cc] = err;
 #pragma unroll
           for (int j = cc + 1; j < P; ++j) {  // :377-386 inside the panel
             const float d = err * cp[cc * P + j];
@@ -242,29 +268,19 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
           }
         }
       }
+    } else if (tid >= 64 && p0 > 0) {
+      // deferred trailing update of panel p-1: the columns after panel p
+      for (int j = p0 + P + (tid - 64); j < a.bw; j += blockDim.x - 64)
+        apply_col(elp, p0 - P, j, 0, 1);
     }
     __syncthreads();
-
-    // trailing update: columns after the panel, panel errors applied in order
-    const int jbeg = p0 + pw;
-    if (jbeg < a.bw) {
-      for (int j = jbeg + tid; j < a.bw; j += blockDim.x) {
-        float cv[P];
-#pragma unroll
-        for (int cc = 0; cc < P; ++cc) cv[cc] = a.corr[size_t(p0 + cc) * a.ldcorr + j];
-#pragma unroll 2
-        for (int rr = 0; rr < RW; ++rr) {
-          float w = Wb[rr * bwp + j];
-#pragma unroll
-          for (int cc = 0; cc < P; ++cc) {
-            const float d = el[rr * (P + 1) + cc] * cv[cc];
-            w = w - d;
-          }
-          Wb[rr * bwp + j] = w;
-        }
-      }
+    if (p0 + pw < a.bw) {  // panel p+1's columns get panel p's errors, then its corr block
+      const int q0 = p0 + P, qw = min(P, a.bw - q0);
+      const int jj = tid & 31;
+      if (jj < qw) apply_col(elc, p0, q0 + jj, tid >> 5, blockDim.x / 32);
+      load_cp(q0);
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -527,7 +543,7 @@ __global__ void pack_zeros_kernel(const float *__restrict__ zero, int m, int G, 
   qz[size_t(gi) * nw + wi] = int32_t(uint32_t(acc & 0xffffffffu));
 }
 
-size_t block_smem(int bw) { return sizeof(float) * (size_t(RW) * (bw + 1) + RW * (P + 1) + P * P); }
+size_t block_smem(int bw) { return sizeof(float) * (size_t(RW) * (bw + 1) + 2 * RW * (P + 1) + P * P); }
 
 constexpr int MAX_BLOCK = 2048;
 
