@@ -115,6 +115,12 @@ __device__ inline double xdpp(double x) {
 }
 constexpr int DPP_MIRROR = 0x140, DPP_HALF_MIRROR = 0x141, DPP_XOR3 = 0x1B, DPP_XOR1 = 0xB1;
 
+__device__ inline double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+
 __device__ inline double wave_allsum(double s) {
   s = hsum32(s);
   s = hsum16(s);
@@ -279,8 +285,10 @@ __global__ __launch_bounds__(QT) void tsqr_qr_kernel(const double *__restrict__ 
     double tau = 0.0, scal = 0.0, beta = alpha;
     if (s != 0.0) {
       beta = -copysign(sqrt(alpha * alpha + s), alpha);
-      tau = (beta - alpha) / beta;
-      scal = 1.0 / (alpha - beta);
+      // reciprocals by v_rcp_f64 + two Newton steps (~1 ulp): the two IEEE
+      // division sequences sit on the serial column chain
+      tau = (beta - alpha) * rcp_nr(beta);
+      scal = rcp_nr(alpha - beta);
     }
     const uint64_t p3 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (tid < SB_B) {
