@@ -743,6 +743,157 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
   }
 }
 
+// Few-vector form of invit_kernel: one wave per vector, its lane 0 runs the
+// serial sweeps with x and the LU factors (pivot reciprocals, du, du2) held in
+// LDS, and d, e streamed from global one chunk ahead of the chain, so the
+// sweeps wait on neither global loads nor stores.  The whole wave rescales.
+// Same dgttrf pivoting and substitution order as invit_kernel.
+constexpr int IFCH = 16;
+__global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict__ d,
+                                                       const double *__restrict__ e, int n, int k,
+                                                       int first,
+                                                       const double *__restrict__ w_asc,
+                                                       const double *__restrict__ bnd, int iters,
+                                                       Tri w) {
+  extern __shared__ double sm[];
+  const int jj = blockIdx.x, lane = threadIdx.x;
+  const int gi = n - 1 - (first + jj);
+  const double lam = w_asc[gi];
+  const int sl = w.slot[gi];
+  const int b0 = w.bs[sl], b1 = w.be[sl], m = b1 - b0;
+  const double tol = fmax(DBL_EPSILON * bnd[2], 1e-300);
+  const size_t K = size_t(k);
+  double *xs = sm, *rd = sm + m, *du = sm + 2 * m, *du2 = sm + 3 * m;
+  for (int i = lane; i < n; i += 64)
+    if (i < b0 || i >= b1) w.Z[size_t(i) * K + jj] = 0.0;
+  d += b0;
+  e += b0;
+  for (int i = lane; i < m; i += 64)
+    xs[i] = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
+  auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
+  auto rcp2 = [](double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return fma(fma(-b, r, 1.0), r, r);
+  };
+  auto qdiv = [](double a, double b, double r) {  // a / b given r ~ 1/b (fdiv's last step)
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+  };
+  // e[i] for i in [0, m-1), zero past the block
+  auto eat = [&](int i) { return i < m - 1 ? e[i] : 0.0; };
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    double amax = 0.0;
+    if (lane == 0) {
+      double cur_d = d[0] - lam, cur_u = eat(0), xi = xs[0];
+      double dn[IFCH], en[IFCH], enn[IFCH], pd[IFCH], pe[IFCH], pee[IFCH];
+      // a zero the compiler cannot prove uniform: d and e then arrive by vector
+      // loads (vmcnt), not scalar ones, so waiting on the chain's LDS traffic
+      // (lgkmcnt) does not also wait on the prefetch
+      int vz;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+      auto fetch = [&](int i0, double *a, double *b, double *c) {
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) {
+          const int i = min(i0 + u, max(m - 2, 0)) + vz;
+          a[u] = d[min(i + 1, m - 1)];
+          b[u] = eat(i);
+          c[u] = eat(i + 1);
+        }
+      };
+      // one dgttrf step + forward substitution, branch-free (selects only)
+      auto step = [&](int i, double sub, double nd, double nu, double xnext) {
+        const bool sw = !(fabs(cur_d) >= fabs(sub));  // row interchange
+        const double den = sw ? sub : clampp(cur_d), num = sw ? cur_d : sub;
+        const double r = rcp2(den);
+        const double f = qdiv(num, den, r);
+        const double A = sw ? xi : xnext, B = sw ? xnext : xi;
+        const double C = sw ? cur_u : nd, D = sw ? nd : cur_u;
+        rd[i] = r;
+        du[i] = D;
+        du2[i] = sw ? nu : 0.0;
+        xs[i] = B;
+        xi = A - f * B;
+        cur_d = C - f * D;
+        cur_u = sw ? -f * nu : nu;
+      };
+      fetch(0, dn, en, enn);
+      for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
+        const int cnt = min(IFCH, m - 1 - i0);
+        fetch(i0 + IFCH, pd, pe, pee);  // next chunk in flight while this one runs
+        double xn[IFCH];
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) xn[u] = xs[min(i0 + u + 1, m - 1)];
+        if (cnt == IFCH) {
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) step(i0 + u, en[u], dn[u] - lam, enn[u], xn[u]);
+        } else {
+          for (int u = 0; u < cnt; ++u) step(i0 + u, en[u], dn[u] - lam, enn[u], xn[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) {
+          dn[u] = pd[u];
+          en[u] = pe[u];
+          enn[u] = pee[u];
+        }
+      }
+      rd[m - 1] = rcp2(clampp(cur_d));
+      xs[m - 1] = xi;
+      // backward substitution with U
+      double xn1 = 0.0, xn2 = 0.0;
+      auto bstep = [&](double &xv, double rv, double uv, double u2v) {
+        const double v = (xv - u2v * xn2 - uv * xn1) * rv;
+        xv = v;
+        xn2 = xn1;
+        xn1 = v;
+        amax = fmax(amax, fabs(v));
+      };
+      for (int i1 = m; i1 > 0; i1 -= IFCH) {
+        const int i0 = max(0, i1 - IFCH), cnt = i1 - i0;
+        double xv[IFCH], rv[IFCH], uv[IFCH], u2v[IFCH];
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) {
+          const int i = min(i0 + u, m - 1);
+          xv[u] = xs[i];
+          rv[u] = rd[i];
+          uv[u] = i >= m - 1 ? 0.0 : du[i];
+          u2v[u] = i >= m - 2 ? 0.0 : du2[i];
+        }
+        if (cnt == IFCH) {
+#pragma unroll
+          for (int u = IFCH - 1; u >= 0; --u) bstep(xv[u], rv[u], uv[u], u2v[u]);
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) xs[i0 + u] = xv[u];
+        } else {
+          for (int u = cnt - 1; u >= 0; --u) {
+            double x1 = xs[i0 + u];
+            bstep(x1, rd[i0 + u], i0 + u >= m - 1 ? 0.0 : du[i0 + u],
+                  i0 + u >= m - 2 ? 0.0 : du2[i0 + u]);
+            xs[i0 + u] = x1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    amax = __shfl(amax, 0);
+    const double sc = amax > 0.0 ? 1.0 / amax : 1.0;
+    double nrm = 0.0;
+    for (int i = lane; i < m; i += 64) {
+      const double v = xs[i] * sc;
+      nrm += v * v;
+      xs[i] = v;
+    }
+    if (it == iters - 1) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o);
+      const double inv = 1.0 / sqrt(nrm);
+      for (int i = lane; i < m; i += 64) w.Z[size_t(b0 + i) * K + jj] = xs[i] * inv;
+    }
+    __syncthreads();
+  }
+}
+
 // Re-orthogonalise clusters of (near-)equal eigenvalues (gap <= reltol*||T||)
 // by modified Gram-Schmidt, one workgroup walking the k columns (column jj =
 // eigenvalue first + jj in descending order).
@@ -998,8 +1149,17 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
   const char *ie = getenv("TG_INVIT_ITERS");
   const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
-  hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k, first,
-                     w_asc, bnd, iters, w);
+  // few vectors: one LDS-resident wave per vector (4 doubles per row of T)
+  const size_t ilds = 4 * sizeof(double) * size_t(n);
+  if (k <= 256 && ilds <= 160 * 1024 && !getenv("TG_INVIT_REG")) {
+    TG_HIP(hipFuncSetAttribute((const void *)invit_lds_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(ilds)));
+    hipLaunchKernelGGL(invit_lds_kernel, dim3(k), dim3(64), ilds, st, w.d, w.es, n, k, first,
+                       w_asc, bnd, iters, w);
+  } else {
+    hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k,
+                       first, w_asc, bnd, iters, w);
+  }
   tg::prof_end(st, itok);
   TG_LAUNCHED();
   hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, first, bnd, 1e-9,
