@@ -744,18 +744,27 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 }
 
 // Few-vector form of invit_kernel: one wave per vector, its lane 0 runs the
-// serial sweeps with x and the LU factors (pivot reciprocals, du, du2) held in
-// LDS, and d, e streamed from global one chunk ahead of the chain, so the
-// sweeps wait on neither global loads nor stores.  The whole wave rescales.
-// Same dgttrf pivoting and substitution order as invit_kernel.
+// serial sweeps with x and the LU factors held in LDS, and d, e streamed from
+// global one chunk ahead of the chain, so the sweeps wait on neither global
+// loads nor stores.  A single lane's LDS instructions cost tens of cycles of
+// issue each, so row i keeps {1/pivot, du, du2, x} together (32 bytes) and
+// moves as two 16-byte accesses.  The whole wave rescales.  Same dgttrf
+// pivoting and substitution order as invit_kernel.
 constexpr int IFCH = 16;
+// msk[lane] ? t : f as two v_cndmask_b32 (no control flow)
+__device__ inline double vsel(uint64_t msk, double t, double f) {
+  int lo, hi;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(__double2loint(f)), "v"(__double2loint(t)), "s"(msk));
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(__double2hiint(f)), "v"(__double2hiint(t)), "s"(msk));
+  return __hiloint2double(hi, lo);
+}
 __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict__ d,
                                                        const double *__restrict__ e, int n, int k,
                                                        int first,
                                                        const double *__restrict__ w_asc,
                                                        const double *__restrict__ bnd, int iters,
                                                        Tri w) {
-  extern __shared__ double sm[];
+  extern __shared__ double2 rows[];  // rows[2i] = {1/pivot, du}, rows[2i+1] = {du2, x}
   const int jj = blockIdx.x, lane = threadIdx.x;
   const int gi = n - 1 - (first + jj);
   const double lam = w_asc[gi];
@@ -763,115 +772,126 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
   const int b0 = w.bs[sl], b1 = w.be[sl], m = b1 - b0;
   const double tol = fmax(DBL_EPSILON * bnd[2], 1e-300);
   const size_t K = size_t(k);
-  double *xs = sm, *rd = sm + m, *du = sm + 2 * m, *du2 = sm + 3 * m;
+  double *rw = reinterpret_cast<double *>(rows);
+  auto X = [&](int i) -> double & { return rw[4 * i + 3]; };
   for (int i = lane; i < n; i += 64)
     if (i < b0 || i >= b1) w.Z[size_t(i) * K + jj] = 0.0;
   d += b0;
   e += b0;
-  for (int i = lane; i < m; i += 64)
-    xs[i] = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
+  for (int i = lane; i < m; i += 64) X(i) = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
   auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
   auto rcp2 = [](double b) {
     double r = __builtin_amdgcn_rcp(b);
     r = fma(fma(-b, r, 1.0), r, r);
     return fma(fma(-b, r, 1.0), r, r);
   };
-  auto qdiv = [](double a, double b, double r) {  // a / b given r ~ 1/b (fdiv's last step)
-    const double q = a * r;
-    return fma(fma(-b, q, a), r, q);
+  // e[i] for i in [0, m-1), zero past the block (unconditional load + select)
+  auto eat = [&](int i) {
+    const double v = e[max(min(i, m - 2), 0)];
+    return i < m - 1 ? v : 0.0;
   };
-  // e[i] for i in [0, m-1), zero past the block
-  auto eat = [&](int i) { return i < m - 1 ? e[i] : 0.0; };
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
     double amax = 0.0;
     if (lane == 0) {
-      double cur_d = d[0] - lam, cur_u = eat(0), xi = xs[0];
-      double dn[IFCH], en[IFCH], enn[IFCH], pd[IFCH], pe[IFCH], pee[IFCH];
+      double cur_d = d[0] - lam, cur_u = eat(0), xi = X(0);
+      // chunk c covers steps i0..i0+IFCH-1: dn[u] = d[i0+u+1], en[u] = e[i0+u]
+      // (e[i0+u+1] is en[u+1], or the next chunk's en[0])
+      double dn[IFCH], en[IFCH], pd[IFCH], pe[IFCH];
       // a zero the compiler cannot prove uniform: d and e then arrive by vector
       // loads (vmcnt), not scalar ones, so waiting on the chain's LDS traffic
       // (lgkmcnt) does not also wait on the prefetch
       int vz;
       asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-      auto fetch = [&](int i0, double *a, double *b, double *c) {
+      auto fetch = [&](int i0, double *a, double *b) {
 #pragma unroll
         for (int u = 0; u < IFCH; ++u) {
-          const int i = min(i0 + u, max(m - 2, 0)) + vz;
+          const int i = i0 + u + vz;
           a[u] = d[min(i + 1, m - 1)];
           b[u] = eat(i);
-          c[u] = eat(i + 1);
         }
       };
-      // one dgttrf step + forward substitution, branch-free (selects only)
-      auto step = [&](int i, double sub, double nd, double nu, double xnext) {
-        const bool sw = !(fabs(cur_d) >= fabs(sub));  // row interchange
-        const double den = sw ? sub : clampp(cur_d), num = sw ? cur_d : sub;
-        const double r = rcp2(den);
-        const double f = qdiv(num, den, r);
-        const double A = sw ? xi : xnext, B = sw ? xnext : xi;
-        const double C = sw ? cur_u : nd, D = sw ? nd : cur_u;
-        rd[i] = r;
-        du[i] = D;
-        du2[i] = sw ? nu : 0.0;
-        xs[i] = B;
+      // one dgttrf step + forward substitution, branch-free.  Row interchange
+      // when !(|cur_d| >= |sub|); lane masks + v_cndmask keep the compiler from
+      // turning the selects into exec-mask branches.  a / b = q0 + r1 (a - b q0)
+      // with r1 one Newton step from v_rcp_f64: the correction runs beside the
+      // refinement, shortening the serial chain.
+      auto step = [&](double sub, double nd, double nu, double xnext, double2 &o0, double2 &o1) {
+        const uint64_t sw = __builtin_amdgcn_fcmp(fabs(cur_d), fabs(sub), 12);  // ULT
+        const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(cur_d), tol, 4);       // OLT
+        const double den = vsel(sw, sub, vsel(tiny, copysign(tol, cur_d), cur_d));
+        const double num = vsel(sw, cur_d, sub);
+        const double r0 = __builtin_amdgcn_rcp(den);
+        const double q0 = num * r0, ee = fma(-den, r0, 1.0);
+        const double res = fma(-den, q0, num), r1 = fma(r0, ee, r0);
+        const double f = fma(r1, res, q0);
+        const double A = vsel(sw, xi, xnext), B = vsel(sw, xnext, xi);
+        const double C = vsel(sw, cur_u, nd), D = vsel(sw, nd, cur_u);
+        o0 = make_double2(fma(fma(-den, r1, 1.0), r1, r1), D);
+        o1 = make_double2(vsel(sw, nu, 0.0), B);
         xi = A - f * B;
         cur_d = C - f * D;
-        cur_u = sw ? -f * nu : nu;
+        cur_u = vsel(sw, -f * nu, nu);
       };
-      fetch(0, dn, en, enn);
+      fetch(0, dn, en);
       for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
         const int cnt = min(IFCH, m - 1 - i0);
-        fetch(i0 + IFCH, pd, pe, pee);  // next chunk in flight while this one runs
+        fetch(i0 + IFCH, pd, pe);  // next chunk in flight while this one runs
         double xn[IFCH];
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) xn[u] = xs[min(i0 + u + 1, m - 1)];
+        for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
         if (cnt == IFCH) {
+          // outputs leave in one batch after the chunk, off the chain
+          double2 o0[IFCH], o1[IFCH];
 #pragma unroll
-          for (int u = 0; u < IFCH; ++u) step(i0 + u, en[u], dn[u] - lam, enn[u], xn[u]);
+          for (int u = 0; u < IFCH; ++u)
+            step(en[u], dn[u] - lam, u + 1 < IFCH ? en[u + 1] : pe[0], xn[u], o0[u], o1[u]);
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) {
+            rows[2 * (i0 + u)] = o0[u];
+            rows[2 * (i0 + u) + 1] = o1[u];
+          }
         } else {
-          for (int u = 0; u < cnt; ++u) step(i0 + u, en[u], dn[u] - lam, enn[u], xn[u]);
+          for (int u = 0; u < cnt; ++u) {
+            double2 o0, o1;
+            step(en[u], dn[u] - lam, eat(i0 + u + 1), xn[u], o0, o1);
+            rows[2 * (i0 + u)] = o0;
+            rows[2 * (i0 + u) + 1] = o1;
+          }
         }
 #pragma unroll
         for (int u = 0; u < IFCH; ++u) {
           dn[u] = pd[u];
           en[u] = pe[u];
-          enn[u] = pee[u];
         }
       }
-      rd[m - 1] = rcp2(clampp(cur_d));
-      xs[m - 1] = xi;
-      // backward substitution with U
+      rows[2 * (m - 1)] = make_double2(rcp2(clampp(cur_d)), 0.0);
+      rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
+      // backward substitution with U (du of row m-1 and du2 of rows m-2, m-1 are 0)
       double xn1 = 0.0, xn2 = 0.0;
-      auto bstep = [&](double &xv, double rv, double uv, double u2v) {
-        const double v = (xv - u2v * xn2 - uv * xn1) * rv;
-        xv = v;
+      auto bstep = [&](double2 r0, double2 r1) {
+        const double v = (r1.y - r1.x * xn2 - r0.y * xn1) * r0.x;
         xn2 = xn1;
         xn1 = v;
         amax = fmax(amax, fabs(v));
+        return v;
       };
       for (int i1 = m; i1 > 0; i1 -= IFCH) {
-        const int i0 = max(0, i1 - IFCH), cnt = i1 - i0;
-        double xv[IFCH], rv[IFCH], uv[IFCH], u2v[IFCH];
+        const int i0 = i1 - IFCH;
+        if (i0 >= 0) {
+          double2 r0[IFCH], r1[IFCH];
+          double xv[IFCH];
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) {
-          const int i = min(i0 + u, m - 1);
-          xv[u] = xs[i];
-          rv[u] = rd[i];
-          uv[u] = i >= m - 1 ? 0.0 : du[i];
-          u2v[u] = i >= m - 2 ? 0.0 : du2[i];
-        }
-        if (cnt == IFCH) {
-#pragma unroll
-          for (int u = IFCH - 1; u >= 0; --u) bstep(xv[u], rv[u], uv[u], u2v[u]);
-#pragma unroll
-          for (int u = 0; u < IFCH; ++u) xs[i0 + u] = xv[u];
-        } else {
-          for (int u = cnt - 1; u >= 0; --u) {
-            double x1 = xs[i0 + u];
-            bstep(x1, rd[i0 + u], i0 + u >= m - 1 ? 0.0 : du[i0 + u],
-                  i0 + u >= m - 2 ? 0.0 : du2[i0 + u]);
-            xs[i0 + u] = x1;
+          for (int u = 0; u < IFCH; ++u) {
+            r0[u] = rows[2 * (i0 + u)];
+            r1[u] = rows[2 * (i0 + u) + 1];
           }
+#pragma unroll
+          for (int u = IFCH - 1; u >= 0; --u) xv[u] = bstep(r0[u], r1[u]);
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) X(i0 + u) = xv[u];
+        } else {
+          for (int i = i1 - 1; i >= 0; --i) X(i) = bstep(rows[2 * i], rows[2 * i + 1]);
         }
       }
     }
@@ -880,15 +900,15 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
     const double sc = amax > 0.0 ? 1.0 / amax : 1.0;
     double nrm = 0.0;
     for (int i = lane; i < m; i += 64) {
-      const double v = xs[i] * sc;
+      const double v = X(i) * sc;
       nrm += v * v;
-      xs[i] = v;
+      X(i) = v;
     }
     if (it == iters - 1) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o);
       const double inv = 1.0 / sqrt(nrm);
-      for (int i = lane; i < m; i += 64) w.Z[size_t(b0 + i) * K + jj] = xs[i] * inv;
+      for (int i = lane; i < m; i += 64) w.Z[size_t(b0 + i) * K + jj] = X(i) * inv;
     }
     __syncthreads();
   }
