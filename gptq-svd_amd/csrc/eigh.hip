@@ -348,6 +348,14 @@ __device__ inline double fdiv(double a, double b) {
   return fma(fma(-b, q, a), r, q);
 }
 
+// msk[lane] ? t : f as two v_cndmask_b32 (no control flow)
+__device__ inline double vsel(uint64_t msk, double t, double f) {
+  int lo, hi;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(__double2loint(f)), "v"(__double2loint(t)), "s"(msk));
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(__double2hiint(f)), "v"(__double2hiint(t)), "s"(msk));
+  return __hiloint2double(hi, lo);
+}
+
 // Negative pivots of the LDL^T of T - x I (dlaebz's q recurrence).  The
 // division e2/q uses the hardware reciprocal plus one Newton step (relative
 // error ~2^-50, the count of a matrix a few ulps away) to keep the serial
@@ -377,6 +385,37 @@ __device__ inline int sturm_count(const double *__restrict__ d, const double *__
     }
   }
   return c;
+}
+
+// sturm_count over LDS rows de[k] = {d[k], e2[k-1]} (one 16-byte read per
+// step), same arithmetic: the reciprocal of q and the pivmin test of q run side
+// by side and the clamp selects between rcp(q) and rcp(-pivmin) (v_cndmask,
+// no branch), so the clamp is off the serial chain.
+__device__ inline int sturm_count_rows(const double2 *__restrict__ de, int n, double x,
+                                       double pivmin) {
+  const double rpiv = __builtin_amdgcn_rcp(-pivmin);
+  double q = de[0].x - x;
+  int c = 0;
+  auto stepq = [&](double2 v) {
+    const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(q), pivmin, 5);  // OLE
+    const double r0 = __builtin_amdgcn_rcp(q);
+    const double qe = vsel(tiny, -pivmin, q);
+    c += qe < 0.0;
+    double r = vsel(tiny, rpiv, r0);
+    r = fma(fma(-qe, r, 1.0), r, r);
+    q = fma(-v.y, r, v.x - x);
+  };
+  int k0 = 1;
+  for (; k0 + 8 <= n; k0 += 8) {
+    double2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = de[k0 + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) stepq(v[u]);
+  }
+  for (; k0 < n; ++k0) stepq(de[k0]);
+  const double qe = fabs(q) <= pivmin ? -pivmin : q;
+  return c + (qe < 0.0);
 }
 
 // Gershgorin bounds, ||T||_1 and pivmin: one workgroup.
@@ -498,15 +537,11 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
                                                      double *__restrict__ w_out) {
   extern __shared__ double sh[];
   const double *dd = d, *ee2 = e2g;
+  double2 *rows = reinterpret_cast<double2 *>(sh);  // rows[k] = {d[k], e2[k-1]}
   if (LDS) {
-    double *sd = sh, *se2 = sh + n;
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-      sd[k] = d[k];
-      se2[k] = e2g[k];
-    }
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+      rows[k] = make_double2(d[k], k > 0 ? e2g[k - 1] : 0.0);
     __syncthreads();
-    dd = sd;
-    ee2 = se2;
   }
   const int lane = threadIdx.x & 63;
   const int sub = lane & (ML - 1);
@@ -520,7 +555,9 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
   for (int round = 0; round < ROUNDS; ++round) {
     const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
     int c = 0;
-    if (j < n) c = sturm_count(dd + b0, ee2 + b0, b1 - b0, x, pivmin);
+    if (j < n)
+      c = LDS ? sturm_count_rows(rows + b0, b1 - b0, x, pivmin)
+              : sturm_count(dd + b0, ee2 + b0, b1 - b0, x, pivmin);
     // lanes with count(x) <= jl have x <= lambda_jl
     const unsigned long long m = __ballot(j < n && c <= jl);
     const unsigned long long gm = ML == 64 ? ~0ull : ((1ull << (ML & 63)) - 1) << grp_base;
@@ -751,13 +788,6 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 // moves as two 16-byte accesses.  The whole wave rescales.  Same dgttrf
 // pivoting and substitution order as invit_kernel.
 constexpr int IFCH = 16;
-// msk[lane] ? t : f as two v_cndmask_b32 (no control flow)
-__device__ inline double vsel(uint64_t msk, double t, double f) {
-  int lo, hi;
-  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(__double2loint(f)), "v"(__double2loint(t)), "s"(msk));
-  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(__double2hiint(f)), "v"(__double2hiint(t)), "s"(msk));
-  return __hiloint2double(hi, lo);
-}
 __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict__ d,
                                                        const double *__restrict__ e, int n, int k,
                                                        int first,
