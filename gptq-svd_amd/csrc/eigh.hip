@@ -39,8 +39,13 @@ constexpr int NG = 256;   // workgroups of the symv kernel (16 waves each)
 constexpr int SYT = 1024; // symv threads per workgroup
 constexpr int BT = 64;    // back-transformation block of reflectors
 constexpr int PST = 2 * NB + 2;  // partials stride
-constexpr int ML = 16;    // multisection lanes per eigenvalue
-constexpr int ROUNDS = 14;  // 17^14 > 2^57: the Gershgorin interval shrinks below one ulp
+#ifndef TG_ML
+#define TG_ML 16
+#endif
+constexpr int ML = TG_ML;  // multisection lanes per eigenvalue
+// (ML+1)^ROUNDS > 2^57: the Gershgorin interval shrinks below one ulp
+constexpr int ROUNDS = ML == 16 ? 14 : (ML == 32 ? 12 : 10);
+static_assert(ML == 16 || ML == 32 || ML == 64, "ML");
 constexpr int SPLITK = 8;
 
 struct Tri {
