@@ -508,25 +508,31 @@ __global__ __launch_bounds__(1024) void tri_split_kernel(const double *__restric
 }
 
 // Global ascending order of the block eigenvalues: rank(j) = #{i: v_i < v_j or
-// (v_i == v_j and i < j)} -- deterministic, O(n^2) compares spread over n threads.
-__global__ void rank_sort_kernel(const double *__restrict__ v, int n, double *__restrict__ w_asc,
-                                 int32_t *__restrict__ slot) {
+// (v_i == v_j and i < j)} -- deterministic, O(n^2) compares; 16 lanes per
+// element each count a strided share of i (n/16 workgroups fill the chip).
+constexpr int RS_G = 16;
+__global__ __launch_bounds__(256) void rank_sort_kernel(const double *__restrict__ v, int n,
+                                                        double *__restrict__ w_asc,
+                                                        int32_t *__restrict__ slot) {
   extern __shared__ double sv[];
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tid = threadIdx.x, g = tid & (RS_G - 1);
+  const int j = blockIdx.x * (256 / RS_G) + tid / RS_G;
   const double vj = j < n ? v[j] : 0.0;
   int r = 0;
   for (int c0 = 0; c0 < n; c0 += 2048) {
     const int cn = min(2048, n - c0);
     __syncthreads();
-    for (int c = threadIdx.x; c < cn; c += blockDim.x) sv[c] = v[c0 + c];
+    for (int c = tid; c < cn; c += blockDim.x) sv[c] = v[c0 + c];
     __syncthreads();
     if (j < n)
-      for (int c = 0; c < cn; ++c) {
+      for (int c = g; c < cn; c += RS_G) {
         const double vi = sv[c];
         r += (vi < vj) || (vi == vj && c0 + c < j);
       }
   }
-  if (j < n) {
+#pragma unroll
+  for (int off = RS_G / 2; off > 0; off >>= 1) r += __shfl_xor(r, off, RS_G);
+  if (j < n && g == 0) {
     w_asc[r] = vj;
     slot[r] = j;
   }
@@ -587,10 +593,20 @@ __global__ void square_kernel(const double *__restrict__ e, int n, double *__res
 // A3: truncation rank (gptq_utils.py:94, 97-108), one thread (sequential sums,
 // deterministic).
 // ---------------------------------------------------------------------------
+// LDS: S also staged in LDS (n <= RANK_LDS_N) so the serial passes wait on
+// LDS, not on the global round trip of each batch.
+constexpr int RANK_LDS_N = 16384;
+template <bool LDS>
 __global__ void rank_kernel(const double *__restrict__ w_asc, int n, double thr, int rule,
-                            double *__restrict__ S, int32_t *__restrict__ kout) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) S[i] = sqrt(fmax(w_asc[n - 1 - i], 1e-12));
+                            double *__restrict__ Sg, int32_t *__restrict__ kout) {
+  extern __shared__ double Sl[];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double v = sqrt(fmax(w_asc[n - 1 - i], 1e-12));
+    Sg[i] = v;
+    if (LDS) Sl[i] = v;
+  }
   __syncthreads();
+  const double *S = LDS ? Sl : Sg;
   if (threadIdx.x != 0) return;
   int k = n;
   if (rule == TG_RULE_ENERGY) {
@@ -1162,7 +1178,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   }
   tg::prof_end(st, btok);
   TG_LAUNCHED();
-  hipLaunchKernelGGL(rank_sort_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 2048 * sizeof(double), st,
+  hipLaunchKernelGGL(rank_sort_kernel, dim3(tg::cdiv(n, 256 / RS_G)), dim3(256), 2048 * sizeof(double), st,
                      w.wraw, n, w_asc, w.slot);
   TG_LAUNCHED();
   return 0;
@@ -1173,8 +1189,17 @@ extern "C" int tg_truncation_rank(void *stream, const double *w_asc, int n, doub
   TG_ARG(w_asc, 2, "null w");
   TG_ARG(n >= 1, 3, "n < 1");
   TG_ARG(S_desc && k_dev, 6, "null output");
-  hipLaunchKernelGGL(rank_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, w_asc, n, threshold,
-                     rule, S_desc, k_dev);
+  if (n <= RANK_LDS_N) {
+    const size_t lds = sizeof(double) * size_t(n);
+    if (lds > 48 * 1024)
+      TG_HIP(hipFuncSetAttribute((const void *)rank_kernel<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    hipLaunchKernelGGL(rank_kernel<true>, dim3(1), dim3(256), lds, (hipStream_t)stream, w_asc, n,
+                       threshold, rule, S_desc, k_dev);
+  } else {
+    hipLaunchKernelGGL(rank_kernel<false>, dim3(1), dim3(256), 0, (hipStream_t)stream, w_asc, n,
+                       threshold, rule, S_desc, k_dev);
+  }
   TG_LAUNCHED();
   return 0;
 }
