@@ -607,32 +607,49 @@ __global__ void rank_kernel(const double *__restrict__ w_asc, int n, double thr,
   }
   __syncthreads();
   const double *S = LDS ? Sl : Sg;
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
   int k = n;
   if (rule == TG_RULE_ENERGY) {
-    // sequential sums (the reference's order), loads batched 16 at a time
+    // sequential sums in the reference's order: the lanes square a chunk of
+    // 64 values side by side and the serial adds take them by v_readlane
+    auto sq_at = [&](int i0) {
+      const double v = i0 + lane < n ? S[i0 + lane] : 0.0;
+      return v * v;
+    };
+    auto rl = [](double x, int u) {
+      return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), u),
+                              __builtin_amdgcn_readlane(__double2loint(x), u));
+    };
     double total = 0.0;
-    for (int i0 = 0; i0 < n; i0 += 16) {
-      double v[16];
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const double q = sq_at(i0);
+      if (i0 + 64 <= n) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = S[min(i0 + u, n - 1)];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (i0 + u < n) total += v[u] * v[u];
+        for (int u = 0; u < 64; ++u) total += rl(q, u);
+      } else {
+        for (int u = 0; u < n - i0; ++u) total += rl(q, u);
+      }
     }
     const double target = (1.0 - thr) * total;
+    // the partial sums never decrease (squares >= 0): once one exceeds the
+    // target every later one does, so the count stops at that chunk
     double cs = 0.0;
     int cnt = 0;
-    for (int i0 = 0; i0 < n; i0 += 16) {
-      double v[16];
+    for (int i0 = 0; i0 < n && cs <= target; i0 += 64) {
+      const double q = sq_at(i0);
+      if (i0 + 64 <= n) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = S[min(i0 + u, n - 1)];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (i0 + u < n) {
-          cs += v[u] * v[u];
+        for (int u = 0; u < 64; ++u) {
+          cs += rl(q, u);
           cnt += cs <= target;
         }
+      } else {
+        for (int u = 0; u < n - i0; ++u) {
+          cs += rl(q, u);
+          cnt += cs <= target;
+        }
+      }
     }
     k = cnt < n ? cnt + 1 : cnt;
   } else if (rule == TG_RULE_MEAN_TRIMMED) {
@@ -644,10 +661,12 @@ __global__ void rank_kernel(const double *__restrict__ w_asc, int n, double thr,
       ref = s / double(ref_k - 1);
     }
     int cnt = 0;
-    for (int i = 0; i < n; ++i) cnt += S[i] > thr * ref;
+    for (int i = lane; i < n; i += 64) cnt += S[i] > thr * ref;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
     k = cnt;
   }
-  *kout = k;
+  if (lane == 0) *kout = k;
 }
 
 // ---------------------------------------------------------------------------
