@@ -14,13 +14,31 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-@pytest.mark.parametrize("n,first,count", [(600, 0, 14), (2048, 1500, 14), (2048, 0, 48),
-                                           (4100, 3058, 14), (4100, 4099, 1)])
-def test_few_vectors(n, first, count):
-    from gptq_svd_amd import _lib as lib
-    rng = np.random.default_rng(n + first)
+def _wishart(n, seed):
+    rng = np.random.default_rng(seed)
     X = rng.standard_normal((3 * n // 2, n))
-    H = X.T @ X / X.shape[0]
+    return X.T @ X / X.shape[0]
+
+
+def _blockdiag(n, seed):
+    """Wishart block + a diagonal tail: the tridiagonal splits into an
+    unreduced block and 1x1 blocks (exercises the block-local solves)."""
+    nb = n // 2
+    H = np.zeros((n, n))
+    H[:nb, :nb] = _wishart(nb, seed)
+    H[nb:, nb:] = np.diag(np.linspace(0.05, 2.5, n - nb))
+    return H
+
+
+# count <= 256: one LDS-resident wave per vector (invit_lds_kernel);
+# count > 256: the register path (invit_kernel)
+@pytest.mark.parametrize("n,first,count,kind", [
+    (600, 0, 14, "wishart"), (2048, 1500, 14, "wishart"), (2048, 0, 48, "wishart"),
+    (4100, 3058, 14, "wishart"), (4100, 4099, 1, "wishart"), (1000, 0, 300, "wishart"),
+    (700, 0, 20, "blockdiag"), (700, 640, 60, "blockdiag")])
+def test_few_vectors(n, first, count, kind):
+    from gptq_svd_amd import _lib as lib
+    H = _wishart(n, n + first) if kind == "wishart" else _blockdiag(n, n + first)
     A = torch.from_numpy(H).to(DEV)
     ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
     w = torch.empty(n, dtype=torch.float64, device=DEV)
