@@ -702,16 +702,24 @@ __global__ __launch_bounds__(256) void q2_tfactor_kernel(const double *__restric
     Ts[a][c] = 0.0;
   }
   __syncthreads();
-  for (int c = 0; c < QB; ++c) {
-    const double tc = taus[c];
-    if (tid < c) {
+  // row a of T is independent of the other rows (dlarft forward columnwise):
+  // T[a][c] = -tau_c sum_{a<=e<c} T[a][e] G[e][c], T[a][a] = tau_a; thread a
+  // keeps its row in registers (no barrier per column).  The terms e < a are
+  // exact zeros, so the sums match the column-by-column order bit for bit.
+  if (tid < QB) {
+    double trow[QB];
+#pragma unroll
+    for (int c = 0; c < QB; ++c) {
       double acc = 0.0;
-      for (int e = tid; e < c; ++e) acc += Ts[tid][e] * Gs[e][c];
-      Ts[tid][c] = -tc * acc;
+#pragma unroll
+      for (int e = 0; e < c; ++e) acc += trow[e] * Gs[e][c];
+      const double tc = taus[c];
+      trow[c] = tid < c ? -tc * acc : (tid == c ? tc : 0.0);
     }
-    if (tid == c) Ts[c][c] = tc;
-    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < QB; ++c) Ts[tid][c] = trow[c];
   }
+  __syncthreads();
   for (int idx = tid; idx < QB * QB; idx += 256) Tout[idx] = Ts[idx >> 5][idx & 31];
 }
 
