@@ -77,16 +77,21 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.V2, nsw * smax * SB_B);
   take(b.tau2, nsw * smax);
   take(b.T2, sb2st_t2_count(n));
-  if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw);
-  else ar.template take<unsigned>(nsw);
+  // per-group progress + 4 control words (XCD, group queue, stall flag)
+  if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw + 4);
+  else ar.template take<unsigned>(nsw + 4);
 }
 
 // A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth
 // SB_B in place (full storage, zeros outside the band); reflectors in bufs.
 hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b);
 // Band (in A after sy2sb) -> tridiagonal (d, e) by bulge chasing.
+// A stalled hand-off (a wait beyond the timeout, TG_BULGE_TIMEOUT_TICKS of the
+// 100 MHz clock, default 2 s) poisons d and e with NaN; the stall flag stays
+// in prog and is read back by sb2st_stalled (one D2H copy + stream sync).
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
                  double *tau2, unsigned *prog, double *d, double *e);
+hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled);
 // Z (n x k row-major) <- Q2 Z.
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
                        const double *tau2, double *T2);

@@ -357,7 +357,8 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
                                                        double *__restrict__ tau2, int smax,
                                                        unsigned *__restrict__ prog,
                                                        unsigned *__restrict__ ctl,
-                                                       unsigned long long *__restrict__ stats) {
+                                                       unsigned long long *__restrict__ stats,
+                                                       unsigned long long timeout) {
   uint64_t sw = 0, stk = 0, sbar = 0, spf = 0, swb = 0, nsteps = 0;
   __shared__ double R[RING][LDB];
   __shared__ WaveScratch wsc[NCW];
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
         while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                unsigned(need)) {
           __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up
+          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
             __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
               while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                      unsigned(need)) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
                   __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                   break;
                 }
@@ -580,12 +581,16 @@ __global__ void extract_band_kernel(const double *__restrict__ A, int64_t lda, i
   Bst[idx] = (d <= SB_B && c + d < n) ? A[int64_t(c + d) * lda + c] : 0.0;
 }
 
-__global__ void extract_tri_kernel(const double *__restrict__ Bst, int n, double *__restrict__ dg,
+__global__ void extract_tri_kernel(const double *__restrict__ Bst, int n,
+                                   const unsigned *__restrict__ stall, double *__restrict__ dg,
                                    double *__restrict__ e) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  dg[i] = Bst[int64_t(i) * LDB];
-  e[i] = (i + 1 < n) ? Bst[int64_t(i) * LDB + 1] : 0.0;
+  // a stalled pipeline chased on stale band data: poison (d, e) so no
+  // consumer takes its eigenvalues for real ones
+  const bool bad = stall && *stall != 0u;
+  dg[i] = bad ? __builtin_nan("") : Bst[int64_t(i) * LDB];
+  e[i] = bad ? __builtin_nan("") : (i + 1 < n) ? Bst[int64_t(i) * LDB + 1] : 0.0;
 }
 
 }  // namespace
@@ -601,11 +606,15 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   const int nsw = n - 2;
+  const unsigned *stall = nullptr;
   if (nsw > 0) {
     const int ngroups = cdiv(nsw, G_SW);
     err = hipMemsetAsync(prog, 0, sizeof(unsigned) * (ngroups + 4), st);
     if (err != hipSuccess) return err;
-    unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] timeout flag
+    unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] stall flag
+    stall = ctl + 2;
+    const char *tt = getenv("TG_BULGE_TIMEOUT_TICKS");
+    const unsigned long long timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s
     unsigned long long *stats = nullptr;
     const bool want = getenv("TG_BULGE_STATS") != nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -623,7 +632,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / G_SW,
                           12.0 * SB_B * SB_B * ntask);
     hipLaunchKernelGGL(bulge_lds_kernel, dim3(256), dim3(BT), 0, st, Bst, n, V2, tau2, sb_smax(n),
-                       prog, ctl, stats);
+                       prog, ctl, stats, timeout);
     tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -652,8 +661,21 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       (void)hipFree(stats);
     }
   }
-  hipLaunchKernelGGL(extract_tri_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, Bst, n, d, e);
+  hipLaunchKernelGGL(extract_tri_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, Bst, n, stall, d,
+                     e);
   return hipGetLastError();
+}
+
+hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled) {
+  *stalled = false;
+  const int nsw = n - 2;
+  if (nsw <= 0) return hipSuccess;
+  unsigned h = 0;
+  hipError_t e = hipMemcpyAsync(&h, prog + cdiv(nsw, G_SW) + 2, sizeof(unsigned),
+                                hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  *stalled = h != 0u;
+  return e;
 }
 
 }  // namespace tg

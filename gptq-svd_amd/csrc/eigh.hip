@@ -21,6 +21,7 @@
 //   4. Back-transformation V = Q Z with compact-WY blocks of BT reflectors
 //      (dlarft T factors, FP64 MFMA GEMMs, split-K for the V^T Z products).
 #include <algorithm>
+#include <vector>
 #include <cfloat>
 #include <cstdlib>
 #include <cmath>
@@ -71,6 +72,8 @@ struct Tri {
   int32_t *be;   // n   end (exclusive) of that block
   int32_t *slot; // n   slot of the j-th smallest eigenvalue
   unsigned *cnt; // reduction tickets
+  int32_t *cl;   // 2 + 4n  cluster lists: [0] small count, [1] big count, small (start, len)
+                 //         pairs from 2, big pairs from 2 + 2n
 };
 
 template <class A>
@@ -106,6 +109,7 @@ void tri_layout(A &ar, int n, Tri *t) {
   take(q.bs, n);
   take(q.be, n);
   take(q.slot, n);
+  take(q.cl, 2 + 4 * size_t(n));
 }
 
 // ---------------------------------------------------------------------------
@@ -984,22 +988,47 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
   }
 }
 
-// Re-orthogonalise clusters of (near-)equal eigenvalues (gap <= reltol*||T||)
-// by modified Gram-Schmidt, one workgroup walking the k columns (column jj =
-// eigenvalue first + jj in descending order).
-__global__ __launch_bounds__(256) void cluster_mgs_kernel(const double *__restrict__ w_asc, int n,
-                                                          int k, int first,
-                                                          const double *__restrict__ bnd,
-                                                          double reltol, double *__restrict__ Z) {
-  __shared__ double scratch[8];
+// Re-orthogonalisation of clusters.  Inverse iteration leaves eigenvectors of
+// eigenvalues a gap apart orthogonal to ~eps ||T|| / gap, so columns whose
+// consecutive eigenvalues are within ortol * ||T|| (default 1e-6: the other
+// pairs stay orthogonal to ~2e-10) are re-orthogonalised as a group (LAPACK
+// dstein does the same with ortol = 1e-3, at O(c^2 n) per cluster of c).
+// cluster_scan_kernel lists the clusters (columns jj = eigenvalue first + jj
+// in descending order); clusters of <= MGS_MAX columns are handled by
+// mgs_cols_kernel, one workgroup each, all at once; larger ones by block
+// Gram-Schmidt twice (GEMMs against the finished columns) over MGS_MAX-column
+// panels, each panel finished by mgs_cols_kernel.
+constexpr int MGS_MAX = 64;
+
+__global__ void cluster_scan_kernel(const double *__restrict__ w_asc, int n, int k, int first,
+                                    const double *__restrict__ bnd, double reltol,
+                                    int32_t *__restrict__ cl) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const double gap = reltol * bnd[2];
   const double *wd = w_asc + (n - 1 - first);  // wd[-jj] = eigenvalue of column jj
-  int start = 0;
+  int ns = 0, nb = 0, start = 0;
   while (start < k) {
     int end = start + 1;
     while (end < k && fabs(wd[-(end - 1)] - wd[-end]) <= gap) ++end;
-    for (int c = start; c < end && end - start > 1; ++c) {
-      for (int pass = 0; pass < 2; ++pass)  // MGS twice ("twice is enough")
+    if (end - start > 1) {
+      int32_t *dst = end - start <= MGS_MAX ? cl + 2 + 2 * ns++ : cl + 2 + 2 * n + 2 * nb++;
+      dst[0] = start;
+      dst[1] = end - start;
+    }
+    start = end;
+  }
+  cl[0] = ns;
+  cl[1] = nb;
+}
+
+// Modified Gram-Schmidt twice ("twice is enough") over the columns
+// [start, start + len) of Z (n x k), one workgroup per (start, len) entry.
+__global__ __launch_bounds__(256) void mgs_cols_kernel(const int32_t *__restrict__ list, int n,
+                                                       int k, double *__restrict__ Z) {
+  __shared__ double scratch[8];
+  const int start = list[2 * blockIdx.x], end = start + list[2 * blockIdx.x + 1];
+  for (int c = start; c < end; ++c) {
+    for (int pass = 0; pass < 2; ++pass)
       for (int b = start; b < c; ++b) {
         double dot = 0.0;
         for (int i = threadIdx.x; i < n; i += blockDim.x) dot += Z[size_t(i) * k + b] * Z[size_t(i) * k + c];
@@ -1007,14 +1036,12 @@ __global__ __launch_bounds__(256) void cluster_mgs_kernel(const double *__restri
         for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] -= dot * Z[size_t(i) * k + b];
         __syncthreads();
       }
-      double nrm = 0.0;
-      for (int i = threadIdx.x; i < n; i += blockDim.x) nrm += Z[size_t(i) * k + c] * Z[size_t(i) * k + c];
-      nrm = tg::block_sum(nrm, scratch);
-      const double inv = 1.0 / sqrt(nrm);
-      for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] *= inv;
-      __syncthreads();
-    }
-    start = end;
+    double nrm = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) nrm += Z[size_t(i) * k + c] * Z[size_t(i) * k + c];
+    nrm = tg::block_sum(nrm, scratch);
+    const double inv = 1.0 / sqrt(nrm);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] *= inv;
+    __syncthreads();
   }
 }
 
@@ -1128,6 +1155,13 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   if (ts) {
     TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
     TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.tau2, sb.prog, w.d, w.e));
+    bool stalled = false;
+    TG_HIP(tg::sb2st_stalled(st, n, sb.prog, &stalled));
+    if (stalled) {
+      tg::set_error("tg_eigh_values: bulge-chasing pipeline stalled (a hand-off wait timed out); "
+                    "the tridiagonal form is invalid");
+      return int(hipErrorLaunchTimeOut);
+    }
   }
   if (!ts) {
   TG_HIP(hipMemsetAsync(w.V, 0, sizeof(double) * size_t(n) * n, st));
@@ -1261,9 +1295,53 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   }
   tg::prof_end(st, itok);
   TG_LAUNCHED();
-  hipLaunchKernelGGL(cluster_mgs_kernel, dim3(1), dim3(256), 0, st, w_asc, n, k, first, bnd, 1e-9,
-                     w.Z);
-  TG_LAUNCHED();
+  {
+    const char *ot = getenv("TG_INVIT_ORTOL");
+    const double ortol = ot ? atof(ot) : 1e-6;
+    hipLaunchKernelGGL(cluster_scan_kernel, dim3(1), dim3(64), 0, st, w_asc, n, k, first, bnd,
+                       ortol, w.cl);
+    TG_LAUNCHED();
+    int32_t cnt[2] = {0, 0};
+    TG_HIP(hipMemcpyAsync(cnt, w.cl, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    TG_HIP(hipStreamSynchronize(st));
+    if (cnt[0] > 0) {
+      hipLaunchKernelGGL(mgs_cols_kernel, dim3(cnt[0]), dim3(256), 0, st, w.cl + 2, n, k, w.Z);
+      TG_LAUNCHED();
+    }
+    if (cnt[1] > 0) {
+      std::vector<int32_t> big(2 * size_t(cnt[1]));
+      TG_HIP(hipMemcpyAsync(big.data(), w.cl + 2 + 2 * size_t(n), sizeof(int32_t) * big.size(),
+                            hipMemcpyDeviceToHost, st));
+      TG_HIP(hipStreamSynchronize(st));
+      // panel entries (start, width) of every big cluster, for mgs_cols_kernel
+      std::vector<int32_t> pan;
+      for (int c = 0; c < cnt[1]; ++c)
+        for (int p = 0; p < big[2 * c + 1]; p += MGS_MAX) {
+          pan.push_back(big[2 * c] + p);
+          pan.push_back(std::min(MGS_MAX, big[2 * c + 1] - p));
+        }
+      int32_t *plist = w.cl + 2 + 2 * size_t(n) + 2 * size_t(cnt[1]);
+      TG_HIP(hipMemcpyAsync(plist, pan.data(), sizeof(int32_t) * pan.size(),
+                            hipMemcpyHostToDevice, st));
+      double *X = w.lu;  // (cluster columns done) x MGS_MAX scratch
+      int e = 0;
+      for (int c = 0; c < cnt[1]; ++c) {
+        const int cs = big[2 * c], cl = big[2 * c + 1];
+        for (int p = 0; p < cl; p += MGS_MAX, ++e) {
+          const int pw = std::min(MGS_MAX, cl - p), p0 = cs + p;
+          for (int pass = 0; pass < 2 && p > 0; ++pass) {
+            // Z_p -= Z_done (Z_done^T Z_p)
+            TG_HIP(tg::dgemm(st, true, false, p, pw, n, 1.0, w.Z + cs, k, w.Z + p0, k, 0.0, X, pw));
+            TG_HIP(tg::dgemm(st, false, false, n, pw, p, -1.0, w.Z + cs, k, X, pw, 1.0, w.Z + p0,
+                             k));
+          }
+          hipLaunchKernelGGL(mgs_cols_kernel, dim3(1), dim3(256), 0, st, plist + 2 * e, n, k, w.Z);
+          TG_LAUNCHED();
+        }
+      }
+      TG_HIP(hipStreamSynchronize(st));  // pan is read by the copy above
+    }
+  }
   // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
   const bool ts = two_stage(n);
   const int nref = ts ? 0 : n - 1;

@@ -1421,6 +1421,183 @@ __global__ void identity_kernel(int n, double *__restrict__ R, int64_t ldr) {
     R[i * ldr + j] = i == j ? 1.0 : 0.0;
 }
 
+// ---------------------------------------------------------------------------
+// Conditioning guard of the Gram-matrix (CholeskyQR) factors of U.
+// tg_u_factor and tg_u_factor_rx take R from the Cholesky factor of a Gram
+// matrix Y^T Y, which squares Y's condition number (the reference runs a
+// Householder QR, gptq_utils.py:120).  After the first Cholesky the host reads
+// the factor's info count and diagonal range; when a pivot broke down, or
+// (max/min diag)^2 * eps puts the factor's error above ~1e-9, the factor is
+// refined by CholeskyQR passes on the explicit Q = Y R^-1 (CholeskyQR2), with
+// a shifted first factorisation when the plain one broke down (shifted
+// CholeskyQR3: G + s I, s = 11 (k^2 + k (k+1)) u ||Y||_F^2).
+// ---------------------------------------------------------------------------
+// out[0] = max |d_i|, out[1] = min d_i (0 when any is non-positive or not
+// finite), diagonal of the k x k upper factor U
+__global__ __launch_bounds__(256) void diag_range_kernel(const double *__restrict__ U, int64_t ldu,
+                                                         int k, double *__restrict__ out) {
+  __shared__ double mx[256], mn[256];
+  double a = 0.0, b = DBL_MAX;
+  for (int i = threadIdx.x; i < k; i += 256) {
+    const double d = U[i * ldu + i];
+    const bool ok = d > 0.0 && d <= DBL_MAX;
+    a = ok ? fmax(a, d) : a;
+    b = ok ? fmin(b, d) : 0.0;
+  }
+  mx[threadIdx.x] = a;
+  mn[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      mx[threadIdx.x] = fmax(mx[threadIdx.x], mx[threadIdx.x + s]);
+      mn[threadIdx.x] = fmin(mn[threadIdx.x], mn[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = mx[0];
+    out[1] = mn[0];
+  }
+}
+
+// out[0] = trace of the k x k matrix G (fixed summation order)
+__global__ __launch_bounds__(256) void diag_sum_kernel(const double *__restrict__ G, int64_t ldg,
+                                                       int k, double *__restrict__ out) {
+  __shared__ double part[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < k; i += 256) acc += G[i * ldg + i];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = part[0];
+}
+
+__global__ void add_diag_kernel(double *__restrict__ G, int64_t ldg, int k, double s) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k) G[i * ldg + i] += s;
+}
+
+struct CholStat {
+  double dmax, dmin, trace;
+  int info;
+};
+
+// stats[0..2] = {max diag, min diag, trace}, info -> host (one sync)
+static hipError_t read_stat(hipStream_t st, const double *stats, const int *info, CholStat &h) {
+  double v[3];
+  hipError_t e = hipMemcpyAsync(v, stats, sizeof(v), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(&h.info, info, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  h.dmax = v[0];
+  h.dmin = v[1];
+  h.trace = v[2];
+  return e;
+}
+
+// 0: never refine, 1: always refine, 2 (default): refine when the guard asks
+static int refine_mode() {
+  const char *e = getenv("TG_U_REFINE");
+  return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
+}
+
+// the first factor is not trusted: breakdown (always handled), or
+// (dmax/dmin)^2 eps > 1e-9 (TG_U_REFINE=0 / 1 disable / force this part)
+static bool needs_refine(const CholStat &h) {
+  if (h.info > 0 || !(h.dmin > 0.0)) return true;
+  const int mode = refine_mode();
+  if (mode != 2) return mode == 1;
+  const double r = h.dmax / h.dmin;
+  return r * r * DBL_EPSILON > 1e-9;
+}
+
+// Y = R^-1 (k x k upper, ld k); T: trinv_offdiag scratch
+static hipError_t trinv(hipStream_t st, const double *R, int ldr, int k, double *Y, double *T) {
+  hipError_t e = hipMemsetAsync(Y, 0, sizeof(double) * size_t(k) * k, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, R, ldr, k, Y, k);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return trinv_offdiag(st, R, ldr, Y, k, k, T);
+}
+
+static hipError_t zero_lower(hipStream_t st, double *U, int ldu, int k) {
+  hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
+                     dim3(256), 0, st, U, ldu, k);
+  return hipGetLastError();
+}
+
+// Scratch of the refinement: Ri, Q, G (k x k each), T (trinv), stats.
+struct RefineWs {
+  double *Ri, *Q, *G, *T, *stats;
+};
+
+// Shifted first factor: R (k x k, ld k) = chol(Y^T Y + s I), s from trace(Y^T Y).
+static int shifted_factor(hipStream_t st, const double *Y, int64_t ldy, int k, double *R,
+                          RefineWs &w, double *Wb, int *info, CholStat &h) {
+  TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, Y, ldy, 0.0, R, k));
+  hipLaunchKernelGGL(diag_sum_kernel, dim3(1), dim3(256), 0, st, R, int64_t(k), k, w.stats + 2);
+  TG_LAUNCHED();
+  TG_HIP(read_stat(st, w.stats, info, h));
+  const double kk = double(k);
+  const double s = 11.0 * (kk * kk + kk * (kk + 1.0)) * (DBL_EPSILON / 2) * h.trace;
+  hipLaunchKernelGGL(add_diag_kernel, dim3(tg::cdiv(k, 256)), dim3(256), 0, st, R, int64_t(k), k, s);
+  TG_LAUNCHED();
+  TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  TG_HIP(chol_upper_rows(st, R, k, k, k, Wb, info));
+  TG_HIP(zero_lower(st, R, k, k));
+  hipLaunchKernelGGL(diag_range_kernel, dim3(1), dim3(256), 0, st, R, int64_t(k), k, w.stats);
+  TG_LAUNCHED();
+  TG_HIP(read_stat(st, w.stats, info, h));
+  if (h.info > 0 || !(h.dmin > 0.0)) {
+    tg::set_error("U factor: shifted Cholesky of the Gram matrix broke down (%d pivots; "
+                  "input not of full rank k = %d)", h.info, k);
+    return int(hipErrorUnknown);
+  }
+  return 0;
+}
+
+// One CholeskyQR pass: Q = Y R^-1, Q^T Q = R'^T R', R <- R' R.
+static int cholqr_pass(hipStream_t st, const double *Y, int64_t ldy, int k, double *R,
+                       RefineWs &w, double *Wb, int *info) {
+  TG_HIP(trinv(st, R, k, k, w.Ri, w.T));
+  TG_HIP(tg::dgemm(st, false, false, k, k, k, 1.0, Y, ldy, w.Ri, k, 0.0, w.Q, k));
+  TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, w.Q, k, 0.0, w.G, k));
+  TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  TG_HIP(chol_upper_rows(st, w.G, k, k, k, Wb, info));
+  TG_HIP(zero_lower(st, w.G, k, k));
+  TG_HIP(tg::dgemm(st, false, false, k, k, k, 1.0, w.G, k, R, k, 0.0, w.Ri, k));  // R' R
+  TG_HIP(hipMemcpyAsync(R, w.Ri, sizeof(double) * size_t(k) * k, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(diag_range_kernel, dim3(1), dim3(256), 0, st, R, int64_t(k), k, w.stats);
+  TG_LAUNCHED();
+  CholStat h{};
+  TG_HIP(read_stat(st, w.stats, info, h));
+  if (h.info > 0 || !(h.dmin > 0.0)) {
+    tg::set_error("U factor: CholeskyQR refinement broke down (%d pivots, k = %d)", h.info, k);
+    return int(hipErrorUnknown);
+  }
+  return 0;
+}
+
+// Refined R (k x k, ld k) of Y (k x k, ld ldy), given the first factor in R
+// and its statistics h: shifted restart on breakdown, then 1 (2 after a
+// shift) CholeskyQR passes.
+static int refine_factor(hipStream_t st, const double *Y, int64_t ldy, int k, double *R,
+                         RefineWs &w, double *Wb, int *info, CholStat h) {
+  int passes = 1;
+  if (h.info > 0 || !(h.dmin > 0.0)) {
+    const int e = shifted_factor(st, Y, ldy, k, R, w, Wb, info, h);
+    if (e != 0) return e;
+    passes = 2;
+  }
+  for (int p = 0; p < passes; ++p) {
+    const int e = cholqr_pass(st, Y, ldy, k, R, w, Wb, info);
+    if (e != 0) return e;
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" size_t tg_pivot_workspace_size(int n, int k) {
@@ -1616,11 +1793,42 @@ extern "C" int tg_pivoted_factor_complement(void *stream, const double *H, int l
   return pivot_core(st, w, n, k, perm, Rx, ldr);
 }
 
+template <class Ar>
+static void refine_layout(Ar &ar, int k, RefineWs *w) {
+  RefineWs d{};
+  RefineWs &q = w ? *w : d;
+  const size_t h = size_t(NU) * ((tg::cdiv(k, NU) + 1) / 2);
+  auto t = [&](double *&dst, size_t cnt) {
+    if constexpr (std::is_same_v<Ar, tg::Arena>) dst = ar.template take<double>(cnt);
+    else ar.template take<double>(cnt);
+  };
+  t(q.Ri, size_t(k) * k);
+  t(q.Q, size_t(k) * k);
+  t(q.G, size_t(k) * k);
+  t(q.T, h * h);
+  t(q.stats, 8);
+}
+
+template <class Ar>
+static void ufac_layout(Ar &ar, int n, int k, double **A, int **info, double **Wb, double **Rk,
+                        RefineWs *w) {
+  auto t = [&](auto *&dst, size_t cnt) {
+    using T = std::remove_reference_t<decltype(*dst)>;
+    if constexpr (std::is_same_v<Ar, tg::Arena>) dst = ar.template take<T>(cnt);
+    else ar.template take<T>(cnt);
+  };
+  double *d[3];
+  int *i0;
+  t(A ? *A : d[0], size_t(k) * n);
+  t(info ? *info : i0, 16);
+  t(Wb ? *Wb : d[1], NU * NU);
+  t(Rk ? *Rk : d[2], size_t(k) * k);
+  refine_layout(ar, k, w);
+}
+
 extern "C" size_t tg_ufactor_workspace_size(int n, int k) {
   tg::Sizer s;
-  s.take<double>(size_t(k) * n);
-  s.take<int>(16);
-  s.take<double>(NU * NU);
+  ufac_layout(s, n, k, nullptr, nullptr, nullptr, nullptr, nullptr);
   return s.off + 256;
 }
 
@@ -1637,9 +1845,10 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   TG_ARG(ldu >= n, 9, "ldu < n");
   hipStream_t st = (hipStream_t)stream;
   tg::Arena ar(ws, ws_bytes);
-  double *A = ar.take<double>(size_t(k) * n);
-  int *info = ar.take<int>(16);
-  double *Wb = ar.take<double>(NU * NU);
+  double *A, *Wb, *Rk;
+  int *info;
+  RefineWs rw{};
+  ufac_layout(ar, n, k, &A, &info, &Wb, &Rk, &rw);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   hipLaunchKernelGGL(gather_scale_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
@@ -1648,9 +1857,25 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
   // G[:k, :] = A[:, :k]^T A   (k x n) into U
   TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));
   TG_HIP(chol_upper_rows(st, U, ldu, k, n, Wb, info));
-  hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
-                     dim3(256), 0, st, U, ldu, k);
+  TG_HIP(zero_lower(st, U, ldu, k));
+  hipLaunchKernelGGL(diag_range_kernel, dim3(1), dim3(256), 0, st, U, int64_t(ldu), k, rw.stats);
   TG_LAUNCHED();
+  CholStat h{};
+  TG_HIP(read_stat(st, rw.stats, info, h));
+  if (!needs_refine(h)) return 0;
+  // Refined: R11 by CholeskyQR passes on A1 = A[:, :k], then R12 = Q^T A2
+  // with the explicit Q = A1 R11^-1 (not R11^-T G12, whose error grows with
+  // cond(A1)^2).
+  if (h.info == 0 && h.dmin > 0.0)
+    TG_HIP(hipMemcpy2DAsync(Rk, sizeof(double) * k, U, sizeof(double) * ldu, sizeof(double) * k,
+                            k, hipMemcpyDeviceToDevice, st));
+  const int e = refine_factor(st, A, n, k, Rk, rw, Wb, info, h);
+  if (e != 0) return e;
+  TG_HIP(trinv(st, Rk, k, k, rw.Ri, rw.T));
+  TG_HIP(tg::dgemm(st, false, false, k, k, k, 1.0, A, n, rw.Ri, k, 0.0, rw.Q, k));
+  TG_HIP(hipMemcpy2DAsync(U, sizeof(double) * ldu, Rk, sizeof(double) * k, sizeof(double) * k, k,
+                          hipMemcpyDeviceToDevice, st));
+  if (n > k) TG_HIP(tg::dgemm(st, true, false, k, n - k, k, 1.0, rw.Q, k, A + k, n, 0.0, U + k, ldu));
   return 0;
 }
 
@@ -1676,14 +1901,14 @@ extern "C" int tg_u_factor(void *stream, const double *Vh, int ldv, const double
 // Cholesky of the two-Cholesky form factors.
 template <class Ar>
 static void urx_layout(Ar &ar, int n, int k, double **S, double **Y, double **Bm, double **A,
-                       double **Tt, double **Wb, int **info) {
+                       double **Tt, double **Wb, int **info, double **Rq, RefineWs *rw) {
   const size_t h = size_t(NU) * ((tg::cdiv(k, NU) + 1) / 2);
   auto t = [&](auto *&dst, size_t cnt) {
     using T = std::remove_reference_t<decltype(*dst)>;
     if constexpr (std::is_same_v<Ar, tg::Arena>) dst = ar.template take<T>(cnt);
     else ar.template take<T>(cnt);
   };
-  double *d[6];
+  double *d[7];
   int *i0;
   t(S ? *S : d[0], size_t(k) * k);
   t(Y ? *Y : d[1], size_t(k) * k);
@@ -1692,6 +1917,8 @@ static void urx_layout(Ar &ar, int n, int k, double **S, double **Y, double **Bm
   t(Tt ? *Tt : d[4], h * h);
   t(Wb ? *Wb : d[5], size_t(NU) * NU);
   t(info ? *info : i0, 16);
+  t(Rq ? *Rq : d[6], size_t(k) * k);
+  refine_layout(ar, k, rw);
 }
 
 
@@ -1705,7 +1932,8 @@ __global__ void flip_both_kernel(const double *__restrict__ N, int k, double *__
 
 extern "C" size_t tg_ufactor_rx_workspace_size(int n, int k) {
   tg::Sizer s;
-  urx_layout(s, n, k, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  urx_layout(s, n, k, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+             nullptr);
   return s.off + 256;
 }
 
@@ -1719,9 +1947,10 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
   TG_ARG(ldu >= n, 7, "ldu < n");
   hipStream_t st = (hipStream_t)stream;
   tg::Arena ar(ws, ws_bytes);
-  double *S, *Y, *Bm, *A, *Tt, *Wb;
+  double *S, *Y, *Bm, *A, *Tt, *Wb, *Rq;
   int *info;
-  urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info);
+  RefineWs rw{};
+  urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info, &Rq, &rw);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   static const bool two_chol = getenv("TG_URX_TWOCHOL") != nullptr;
@@ -1741,21 +1970,38 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
       TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));  // + R12 C^T
     }
     TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));           // N = Z Z^T
-    hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, ZT);  // N' = J N J
+    hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, Rq);  // N' = J N J
     TG_LAUNCHED();
-    TG_HIP(chol_upper_rows(st, ZT, k, k, k, Wb, info));               // N' = R^T R
-    TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
-    hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, ZT, k, k, Yr, k);
+    TG_HIP(chol_upper_rows(st, Rq, k, k, k, Wb, info));               // N' = R^T R
+    hipLaunchKernelGGL(diag_range_kernel, dim3(1), dim3(256), 0, st, Rq, int64_t(k), k, rw.stats);
     TG_LAUNCHED();
-    TG_HIP(trinv_offdiag(st, ZT, k, Yr, k, k, Tt));                   // Yr = R^-1
+    CholStat h{};
+    TG_HIP(read_stat(st, rw.stats, info, h));
+    if (needs_refine(h)) {
+      // R is the R factor of Yq = J Z^T J (Yq^T Yq = N'): CholeskyQR passes on Yq
+      double *Yq = Nm;
+      TG_HIP(zero_lower(st, Rq, k, k));
+      hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, ZT, k, Yq);
+      TG_LAUNCHED();
+      const int e = refine_factor(st, Yq, k, k, Rq, rw, Wb, info, h);
+      if (e != 0) return e;
+    }
+    TG_HIP(trinv(st, Rq, k, k, Yr, Tt));                              // Yr = R^-1
     hipLaunchKernelGGL(flip_transpose_kernel, gk, dim3(256), 0, st, Yr, k, U, int64_t(ldu));
     TG_LAUNCHED();                                                    // U11 = V^-1 = J R^-T J
     if (m > 0)
       TG_HIP(tg::dgemm(st, false, false, k, m, k, 1.0, U, ldu, C, m, 0.0, U + k, ldu));  // V^-1 C
     return 0;
   }
+  CholStat h{};
   TG_HIP(tg::dsyrk_nt(st, k, n, 1.0, Rx, ldr, 0.0, S, k));        // S = R_x R_x^T
   TG_HIP(chol_upper_rows(st, S, k, k, k, Wb, info));                // S <- T, T^T T = S
+  TG_HIP(read_stat(st, rw.stats, info, h));
+  if (h.info > 0) {
+    tg::set_error("U factor (two-Cholesky form): R_x R_x^T is not positive definite (%d pivots)",
+                  h.info);
+    return int(hipErrorUnknown);
+  }
   TG_HIP(hipMemsetAsync(Y, 0, sizeof(double) * size_t(k) * k, st));
   hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, S, k, k, Y, k);
   TG_LAUNCHED();
@@ -1764,9 +2010,13 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
   TG_HIP(tg::dgemm(st, false, false, k, n, k, 1.0, Y, k, Bm, n, 0.0, A, n));    // S^-1 R_x
   TG_HIP(tg::dgemm(st, true, false, k, n, k, 1.0, A, n, A, n, 0.0, U, ldu));    // G[:k, :]
   TG_HIP(chol_upper_rows(st, U, ldu, k, n, Wb, info));
-  hipLaunchKernelGGL(zero_lower_kernel, dim3(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k),
-                     dim3(256), 0, st, U, ldu, k);
-  TG_LAUNCHED();
+  TG_HIP(zero_lower(st, U, ldu, k));
+  TG_HIP(read_stat(st, rw.stats, info, h));
+  if (h.info > 0) {
+    tg::set_error("U factor (two-Cholesky form): Gram matrix not positive definite (%d pivots)",
+                  h.info);
+    return int(hipErrorUnknown);
+  }
   return 0;
 }
 

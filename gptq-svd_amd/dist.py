@@ -77,5 +77,14 @@ def quantize_rows_sharded(W: torch.Tensor, U: torch.Tensor, perm: torch.Tensor, 
             q = Quantizer(b, g, s)
             Wq, _ = gptq_fwrd(Wl, U_, q, perm_, block_size=bs)
             return Wq, q.codes
-    Wq, codes = fn(W[r0:r1], U, perm, w_bits, group_size, sym, block_size)
+    if r1 > r0:
+        Wq, codes = fn(W[r0:r1], U, perm, w_bits, group_size, sym, block_size)
+        # one dtype on every rank (an empty rank cannot ask fn): codes are < 2^8
+        Wq, codes = Wq.to(W.dtype), codes.to(torch.uint8)
+    else:
+        # m < world: this rank owns no rows (the solver rejects m = 0) but
+        # still joins both all_gathers, or the other ranks would block there
+        n = W.shape[1]
+        Wq = torch.empty((0, n), dtype=W.dtype, device=W.device)
+        codes = torch.empty((0, n), dtype=torch.uint8, device=W.device)
     return all_gather_rows(Wq, m, pg), all_gather_rows(codes, m, pg)

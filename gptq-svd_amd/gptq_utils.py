@@ -73,25 +73,29 @@ class HessianAccumulator:
 # ---------------------------------------------------------------------------
 # A2-A5  (gptq_utils.py:87-126)
 # ---------------------------------------------------------------------------
-def _complement_count(w_asc: torch.Tensor, k: int) -> Tuple[int, float]:
-    """Dropped eigenpairs above the rounding threshold n*eps*lambda_max, and
-    lambda_k (the smallest kept eigenvalue).  One 8n-byte copy; the caller
-    has already synchronised on k."""
+def _complement_count(w_asc: torch.Tensor, k: int) -> Tuple[int, float, bool]:
+    """Dropped eigenpairs above the rounding threshold tau = n*eps*lambda_max,
+    lambda_k (the smallest kept eigenvalue), and whether every dropped
+    eigenvalue is >= -tau (H positive semidefinite to rounding).  One 8n-byte
+    copy; the caller has already synchronised on k."""
     w = w_asc.double().cpu()
     n = w.numel()
     tau = n * 2.220446049250313e-16 * max(float(w[-1]), 0.0)
     dropped = w[:n - k]
-    return int((dropped > tau).sum()), float(w[n - k])
+    return int((dropped > tau).sum()), float(w[n - k]), bool(float(w[0]) >= -tau)
 
 
-def spectral_path(n: int, k: int, nc: int, lam_k: float) -> str:
+def spectral_path(n: int, k: int, nc: int, lam_k: float, psd: bool = True) -> str:
     """'complement' when the dropped eigenpairs that matter are fewer than
-    the kept ones (k > n/2 in practice) and no kept eigenvalue is clamped by
-    sqrt(max(L, 1e-12)) (gptq_utils.py:94); else 'kept'.  TG_SPECTRAL_PATH
-    = kept | complement forces one (complement only where it is exact)."""
+    the kept ones (k > n/2 in practice), no kept eigenvalue is clamped by
+    sqrt(max(L, 1e-12)) (gptq_utils.py:94) and no dropped eigenvalue is below
+    -tau (H_k = H - B_c^T B_c removes only the dropped eigenpairs above tau, so
+    a negative one would stay in H_k, unlike the reference's V_k L_k V_k^T);
+    else 'kept'.  TG_SPECTRAL_PATH = kept | complement forces one (complement
+    only where it is exact)."""
     import os
     force = os.environ.get("TG_SPECTRAL_PATH", "auto")
-    ok = lam_k >= 1e-12 and nc <= k and k + nc <= n
+    ok = lam_k >= 1e-12 and nc <= k and k + nc <= n and psd
     if force == "kept" or not ok:
         return "kept"
     if force == "complement":
@@ -132,8 +136,8 @@ def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
             raise RuntimeError("process_hessian_alt: truncation rank is 0 "
                                "(threshold keeps no eigenvalue)")
         del A
-        nc, lam_k = _complement_count(w, k)
-        path = spectral_path(n, k, nc, lam_k)
+        nc, lam_k, psd = _complement_count(w, k)
+        path = spectral_path(n, k, nc, lam_k, psd)
         perm = torch.empty(n, dtype=torch.int64, device=dev)
         R_x = torch.empty((k, n), dtype=torch.float64, device=dev)
         U = torch.empty((k, n), dtype=torch.float64, device=dev)

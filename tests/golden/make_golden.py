@@ -80,6 +80,48 @@ PIPELINE = [
     ("p_n1024_w4a_e4_b256", 1024, 64, 768, "gaussian", 4, 128, False, 1e-4, "energy", 256),
 ]
 
+# Hessians given by their spectrum, H = Q diag(lam) Q^T (Q Haar, float64):
+# graded / cliff spectra at energy eps 1e-7, where the smallest kept
+# eigenvalue is ~1e-7 lam_max and a Gram-matrix (CholeskyQR) U factor loses
+# ~cond^2 eps.  name, n, m, spectrum, bits, group, sym, eps, method, block_size
+SPECTRA = [
+    ("s_n512_w4a_graded_e7", 512, 64, "graded14", 4, 128, False, 1e-7, "energy", 1024),
+    ("s_n384_w3s_cliff_e7", 384, 48, "cliff", 3, 128, True, 1e-7, "energy", 1024),
+]
+
+
+def spectrum(kind, n, gen):
+    if kind == "graded14":   # 1 .. 1e-14, geometric
+        return torch.logspace(0, -14, n, dtype=torch.float64)
+    if kind == "cliff":      # half geometric 1 .. 1e-3, half ~1e-7
+        h = n // 2
+        lo = 1e-7 * (1.0 + 0.5 * torch.rand(n - h, generator=gen, dtype=torch.float64))
+        return torch.cat([torch.logspace(0, -3, h, dtype=torch.float64), lo])
+    raise ValueError(kind)
+
+
+def gen_spectrum(g, spec, seed):
+    name, n, m, kind, bits, group, sym, eps, method, bs = spec
+    gen = torch.Generator().manual_seed(seed)
+    Qm = torch.linalg.qr(torch.randn(n, n, generator=gen, dtype=torch.float64))[0]
+    lam = spectrum(kind, n, gen)
+    H = (Qm * lam) @ Qm.T
+    H = (H + H.T) / 2
+    R, R_x, perm = g.process_hessian_alt(H, threshold=eps, threshold_method=method)
+    W = torch.randn(m, n, generator=gen) * 0.05
+    q = g.Quantizer(w_bits=bits, group_size=group, sym=sym)
+    final_W, k = g.gptq_fwrd(W.clone(), R, q, perm, block_size=bs, use_triton=True, R_x=R_x)
+    L, _ = torch.linalg.eigh(H)
+    S = torch.sqrt(L.clamp(min=1e-12)).flip(0)
+    scale, zero = q.scale.squeeze(-1), q.zero.squeeze(-1)
+    return name, dict(
+        H=H.numpy(), S=S.numpy(), k=np.int64(k), perm=perm.numpy().astype(np.int64),
+        U=R.numpy(), Rx=R_x.numpy(), W=W.numpy(), final_W=final_W.numpy(),
+        scale=scale.numpy(), zero=zero.numpy(), bits=np.int64(bits), group=np.int64(group),
+        sym=np.bool_(sym), eps=np.float64(eps), method=np.str_(method),
+        block_size=np.int64(bs))
+
+
 # block-kernel fixtures: name, m, B, bits, sym
 BLOCKS = [
     ("b_m64_B64_w4a", 64, 64, 4, False),
@@ -200,6 +242,12 @@ def main():
         name, d = gen_gptq(g, spec, 3000 + i)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name)
+    for i, spec in enumerate(SPECTRA):
+        if only and spec[0] not in only:
+            continue
+        name, d = gen_spectrum(g, spec, 4000 + i)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+        print("wrote", name, "k =", int(d["k"]))
 
 
 if __name__ == "__main__":

@@ -72,3 +72,17 @@ def test_complement_path_matches_reference(oracle_mod, name):
     assert np.linalg.norm(U - U_ref) / np.linalg.norm(U_ref) < tol
     if "Rx" in d:
         assert np.linalg.norm(Rx - d["Rx"]) / np.linalg.norm(d["Rx"]) < 1e-8
+
+
+def test_complement_path_requires_psd():
+    """An indefinite H (a dropped eigenvalue below -tau) takes the kept path:
+    H_k = H - B_c^T B_c would keep that negative eigenpair."""
+    import torch
+    from gptq_svd_amd.gptq_utils import _complement_count, spectral_path
+    w = torch.tensor([-1e-3, 1e-14, 0.3, 0.5, 1.0, 2.0], dtype=torch.float64)  # ascending
+    nc, lam_k, psd = _complement_count(w, 4)
+    assert (nc, psd) == (1, False) and lam_k == 0.3
+    assert spectral_path(6, 4, nc, lam_k, psd) == "kept"
+    w[0] = -1e-16  # negative at rounding level only: still PSD to rounding
+    nc, lam_k, psd = _complement_count(w, 4)
+    assert psd and spectral_path(6, 4, nc, lam_k, psd) == "complement"

@@ -34,6 +34,7 @@ def _oracle_fn():
 
 
 def _worker(rank, world, port, W, U, perm, out):
+    torch.set_num_threads(1)
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -50,10 +51,11 @@ def _worker(rank, world, port, W, U, perm, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_row_sharded_matches_single(oracle_mod, world):
+@pytest.mark.parametrize("world,m", [(2, 37), (3, 2)])
+def test_row_sharded_matches_single(oracle_mod, world, m):
+    """m < world included: a rank without rows still joins the gathers."""
     rng = np.random.default_rng(3)
-    m, n, k = 37, 512, 480
+    n, k = 512, 480
     W = (rng.standard_normal((m, n)) * 0.05).astype(np.float32)
     U = np.triu(rng.standard_normal((k, n)) * 0.02)
     U[np.arange(k), np.arange(k)] = 1.0 + np.abs(rng.standard_normal(k))

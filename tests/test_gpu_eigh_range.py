@@ -63,3 +63,44 @@ def test_few_vectors(n, first, count, kind):
                 gaps[first + j] if first + j < n - 1 else np.inf)
         if g > 1e-6 * nrm:
             assert abs(abs(Vh[j] @ Qd[j]) - 1.0) <= 1e-8
+
+
+def _spectrum(n, kind, seed):
+    rng = np.random.default_rng(seed)
+    Q = np.linalg.qr(rng.standard_normal((n, n)))[0]
+    if kind == "graded":        # 1e-10 .. 1: the bottom ~60% forms one ortol cluster
+        lam = np.logspace(-10, 0, n)
+    elif kind == "clustered":   # four 64-fold near-multiple eigenvalues + a dense rest
+        lam = np.linspace(0.1, 1.0, n)
+        for c, v in enumerate((0.2, 0.45, 0.7, 0.95)):
+            lam[c * 64:(c + 1) * 64] = v * (1 + 1e-12 * rng.standard_normal(64))
+        lam.sort()
+    else:
+        raise ValueError(kind)
+    return (Q * lam) @ Q.T
+
+
+@pytest.mark.parametrize("kind,first,count", [("graded", 0, 4096), ("clustered", 0, 4096),
+                                              ("graded", 1200, 600), ("clustered", 3000, 400)])
+def test_orthogonality_n4096(kind, first, count):
+    """Eigenvectors at n = 4096 with graded / clustered spectra: inverse
+    iteration + cluster re-orthogonalisation (ortol 1e-6 ||T||, block
+    Gram-Schmidt for big clusters) keeps them orthogonal to <= 1e-9."""
+    from gptq_svd_amd import _lib as lib
+    n = 4096
+    H = _spectrum(n, kind, 11 + first)
+    A = torch.from_numpy(H).to(DEV)
+    Hd = A.clone()
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+    w = torch.empty(n, dtype=torch.float64, device=DEV)
+    lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws), ws.numel())
+    V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+    lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), first, count, lib.ptr(V), n,
+             lib.ptr(ws), ws.numel())
+    lam = torch.flip(w, [0])[first:first + count]
+    nrm = float(w.abs().max())
+    resid = float(torch.linalg.norm(V @ Hd - lam[:, None] * V, dim=1).max())
+    orth = float((V @ V.T - torch.eye(count, dtype=torch.float64, device=DEV)).abs().max())
+    print(f"{kind} n={n} [{first}, {first + count}): resid {resid / nrm:.2e} ||H||, orth {orth:.2e}")
+    assert resid <= 1e-10 * nrm
+    assert orth <= 1e-9

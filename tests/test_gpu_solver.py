@@ -189,3 +189,24 @@ def test_end_to_end_golden(g, name, path, monkeypatch):
     mism = float(np.mean(Wq.cpu().numpy() != d["final_W"]))
     print(f"{name}: code mismatch vs reference {mism:.2e}")
     assert mism <= 2e-3
+
+
+def test_bulge_stall_reported(lib, monkeypatch):
+    """A bulge-chasing hand-off that times out (forced: timeout of 0 ticks)
+    is an error of tg_eigh_values, with NaN-poisoned eigenvalues, not a
+    silently wrong tridiagonal form; the next call is clean again."""
+    H = eig_problem("wishart", 1024, 3)
+    n = H.shape[0]
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), DEV)
+    w = torch.empty(n, dtype=torch.float64, device=DEV)
+    monkeypatch.setenv("TG_BULGE_TIMEOUT_TICKS", "0")
+    A = t(H).clone()
+    with pytest.raises(RuntimeError, match="stalled"):
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+    torch.cuda.synchronize()
+    monkeypatch.delenv("TG_BULGE_TIMEOUT_TICKS")
+    A = t(H).clone()
+    lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws), ws.numel())
+    L = np.linalg.eigvalsh(H)
+    assert np.max(np.abs(w.cpu().numpy() - L)) <= 1e-12 * np.abs(L).max() * 4

@@ -41,7 +41,7 @@ def test_hessian(oracle_mod, name):
     assert np.allclose(H, H.T)
 
 
-@pytest.mark.parametrize("name", golden_names("p_"))
+@pytest.mark.parametrize("name", golden_names("p_") + golden_names("s_"))
 def test_spectral_factor(oracle_mod, name):
     d = load_golden(name)
     H = d["H"] if "H" in d else hessian_of(oracle_mod, d)
@@ -49,21 +49,25 @@ def test_spectral_factor(oracle_mod, name):
     assert f.k == int(d["k"])
     assert np.array_equal(f.perm, d["perm"])
     U_ref = d["U"] if "U" in d else d["U32"]
-    tol = 1e-10 if "U" in d else 1e-6
+    # s_ fixtures keep eigenvalues ~1e-7 lam_max with gaps ~1e-10: their
+    # eigenvectors (hence U, R_x) are determined only to ~eps ||H|| / gap
+    # by any LAPACK, the reference's included
+    tol = 1e-6 if name.startswith("s_") else 1e-10 if "U" in d else 1e-6
     assert rel_fro(f.U, U_ref) < tol
     if "Rx" in d:
-        assert rel_fro(f.R_x, d["Rx"]) < 1e-10
-    assert rel_fro(f.S, d["S"]) < 1e-12
+        assert rel_fro(f.R_x, d["Rx"]) < (1e-6 if name.startswith("s_") else 1e-10)
+    # S of eigenvalues at rounding level (1e-14 lam_max) carries eps ||H|| noise
+    assert rel_fro(f.S, d["S"]) < (1e-10 if name.startswith("s_") else 1e-12)
 
 
-@pytest.mark.parametrize("name", golden_names("p_"))
+@pytest.mark.parametrize("name", golden_names("p_") + golden_names("s_"))
 def test_find_params_bitexact(oracle_mod, name):
     d = load_golden(name)
     s, z = oracle_mod.find_params(d["W"], int(d["bits"]), int(d["group"]), bool(d["sym"]))
     assert np.array_equal(s, d["scale"]) and np.array_equal(z, d["zero"])
 
 
-@pytest.mark.parametrize("name", golden_names("p_"))
+@pytest.mark.parametrize("name", golden_names("p_") + golden_names("s_"))
 @pytest.mark.parametrize("impl", ["numpy-torch", "numpy-fma", "c"])
 def test_gptq_fwrd(oracle_mod, name, impl):
     """Given the reference's own U and perm: single-block (k == n) configs are
