@@ -119,8 +119,9 @@ def phases(g, H, W, args):
     call("tg_truncation_rank", stream(), ptr(w), n, args.eps, 1, ptr(S), ptr(kd))
     k = int(kd.item())
     t = tick("rank", t)
-    nc, lam_k, psd = g._complement_count(w, k)
-    path = g.spectral_path(n, k, nc, lam_k, psd)
+    sp = g._complement_count(w, k)
+    nc = sp.nc
+    path = g.spectral_path(n, k, sp)
     phases.path = f"{path} (nc={nc})"
     t = time.perf_counter()
     perm = torch.empty(n, dtype=torch.int64, device=dev)

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 
@@ -73,34 +73,46 @@ class HessianAccumulator:
 # ---------------------------------------------------------------------------
 # A2-A5  (gptq_utils.py:87-126)
 # ---------------------------------------------------------------------------
-def _complement_count(w_asc: torch.Tensor, k: int) -> Tuple[int, float, bool]:
-    """Dropped eigenpairs above the rounding threshold tau = n*eps*lambda_max,
-    lambda_k (the smallest kept eigenvalue), and whether every dropped
-    eigenvalue is >= -tau (H positive semidefinite to rounding).  One 8n-byte
-    copy; the caller has already synchronised on k."""
+class SpectrumSplit(NamedTuple):
+    """What the complement path needs to know about the dropped spectrum."""
+    nc: int          # dropped eigenvalues above the rounding threshold tau = n*eps*lambda_max
+    lam_k: float     # smallest kept eigenvalue
+    psd: bool        # every dropped eigenvalue >= -tau
+    left: float      # max |lambda| of the dropped eigenvalues at or below tau
+
+
+def _complement_count(w_asc: torch.Tensor, k: int) -> SpectrumSplit:
+    """One 8n-byte copy of the eigenvalues; the caller has already
+    synchronised on k."""
     w = w_asc.double().cpu()
     n = w.numel()
     tau = n * 2.220446049250313e-16 * max(float(w[-1]), 0.0)
     dropped = w[:n - k]
-    return int((dropped > tau).sum()), float(w[n - k]), bool(float(w[0]) >= -tau)
+    low = dropped[dropped <= tau]
+    return SpectrumSplit(int((dropped > tau).sum()), float(w[n - k]),
+                         bool(float(w[0]) >= -tau),
+                         float(low.abs().max()) if low.numel() else 0.0)
 
 
-def spectral_path(n: int, k: int, nc: int, lam_k: float, psd: bool = True) -> str:
+def spectral_path(n: int, k: int, sp: SpectrumSplit) -> str:
     """'complement' when the dropped eigenpairs that matter are fewer than
-    the kept ones (k > n/2 in practice), no kept eigenvalue is clamped by
-    sqrt(max(L, 1e-12)) (gptq_utils.py:94) and no dropped eigenvalue is below
-    -tau (H_k = H - B_c^T B_c removes only the dropped eigenpairs above tau, so
-    a negative one would stay in H_k, unlike the reference's V_k L_k V_k^T);
-    else 'kept'.  TG_SPECTRAL_PATH = kept | complement forces one (complement
-    only where it is exact)."""
+    the kept ones (k > n/2 in practice) and the complement form is exact to
+    ~1e-9: no kept eigenvalue is clamped by sqrt(max(L, 1e-12))
+    (gptq_utils.py:94); no dropped eigenvalue is below -tau; and the dropped
+    eigenvalues H_k = H - B_c^T B_c keeps (those at or below tau) are below
+    1e-9 lambda_k, since they perturb the pseudo-inverse by ~left / lambda_k
+    (graded spectra reaching down to rounding level fail this, the kept path
+    is exact for them).  Else 'kept'.  TG_SPECTRAL_PATH = kept | complement
+    forces one (complement only where it is defined)."""
     import os
     force = os.environ.get("TG_SPECTRAL_PATH", "auto")
-    ok = lam_k >= 1e-12 and nc <= k and k + nc <= n and psd
-    if force == "kept" or not ok:
+    defined = sp.lam_k >= 1e-12 and sp.nc <= k and k + sp.nc <= n and sp.psd
+    if force == "kept" or not defined:
         return "kept"
     if force == "complement":
         return "complement"
-    return "complement" if nc < k else "kept"
+    exact = sp.left <= 1e-9 * sp.lam_k
+    return "complement" if sp.nc < k and exact else "kept"
 
 
 def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
@@ -136,8 +148,9 @@ def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
             raise RuntimeError("process_hessian_alt: truncation rank is 0 "
                                "(threshold keeps no eigenvalue)")
         del A
-        nc, lam_k, psd = _complement_count(w, k)
-        path = spectral_path(n, k, nc, lam_k, psd)
+        sp = _complement_count(w, k)
+        nc = sp.nc
+        path = spectral_path(n, k, sp)
         perm = torch.empty(n, dtype=torch.int64, device=dev)
         R_x = torch.empty((k, n), dtype=torch.float64, device=dev)
         U = torch.empty((k, n), dtype=torch.float64, device=dev)

@@ -80,9 +80,25 @@ def test_complement_path_requires_psd():
     import torch
     from gptq_svd_amd.gptq_utils import _complement_count, spectral_path
     w = torch.tensor([-1e-3, 1e-14, 0.3, 0.5, 1.0, 2.0], dtype=torch.float64)  # ascending
-    nc, lam_k, psd = _complement_count(w, 4)
-    assert (nc, psd) == (1, False) and lam_k == 0.3
-    assert spectral_path(6, 4, nc, lam_k, psd) == "kept"
+    sp = _complement_count(w, 4)
+    assert (sp.nc, sp.psd, sp.lam_k) == (1, False, 0.3)
+    assert spectral_path(6, 4, sp) == "kept"
     w[0] = -1e-16  # negative at rounding level only: still PSD to rounding
-    nc, lam_k, psd = _complement_count(w, 4)
-    assert psd and spectral_path(6, 4, nc, lam_k, psd) == "complement"
+    sp = _complement_count(w, 4)
+    assert sp.psd and sp.left == 1e-16 and spectral_path(6, 4, sp) == "complement"
+
+
+def test_complement_path_requires_small_leftover():
+    """Dropped eigenvalues at or below tau stay in H_k; when they are not
+    negligible against lambda_k (graded spectra down to rounding level) the
+    kept path is taken."""
+    import torch
+    from gptq_svd_amd.gptq_utils import _complement_count, spectral_path
+    n = 8
+    w = torch.tensor([1e-17, 2e-16, 1e-3, 0.2, 0.4, 0.6, 0.8, 1.0], dtype=torch.float64)
+    sp = _complement_count(w, 6)            # tau = 8 eps ~ 1.8e-15
+    assert sp.nc == 0 and sp.left == 2e-16
+    assert spectral_path(n, 6, sp) == "complement"      # 2e-16 <= 1e-9 * 1e-3
+    w[2] = 1e-7                              # lambda_k = 1e-7: 2e-16 > 1e-16
+    sp = _complement_count(w, 6)
+    assert spectral_path(n, 6, sp) == "kept"
