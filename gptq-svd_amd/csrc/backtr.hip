@@ -1,0 +1,583 @@
+// Back-transformation Z <- Q1 Q2 Z for few eigenvectors (k <= 32 columns) in
+// ONE persistent launch.
+//
+// Second half of `torch.linalg.eigh` (/root/reference/src/TruncGPTQ/
+// gptq_utils.py:93) for the complement path's ~14 dropped eigenvectors.
+// The multi-launch path (sb_apply_q2: one launch per Q2 level, 255 at
+// n = 4096; sb_apply_q1: one launch per TSQR level of every panel, ~240) is
+// launch- and latency-bound for k this small (~8 ms for 14 columns against
+// ~30 us of reflector traffic).  Here one grid of W workgroups (8 waves each)
+// walks the same ~500 steps with an in-kernel grid barrier between steps:
+//   Q2 level L: blocks (G2, s) with s + (NG2 - 1 - G2) = L, one wave per block
+//               (63 x 32 staircase Y, Z -= Y (T (Y^T Z)) on FP64 MFMA);
+//   Q1 step (panel p, level l), panels last to first, levels top down: one
+//               workgroup per TSQR chunk (<= 512 rows, 8 waves x 64 rows).
+// Hand-off between steps (cdna_hip_programming.md Guideline 16, counter
+// form): Z is stored write-through (sc1, 8-B relaxed agent-scope stores),
+// every wave drains vmcnt, one lane adds to the step counter, polls it
+// relaxed (bounded spin; a timeout sets a flag the host reads), then ONE
+// agent-scope acquire before the next step's plain loads.  Reflectors (Y, T,
+// V2, T2) are written by earlier launches and read plainly.
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "band.h"
+#include "common.h"
+
+namespace {
+
+using tg::SB_B;
+using tg::SB_C;
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int QB = 32;             // sweeps per Q2 block (= SB_B)
+constexpr int QR = QB + SB_B - 1;  // rows per Q2 block (63)
+constexpr int BW = 8;              // waves per workgroup
+
+struct Q1Op {
+  int r0, rows, nc, lv, yoff, toff;  // Z row offset, stacked rows, chunks, level, Y/T offsets
+};
+
+struct BtArgs {
+  double *Z;
+  int n, k;
+  const double *V2, *T2;  // Q2 reflectors / block T factors
+  int smax, ng2, nlev2;
+  const double *Y, *T;    // Q1 (TSQR) reflectors / T factors
+  const Q1Op *ops;
+  int nops;
+  unsigned *cnt;          // [0] step counter, [1] timeout flag (zeroed per call)
+  unsigned long long timeout;
+};
+
+struct SmQ2 {
+  double Vs[BW][QB][SB_B + 1];
+  double Ts[BW][QB][QB + 1];
+};
+struct SmQ1 {
+  double red[BW][SB_B][SB_B + 1];
+  double Ps[SB_B][SB_B + 1];
+  double Ms[SB_B][SB_B + 1];
+};
+union BtShared {
+  SmQ2 q2;
+  SmQ1 q1;
+};
+
+__device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) / SB_B + 1 : 0; }
+__device__ inline bool refl_valid(int n, int j, int s) { return j <= n - 3 && s < ntasks(n, j); }
+
+// TG_BT_XCD=1: the workers are the workgroups that landed on the first XCD
+// to arrive (the rest exit), so Z hand-offs stay in that XCD's L2: plain
+// stores drained by vmcnt, relaxed L2 counter, sc1 (L1-bypassing) Z loads,
+// no release/acquire fences.  TG_BT_XCD=0: placement-independent form
+// (write-through Z stores, agent-scope acquire after every barrier).
+#ifndef TG_BT_XCD
+#define TG_BT_XCD 1
+#endif
+
+__device__ inline void store_sc1(double *p, double v) {
+#if TG_BT_XCD
+  *p = v;
+#else
+  __hip_atomic_store((gu64 *)(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+// Z element e (row-major index) as last stored by any worker of this launch
+__device__ inline double load_z(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, int64_t e) {
+#if TG_BT_XCD
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rz, int(e * 8), 0, 16);  // sc1
+  return __builtin_bit_cast(double, v);
+#else
+  return a.Z[e];
+#endif
+}
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Step done by this workgroup; wait for all workers.
+__device__ inline void grid_barrier(const BtArgs &a, unsigned target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Z stores drained
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gu32 *c = (gu32 *)(a.cnt);
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+        __hip_atomic_store((gu32 *)(a.cnt + 1), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+#if !TG_BT_XCD
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  }
+  __syncthreads();
+}
+
+// Reflector data of one Q2 block in registers (issued before the barrier
+// that precedes its use, so its HBM latency overlaps the hand-off).
+struct Q2Pre {
+  double vv[16], tt[16];
+};
+__device__ inline void q2_fetch(const BtArgs &a, int G2, int s, Q2Pre &p) {
+  const int lane = threadIdx.x & 63, j0 = G2 * QB;
+  const double *Tb = a.T2 + (int64_t(G2) * a.smax + s) * QB * QB;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = lane + 64 * q, r = idx >> 5, d = idx & 31;
+    const int jj = refl_valid(a.n, j0 + r, s) ? j0 + r : j0;
+    p.vv[q] = a.V2[(int64_t(jj) * a.smax + s) * SB_B + d];
+    p.tt[q] = Tb[idx];
+  }
+}
+
+// One Q2 block (G2, s) by one wave: Z[rb0 .. rb0 + 62, 0 .. k) -= Y (T (Y^T Z)),
+// NCB 16-column blocks of Z (k <= 16 NCB).
+template <int NCB>
+__device__ void q2_block(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, int G2, int s,
+                         const Q2Pre &pre, double (*Vs)[SB_B + 1], double (*Ts)[QB + 1]) {
+  const int n = a.n, k = a.k, lane = threadIdx.x & 63;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int j0 = G2 * QB;
+  const int rb0 = j0 + 1 + s * SB_B;
+  // Z tile first (its latency overlaps the LDS staging of V and T)
+  double zl[4][4][NCB];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int row = min(rb0 + rb * 16 + lr + 4 * q, n - 1);
+        const int col = min(cb * 16 + lc, k - 1);
+        zl[rb][q][cb] = load_z(a, rz, int64_t(row) * k + col);
+      }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = lane + 64 * q, r = idx >> 5, d = idx & 31;
+    Vs[r][d] = refl_valid(n, j0 + r, s) ? pre.vv[q] : 0.0;
+    Ts[r][d] = pre.tt[q];
+  }
+  wave_sync();
+  auto yval = [&](int i, int c) -> double {
+    const int d = i - c;
+    return (d >= 0 && d < SB_B) ? Vs[c][d] : 0.0;
+  };
+  doublex4 F[4][NCB];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = rb * 16 + lr + 4 * q;
+      const bool ok = i < QR && rb0 + i < n;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb][q] = (ok && cb * 16 + lc < k) ? zl[rb][q][cb] : 0.0;
+    }
+  doublex4 Pa[2][NCB];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = rb * 16 + 4 * q + lr;
+      double ya[2];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ya[ia] = yval(i, ia * 16 + lc);
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][q], Pa[ia][cb], 0, 0, 0);
+    }
+  doublex4 Ma[2][NCB];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) Ma[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = kb * 16 + 4 * q + lr;
+      double ta[2];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ta[ia] = Ts[ia * 16 + lc][kk];
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          Ma[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ta[ia], Pa[kb][cb][q], Ma[ia][cb], 0, 0, 0);
+    }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = kb * 16 + 4 * q + lr;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const double ya = -yval(rb * 16 + lc, kk);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][q], F[rb][cb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = rb * 16 + lr + 4 * q;
+      const int row = rb0 + i;
+      if (i >= QR || row >= n) continue;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + lc;
+        if (col < k) store_sc1(&a.Z[int64_t(row) * k + col], F[rb][cb][q]);
+      }
+    }
+  wave_sync();  // Vs / Ts reused by this wave's next block
+}
+
+// Stacked row s of TSQR level lv -> level-0 row (band.hip RowMap::fwd).
+__device__ inline int fwd_row(int lv, int s) {
+  for (int l = lv; l >= 1; --l) s = (s / SB_B) * SB_C + s % SB_B;
+  return s;
+}
+
+// Reflector data of one Q1 chunk for this wave: Y rows of the P = Y^T Z
+// product in MFMA A-operand order, and this thread's two entries of T.
+struct Q1Pre {
+  double ya[4][4][2];
+  double t[2];
+};
+__device__ inline void q1_fetch(const BtArgs &a, const Q1Op &d, int I, Q1Pre &p) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  const int kb = I * SB_C, ke = (I == d.nc - 1) ? d.rows : kb + SB_C, h = ke - kb;
+  const double *Y = a.Y + d.yoff;
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + 4 * q + lr;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) p.ya[rb][q][ia] = Y[int64_t(kb + min(rl, h - 1)) * SB_B + ia * 16 + lc];
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) p.t[t] = a.T[d.toff + size_t(I) * SB_B * SB_B + tid + 64 * BW * t];
+}
+
+// One Q1 chunk I of step d by the workgroup: Z_c -= Y (T (Y^T Z_c)), wave w
+// owns chunk rows 64w .. 64w + 63.
+template <int NCB>
+__device__ void q1_chunk(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
+                         const Q1Pre &pre, SmQ1 &sm) {
+  const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int kb = I * SB_C, ke = (I == d.nc - 1) ? d.rows : kb + SB_C, h = ke - kb;
+  const double *Y = a.Y + d.yoff;
+  double *Zs = a.Z + int64_t(d.r0) * k;
+  doublex4 F[4][NCB];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      const int zr = fwd_row(d.lv, kb + min(rl, h - 1));
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb][q] = load_z(a, rz, int64_t(d.r0 + zr) * k + min(cb * 16 + lc, k - 1));
+    }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb][q] = (rl < h && cb * 16 + lc < k) ? F[rb][cb][q] : 0.0;
+    }
+  doublex4 Pa[2][NCB];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + 4 * q + lr;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) {
+        const double ya = rl < h ? pre.ya[rb][q][ia] : 0.0;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, F[rb][cb][q], Pa[ia][cb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm.red[wid][ia * 16 + lr + 4 * q][cb * 16 + lc] = Pa[ia][cb][q];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int idx = tid + 64 * BW * t;
+    sm.Ms[idx >> 5][idx & 31] = pre.t[t];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < SB_B * SB_B; idx += 64 * BW) {
+    const int r = idx >> 5, cc = idx & 31;
+    if (cc >= 16 * NCB) continue;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < BW; ++w) v += sm.red[w][r][cc];
+    sm.Ps[r][cc] = v;
+  }
+  __syncthreads();
+  double mval[2] = {0.0, 0.0};
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) {
+    const int r = idx >> 5, cc = idx & 31;
+    if (cc >= 16 * NCB) continue;
+    double v = 0.0;
+    for (int e = r; e < SB_B; ++e) v += sm.Ms[r][e] * sm.Ps[e][cc];
+    mval[t] = v;
+  }
+  __syncthreads();  // T no longer read: Ms <- T P
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) sm.Ms[idx >> 5][idx & 31] = mval[t];
+  __syncthreads();
+#pragma unroll
+  for (int k0 = 0; k0 < SB_B; k0 += 4) {
+    double bm[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) bm[cb] = sm.Ms[k0 + lr][cb * 16 + lc];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int rl = wid * 64 + rb * 16 + lc;
+      const double yl = Y[int64_t(kb + min(rl, h - 1)) * SB_B + k0 + lr];
+      const double ya = rl < h ? -yl : 0.0;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm[cb], F[rb][cb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      if (rl >= h) continue;
+      const int zr = fwd_row(d.lv, kb + rl);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + lc;
+        if (col < k) store_sc1(&Zs[int64_t(zr) * k + col], F[rb][cb][q]);
+      }
+    }
+  __syncthreads();  // red / Ps / Ms reused by the next chunk
+}
+
+template <int NCB>
+__global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
+  __shared__ BtShared sm;
+  __shared__ int sh_w[2];
+  const int wid = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t rz =
+      __builtin_amdgcn_make_buffer_rsrc(a.Z, 0, int(int64_t(a.n) * a.k * 8), 0x00020000);
+#if TG_BT_XCD
+  // workers: the workgroups on the first XCD to arrive; cnt[2] = XCD + 1,
+  // cnt[3] = worker tickets, cnt[4] = workgroups checked in (all of them)
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned expect = 0;
+    __hip_atomic_compare_exchange_strong((gu32 *)(a.cnt + 2), &expect, x + 1, __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool mine = (expect == 0 ? x + 1 : expect) == x + 1;
+    sh_w[0] = mine ? int(__hip_atomic_fetch_add((gu32 *)(a.cnt + 3), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT))
+                   : -1;
+    __hip_atomic_fetch_add((gu32 *)(a.cnt + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mine) {  // worker count is known once every workgroup has checked in
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load((gu32 *)(a.cnt + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             gridDim.x) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+          __hip_atomic_store((gu32 *)(a.cnt + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      sh_w[1] = int(__hip_atomic_load((gu32 *)(a.cnt + 3), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT));
+    }
+  }
+  __syncthreads();
+  if (sh_w[0] < 0) return;
+  const int W = sh_w[1], me = sh_w[0];
+#else
+  const int W = gridDim.x, me = blockIdx.x;
+#endif
+  unsigned step = 0;
+#ifdef TG_BT_STATS
+  uint64_t st_q2 = 0, st_b2 = 0, st_q1 = 0, st_b1 = 0;
+#define BT_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime();
+#else
+#define BT_T(v)
+#endif
+  // the wave's first block of level L (t index), -1 if none
+  auto q2_first = [&](int L, int &G2, int &s) {
+    const int s_lo = max(0, L - (a.ng2 - 1)), s_hi = min(a.smax - 1, L);
+    for (int t = me * BW + wid; t <= s_hi - s_lo; t += W * BW) {
+      s = s_lo + t;
+      G2 = a.ng2 - 1 - (L - s);
+      if (G2 >= 0 && refl_valid(a.n, G2 * QB, s)) return true;
+    }
+    return false;
+  };
+  Q2Pre p2;
+  int nG2 = 0, ns = 0;
+  bool have = a.nlev2 > 0 && q2_first(0, nG2, ns);
+  if (have) q2_fetch(a, nG2, ns, p2);
+  for (int L = 0; L < a.nlev2; ++L) {
+    BT_T(t0)
+    const int s_lo = max(0, L - (a.ng2 - 1)), s_hi = min(a.smax - 1, L);
+    bool first = true;
+    for (int t = me * BW + wid; t <= s_hi - s_lo; t += W * BW) {
+      const int s = s_lo + t, G2 = a.ng2 - 1 - (L - s);
+      if (G2 < 0 || !refl_valid(a.n, G2 * QB, s)) continue;
+      if (!first) q2_fetch(a, G2, s, p2);  // more blocks than waves: no look-ahead
+      first = false;
+      q2_block<NCB>(a, rz, G2, s, p2, sm.q2.Vs[wid], sm.q2.Ts[wid]);
+    }
+    // next level's first block: its reflectors load across the barrier
+    if (L + 1 < a.nlev2 && q2_first(L + 1, nG2, ns)) q2_fetch(a, nG2, ns, p2);
+    BT_T(t1)
+    grid_barrier(a, unsigned(W) * ++step);
+    BT_T(t2)
+#ifdef TG_BT_STATS
+    st_q2 += t1 - t0;
+    st_b2 += t2 - t1;
+#endif
+  }
+  Q1Pre p1;
+  if (a.nops > 0 && me < a.ops[0].nc) q1_fetch(a, a.ops[0], me, p1);
+  for (int o = 0; o < a.nops; ++o) {
+    BT_T(t0)
+    const Q1Op d = a.ops[o];
+    for (int I = me; I < d.nc; I += W) {
+      if (I != me) q1_fetch(a, d, I, p1);
+      q1_chunk<NCB>(a, rz, d, I, p1, sm.q1);
+    }
+    if (o + 1 < a.nops) {
+      const Q1Op dn = a.ops[o + 1];
+      if (me < dn.nc) q1_fetch(a, dn, me, p1);
+    }
+    BT_T(t1)
+    if (o + 1 < a.nops) grid_barrier(a, unsigned(W) * ++step);
+    BT_T(t2)
+#ifdef TG_BT_STATS
+    st_q1 += t1 - t0;
+    st_b1 += t2 - t1;
+#endif
+  }
+#ifdef TG_BT_STATS
+  if (me == 0 && threadIdx.x == 0) {
+    unsigned long long *o = reinterpret_cast<unsigned long long *>(a.cnt + 8);
+    o[0] = st_q2; o[1] = st_b2; o[2] = st_q1; o[3] = st_b1;
+  }
+#endif
+}
+
+}  // namespace
+
+namespace tg {
+
+int sb_smax(int n);
+
+// ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + 64 bytes of
+// device scratch (step counter + timeout flag first).
+size_t sb_apply_few_scratch(const SbPlan &pl) {
+  size_t c = 0;
+  for (const SbPanel &P : pl.panels) c += size_t(P.nl);
+  return 64 + c * sizeof(Q1Op);
+}
+
+hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
+                        const SbBufs &b, void *dev, bool *timed_out) {
+  *timed_out = false;
+  if (k < 1 || k > 32) return hipErrorInvalidValue;
+  std::vector<Q1Op> ops;
+  for (auto it = pl.panels.rbegin(); it != pl.panels.rend(); ++it)
+    for (int l = it->nl - 1; l >= 0; --l) {
+      const SbLevel &L = it->L[l];
+      ops.push_back(Q1Op{it->r0, L.rows, L.nc, l, int(L.yoff), int(L.toff)});
+    }
+  unsigned *cnt = static_cast<unsigned *>(dev);
+  Q1Op *dops = reinterpret_cast<Q1Op *>(static_cast<char *>(dev) + 64);
+  hipError_t e = hipMemsetAsync(cnt, 0, 64, st);
+  if (e != hipSuccess) return e;
+  if (!ops.empty()) {
+    e = hipMemcpyAsync(dops, ops.data(), ops.size() * sizeof(Q1Op), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  const int nsw = n - 2;
+  BtArgs a{};
+  a.Z = Z;
+  a.n = n;
+  a.k = k;
+  a.V2 = b.V2;
+  a.T2 = b.T2;
+  a.smax = sb_smax(n);
+  a.ng2 = nsw > 0 ? cdiv(nsw, QB) : 0;
+  a.nlev2 = nsw > 0 ? a.smax + a.ng2 - 1 : 0;
+  a.Y = b.Y;
+  a.T = b.T;
+  a.ops = dops;
+  a.nops = int(ops.size());
+  a.cnt = cnt;
+  const char *tt = getenv("TG_BT_TIMEOUT_TICKS");
+  a.timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
+  // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
+  const int W = std::min(256, std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax));
+  auto tok = prof_begin(st, PROF_Q2, 0.0, 0.0);
+  const int grid = TG_BT_XCD ? 8 * W : W;  // XCD form: ~W land on each XCD
+  if (k <= 16)
+    hipLaunchKernelGGL(bt_few_kernel<1>, dim3(grid), dim3(64 * BW), 0, st, a);
+  else
+    hipLaunchKernelGGL(bt_few_kernel<2>, dim3(grid), dim3(64 * BW), 0, st, a);
+  prof_end(st, tok);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  unsigned h[24] = {0};
+  e = hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);  // also: ops read before it goes
+  *timed_out = h[1] != 0u;
+#ifdef TG_BT_STATS
+  const unsigned long long *q = reinterpret_cast<const unsigned long long *>(h + 8);
+  fprintf(stderr, "bt_few: W %u  Q2 work %.3f ms barrier %.3f ms (%d levels)  Q1 work %.3f ms "
+          "barrier %.3f ms (%d steps)\n", h[3], q[0] / 1e5, q[1] / 1e5, a.nlev2, q[2] / 1e5,
+          q[3] / 1e5, a.nops);
+#endif
+  return e;
+}
+
+}  // namespace tg

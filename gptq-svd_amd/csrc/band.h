@@ -95,6 +95,14 @@ hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stal
 // Z (n x k row-major) <- Q2 Z.
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
                        const double *tau2, double *T2);
+// Q2 block T factors only (T2), for sb_apply_few.
+hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, const double *tau2, double *T2);
+// Z (n x k row-major, k <= 32) <- Q1 Q2 Z in one persistent launch (backtr.hip);
+// T2 must hold the Q2 T factors; dev: sb_apply_few_scratch bytes of device
+// scratch.  Syncs the stream (reads the barrier timeout flag).
+size_t sb_apply_few_scratch(const SbPlan &pl);
+hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
+                        const SbBufs &b, void *dev, bool *timed_out);
 // Z (n x k row-major) <- Q1 Z.
 hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                        const SbBufs &b);

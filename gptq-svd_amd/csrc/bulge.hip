@@ -89,6 +89,16 @@ constexpr int LAG = 2;               // pipeline lag between consecutive sweeps 
 constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
 constexpr int NCW = 3 * G_SW;        // compute waves (three per sweep: left, diagonal, lower block)
 constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
+// TG_BULGE_WDEFER: the writer publishes step t-1 at step t (its stores had a
+// step to drain) instead of waiting for step t's stores inside step t.
+// TG_BULGE_PF2: the loader issues the global loads of step t+2's columns at
+// step t (registers), and stores them to LDS at step t+1 (same ring timing).
+#ifndef TG_BULGE_WDEFER
+#define TG_BULGE_WDEFER 0
+#endif
+#ifndef TG_BULGE_PF2
+#define TG_BULGE_PF2 0
+#endif
 
 struct WaveScratch {
   double ws[SB_B];
@@ -462,6 +472,48 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     if (wid == 2) first_refl(R, n, j0, rfl[0][0]);
     __syncthreads();
     const int wlane = tid & 63;
+    constexpr int PW = SB_B * nthr_col_c / 64;  // 16-B chunks per loader lane per step
+#if TG_BULGE_PF2
+    // loader prefetch: pb holds the columns [pf_lo, pf_hi) loaded one step early
+    double2 pb[PW];
+    int pf_lo = ld, pf_hi = ld;
+    auto poll = [&](int need) {
+      if (G > 0 && known < need) {
+        if (wlane == 0) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 unsigned(need)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
+              __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        known = need;
+        __builtin_amdgcn_wave_barrier();
+      }
+    };
+    auto issue_pf = [&](int lo, int hi) {  // columns [lo, hi), hi - lo <= SB_B
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int idx = wlane + 64 * u;
+        const int c = min(lo + idx / nthr_col, hi - 1), h = idx % nthr_col;
+        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
+        pb[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                             __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+      }
+      pf_lo = lo;
+      pf_hi = hi;
+    };
+    if (wid == NCW + 1 && 1 < total) {
+      const int nh = group_high(n, j0, 1);
+      if (nh > ld) {
+        poll(min(group_need(1), ptotal + 1));
+        issue_pf(ld, nh);
+      }
+    }
+#endif
     for (int t = 0; t < total; ++t) {
       const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
       if (wid < NCW) {
@@ -480,6 +532,13 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           first_refl(R, n, j0 + pair, rfl[pair][(t + 1) & 1]);
         }
       } else if (wid == NCW) {
+#if TG_BULGE_WDEFER
+        // writer: step t-1's stores had a step to drain: publish t-1, then
+        // retire the columns step t-1 left behind
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (t > 0 && wlane == 0)
+          __hip_atomic_store(prog + G, unsigned(t - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         // writer: retire the columns step t-1 left behind, drain, publish t
         const int nl = group_low(n, nsw, j0, g, t);
         if (nl > wb) {
@@ -493,10 +552,35 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           }
           wb = nl;
         }
+#if !TG_BULGE_WDEFER
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (wlane == 0)
           __hip_atomic_store(prog + G, unsigned(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       } else {
+#if TG_BULGE_PF2
+        // loader: columns of step t+1 (loaded at step t-1) into the ring, then
+        // issue the loads of step t+2's columns
+        if (pf_hi > pf_lo) {
+#pragma unroll
+          for (int u = 0; u < PW; ++u) {
+            const int idx = wlane + 64 * u;
+            const int c = pf_lo + idx / nthr_col, h = idx % nthr_col;
+            if (c < pf_hi) {
+              R[rslot(c)][2 * h] = pb[u].x;
+              R[rslot(c)][2 * h + 1] = pb[u].y;
+            }
+          }
+          ld = max(ld, pf_hi);
+          pf_lo = pf_hi;
+        }
+        if (t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
+        const int nh2 = group_high(n, j0, t + 2);
+        if (t + 2 < total && nh2 > ld) {
+          poll(min(group_need(t + 2), ptotal + 1));
+          issue_pf(ld, nh2);
+        }
+#else
         // loader: columns step t + 1 adds
         const int nh = group_high(n, j0, t + 1);
         if (t + 1 < total && nh > ld) {
@@ -516,7 +600,6 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
             known = need;
             __builtin_amdgcn_wave_barrier();
           }
-          constexpr int PW = SB_B * nthr_col_c / 64;  // 16-B chunks per lane
           double2 buf[PW];
 #pragma unroll
           for (int u = 0; u < PW; ++u) {
@@ -537,6 +620,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           }
         }
         if (t + 1 < total) ld = max(ld, nh);
+#endif
       }
       const uint64_t c1t = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
@@ -882,6 +966,15 @@ __global__ __launch_bounds__(256) void q2_apply_kernel(double *__restrict__ Z, i
 }  // namespace
 
 namespace tg {
+
+hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, const double *tau2,
+                          double *T2) {
+  const int nsw = n - 2;
+  if (nsw <= 0) return hipSuccess;
+  hipLaunchKernelGGL(q2_tfactor_kernel, dim3(sb_smax(n), cdiv(nsw, QB)), dim3(256), 0, st, V2,
+                     tau2, n, sb_smax(n), T2);
+  return hipGetLastError();
+}
 
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
                        const double *tau2, double *T2) {

@@ -1346,8 +1346,20 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   const bool ts = two_stage(n);
   const int nref = ts ? 0 : n - 1;
   if (ts) {
-    TG_HIP(tg::sb_apply_q2(st, n, w.Z, k, sb.V2, sb.tau2, sb.T2));
-    TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
+    // few vectors (the complement path's request): one persistent launch
+    static const bool multi = getenv("TG_BT_MULTI") != nullptr;
+    if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl) <= sizeof(double) * size_t(n) * tg::SB_B) {
+      TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.tau2, sb.T2));
+      bool tmo = false;
+      TG_HIP(tg::sb_apply_few(st, n, w.Z, k, pl, sb, sb.X, &tmo));
+      if (tmo) {
+        tg::set_error("tg_eigh_vectors_range: back-transformation grid barrier timed out");
+        return int(hipErrorLaunchTimeOut);
+      }
+    } else {
+      TG_HIP(tg::sb_apply_q2(st, n, w.Z, k, sb.V2, sb.tau2, sb.T2));
+      TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
+    }
   }
   if (nref > 0) {
     const int nblk = tg::cdiv(nref, BT);
