@@ -50,6 +50,8 @@ struct BtArgs {
   const double *Y, *T;    // Q1 (TSQR) reflectors / T factors
   const Q1Op *ops;
   int nops;
+  int single;             // one-level panels (q1_big_a / q1_big_b)
+  double *part;           // single: per-sub-chunk P partials (32 x 32 each)
   unsigned *cnt;          // [0] step counter, [1] timeout flag (zeroed per call)
   unsigned long long timeout;
 };
@@ -396,6 +398,140 @@ __device__ void q1_chunk(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
   __syncthreads();  // red / Ps / Ms reused by the next chunk
 }
 
+// Single-level panels (one compact-WY block of m rows, band.h SbPlan::single):
+// sub-chunks of 512 rows, two phases with a grid barrier between them.
+// Phase A: sub-chunk I publishes P_I = Y_I^T Z_I (32 x k) to part[I].
+template <int NCB>
+__device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
+                         SmQ1 &sm) {
+  const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int kb = I * 512, h = min(512, d.rows - kb);
+  const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
+  doublex4 Pa[2][NCB];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    double zl[4][NCB], ya[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + 4 * q + lr, rc = min(rl, h - 1);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        zl[q][cb] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) ya[q][ia] = Y[int64_t(rc) * SB_B + ia * 16 + lc];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + 4 * q + lr;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const double zv = (rl < h && cb * 16 + lc < k) ? zl[q][cb] : 0.0;
+          const double yv = rl < h ? ya[q][ia] : 0.0;
+          Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(yv, zv, Pa[ia][cb], 0, 0, 0);
+        }
+    }
+  }
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm.red[wid][ia * 16 + lr + 4 * q][cb * 16 + lc] = Pa[ia][cb][q];
+  __syncthreads();
+  double *out = a.part + int64_t(I) * SB_B * SB_B;
+  for (int idx = tid; idx < SB_B * SB_B; idx += 64 * BW) {
+    const int r = idx >> 5, cc = idx & 31;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < BW; ++w) v += sm.red[w][r][cc];
+    store_sc1(&out[idx], v);
+  }
+  __syncthreads();  // red reused by the next sub-chunk
+}
+
+// Phase B: P = sum_J P_J (sub-chunk order), M = T P, Z_I -= Y_I M.
+template <int NCB>
+__device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
+                         int nsub, SmQ1 &sm) {
+  const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int kb = I * 512, h = min(512, d.rows - kb);
+  const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
+  double *Zs = a.Z + int64_t(d.r0 + kb) * k;
+  doublex4 F[4][NCB];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q, rc = min(rl, h - 1);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb][q] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
+    }
+  for (int idx = tid; idx < SB_B * SB_B; idx += 64 * BW) {
+    double v = 0.0;
+    for (int j0 = 0; j0 < nsub; j0 += 8) {
+      double t[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        t[b] = j0 + b < nsub ? __hip_atomic_load(a.part + int64_t(j0 + b) * SB_B * SB_B + idx,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v += t[b];
+    }
+    sm.Ps[idx >> 5][idx & 31] = v;
+    sm.Ms[idx >> 5][idx & 31] = a.T[d.toff + idx];
+  }
+  __syncthreads();
+  double mval[2] = {0.0, 0.0};
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) {
+    const int r = idx >> 5, cc = idx & 31;
+    if (cc >= 16 * NCB) continue;
+    double v = 0.0;
+    for (int e = r; e < SB_B; ++e) v += sm.Ms[r][e] * sm.Ps[e][cc];
+    mval[t] = v;
+  }
+  __syncthreads();
+  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) sm.Ms[idx >> 5][idx & 31] = mval[t];
+  __syncthreads();
+#pragma unroll
+  for (int k0 = 0; k0 < SB_B; k0 += 4) {
+    double bm[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) bm[cb] = sm.Ms[k0 + lr][cb * 16 + lc];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int rl = wid * 64 + rb * 16 + lc;
+      const double yl = Y[int64_t(min(rl, h - 1)) * SB_B + k0 + lr];
+      const double ya = rl < h ? -yl : 0.0;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm[cb], F[rb][cb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      if (rl >= h) continue;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + lc;
+        if (col < k) store_sc1(&Zs[int64_t(rl) * k + col], F[rb][cb][q]);
+      }
+    }
+  __syncthreads();
+}
+
 template <int NCB>
 __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
   __shared__ BtShared sm;
@@ -479,6 +615,17 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
     st_b2 += t2 - t1;
 #endif
   }
+  if (a.single) {
+    for (int o = 0; o < a.nops; ++o) {
+      const Q1Op d = a.ops[o];
+      const int nsub = (d.rows + 511) / 512;
+      for (int I = me; I < nsub; I += W) q1_big_a<NCB>(a, rz, d, I, sm.q1);
+      grid_barrier(a, unsigned(W) * ++step);
+      for (int I = me; I < nsub; I += W) q1_big_b<NCB>(a, rz, d, I, nsub, sm.q1);
+      if (o + 1 < a.nops) grid_barrier(a, unsigned(W) * ++step);
+    }
+    return;
+  }
   Q1Pre p1;
   if (a.nops > 0 && me < a.ops[0].nc) q1_fetch(a, a.ops[0], me, p1);
   for (int o = 0; o < a.nops; ++o) {
@@ -516,10 +663,16 @@ int sb_smax(int n);
 
 // ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + 64 bytes of
 // device scratch (step counter + timeout flag first).
-size_t sb_apply_few_scratch(const SbPlan &pl) {
+static size_t few_ops_bytes(const SbPlan &pl) {
   size_t c = 0;
   for (const SbPanel &P : pl.panels) c += size_t(P.nl);
-  return 64 + c * sizeof(Q1Op);
+  return (64 + c * sizeof(Q1Op) + 255) & ~size_t(255);
+}
+static int few_nsub(const SbPlan &pl) {
+  return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, 512) : 0;
+}
+size_t sb_apply_few_scratch(const SbPlan &pl) {
+  return few_ops_bytes(pl) + size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double);
 }
 
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
@@ -554,11 +707,13 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.T = b.T;
   a.ops = dops;
   a.nops = int(ops.size());
+  a.single = pl.single ? 1 : 0;
+  a.part = reinterpret_cast<double *>(static_cast<char *>(dev) + few_ops_bytes(pl));
   a.cnt = cnt;
   const char *tt = getenv("TG_BT_TIMEOUT_TICKS");
   a.timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
-  const int W = std::min(256, std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax));
+  const int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
   auto tok = prof_begin(st, PROF_Q2, 0.0, 0.0);
   const int grid = TG_BT_XCD ? 8 * W : W;  // XCD form: ~W land on each XCD
   if (k <= 16)

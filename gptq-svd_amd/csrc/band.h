@@ -1,6 +1,7 @@
 // Stage 1 of the two-stage symmetric eigensolver: full -> band reduction
 // (sy2sb) with TSQR panel factorisations, and its back-transformation.
 #pragma once
+#include <algorithm>
 #include <type_traits>
 #include <vector>
 
@@ -11,6 +12,8 @@ namespace tg {
 constexpr int SB_B = 32;    // half-bandwidth of the band matrix (= panel width)
 constexpr int SB_C = 256;   // TSQR leaf height (last leaf of a level absorbs < SB_C rows)
 constexpr int SB_LV = 6;    // max TSQR levels
+constexpr int PQR_NWMAX = 32;        // panel-QR workgroups (pqr.hip)
+constexpr int PQR_BC_DOUBLES = 8192; // panel-QR broadcast block
 
 // One TSQR level of one panel: `rows` stacked rows split in `nc` chunks.
 struct SbLevel {
@@ -22,10 +25,15 @@ struct SbPanel {
   SbLevel L[SB_LV];
 };
 
+// single: one compact-WY block per panel (Y m x 32, one T; pqr.hip panel
+// QR), the default for n <= 32768; otherwise (or TG_SB_TSQR=1) the TSQR tree
+// of leaves of SB_C rows.  A panel's levels are then one level of one chunk
+// of m rows (P.L[0] = {m, 1, ...}).
 struct SbPlan {
   std::vector<SbPanel> panels;
   size_t ytotal = 0, ttotal = 0;
   int ncmax = 1;
+  bool single = false;
   explicit SbPlan(int n);
 };
 
@@ -43,10 +51,23 @@ struct SbBufs {
   double *V2, *tau2;      // bulge-chasing reflectors ((n-2) x smax x b, (n-2) x smax)
   double *T2;             // Q2 block T factors
   unsigned *prog;         // pipeline progress per sweep group
+  // panel QR (pqr.hip): partials, broadcast block, per-panel control words
+  double *pq_part, *pq_bc;
+  unsigned *pq_ctl;       // [0] timeout flag, [1] M-kernel ticket, [4 + 4 i] panel i counters
 };
+
+int pqr_rows_per_thread(int m);
+// Panel A[r0:r0+m, p:p+32] -> Y (m x 32), YT = Y T, T (32 x 32); writes
+// [R; 0] and its transpose into A.  cnt: 2 words zeroed before the launch.
+hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
+                    double *YT, double *T, double *part, double *bc, unsigned *cnt,
+                    unsigned *tmo);
 
 int sb_smax(int n);
 size_t sb2st_t2_count(int n);
+
+// control words: 4 + 4 per panel, padded to a multiple of 16 bytes
+inline size_t pq_ctl_words(int n) { return 4 + 4 * size_t(std::max(1, n / SB_B + 1)); }
 
 template <class A>
 void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
@@ -80,11 +101,18 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   // per-group progress + 4 control words (XCD, group queue, stall flag)
   if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw + 4);
   else ar.template take<unsigned>(nsw + 4);
+  const size_t npart = std::max<size_t>(2 * PQR_NWMAX + 2, size_t(n) / SB_C + 2) * 1024;
+  take(b.pq_part, npart);
+  take(b.pq_bc, PQR_BC_DOUBLES);
+  if constexpr (std::is_same_v<A, Arena>) b.pq_ctl = ar.template take<unsigned>(pq_ctl_words(n));
+  else ar.template take<unsigned>(pq_ctl_words(n));
 }
 
 // A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth
 // SB_B in place (full storage, zeros outside the band); reflectors in bufs.
 hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b);
+// Single-level plans: reads the panel-QR timeout flag (one D2H copy + sync).
+hipError_t sy2sb_timed_out(hipStream_t st, const SbPlan &pl, const SbBufs &b, bool *tmo);
 // Band (in A after sy2sb) -> tridiagonal (d, e) by bulge chasing.
 // A stalled hand-off (a wait beyond the timeout, TG_BULGE_TIMEOUT_TICKS of the
 // 100 MHz clock, default 2 s) poisons d and e with NaN; the stall flag stays

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <utility>
+#include <vector>
 
 #include "band.h"
 #include "gemm64.h"
@@ -35,12 +36,23 @@ namespace tg {
 
 SbPlan::SbPlan(int n) {
   ncmax = std::max(1, n / SB_C);
+  const char *e = getenv("TG_SB_TSQR");
+  single = !(e && e[0] == '1') && pqr_rows_per_thread(n) > 0;
   int p = 0;
   while (p + SB_B < n - 1) {
     SbPanel P{};
     P.p = p;
     P.r0 = p + SB_B;
     P.m = n - P.r0;
+    if (single) {
+      P.L[0] = SbLevel{P.m, 1, ytotal, ttotal};
+      ytotal += size_t(P.m) * SB_B;
+      ttotal += size_t(SB_B) * SB_B;
+      P.nl = 1;
+      panels.push_back(P);
+      p += SB_B;
+      continue;
+    }
     int rows = P.m, l = 0;
     while (true) {
       SbLevel &L = P.L[l];
@@ -755,6 +767,78 @@ __global__ void sym_scatter_kernel(double *__restrict__ A, int64_t lda, int m, i
   }
 }
 
+// Single-level panels: M = T^T (Y^T X)  (32 x 32, K = m rows).  One
+// workgroup per 256 rows (wave w: rows 64w..64w+63 on FP64 MFMA), partials
+// summed in workgroup order by the last arriver (reduce.h hand-off).
+__global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y,
+                                                    const double *__restrict__ X, int m,
+                                                    const double *__restrict__ T,
+                                                    double *__restrict__ M, double *part,
+                                                    unsigned *ticket) {
+  __shared__ double red[4][SB_B][SB_B + 1];
+  __shared__ double Ps[SB_B * SB_B];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  const int base = blockIdx.x * 256 + wid * 64;
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) acc[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    double ya[4][2], xb[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = base + 16 * g4 + 4 * q + lr, rc = min(r, m - 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ya[q][h] = r < m ? Y[int64_t(rc) * SB_B + h * 16 + lc] : 0.0;
+        xb[q][h] = r < m ? X[int64_t(rc) * SB_B + h * 16 + lc] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[q][ia], xb[q][cb], acc[ia][cb], 0, 0, 0);
+  }
+#pragma unroll
+  for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[wid][ia * 16 + lr + 4 * q][cb * 16 + lc] = acc[ia][cb][q];
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    const int x = e >> 5, y = e & 31;
+    Ps[e] = (red[0][x][y] + red[1][x][y]) + (red[2][x][y] + red[3][x][y]);
+  }
+  __syncthreads();
+  if (!tg::publish_partials(Ps, SB_B * SB_B, part, ticket)) return;
+  const int G = int(gridDim.x);
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    double v = 0.0;
+    for (int g0 = 0; g0 < G; g0 += 8) {
+      double t[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) t[b] = g0 + b < G ? tg::load_partial(&part[size_t(e) * G + g0 + b]) : 0.0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v += t[b];
+    }
+    red[0][e >> 5][e & 31] = v;
+  }
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    const int a = e >> 5, c = e & 31;
+    double v = 0.0;
+    for (int k = 0; k <= a; ++k) v = fma(T[k * SB_B + a], red[0][k][c], v);
+    M[e] = v;
+  }
+  if (tid == 0) *ticket = 0u;
+}
+
 // A[r0+i][p+l] = [R; 0] and the transpose (i < m, l < 32).
 __global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, int r0, int m,
                                    const double *__restrict__ R) {
@@ -770,6 +854,8 @@ __global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, i
 }  // namespace
 
 namespace tg {
+
+constexpr int NPQ_STAT = 8;
 
 #define TG_CHK(x)                     \
   do {                                \
@@ -800,7 +886,61 @@ static hipError_t side_stream(SideStream *&out) {
   return hipSuccess;
 }
 
+// One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
+static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
+                               const SbBufs &b) {
+  TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
+  int pi = 0;
+  for (const SbPanel &P : pl.panels) {
+    const int m = P.m, r0 = P.r0;
+    double *A22 = A + int64_t(r0) * lda + r0;
+    double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
+    TG_CHK(panel_qr(st, A, lda, P.p, r0, m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
+                    b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
+    // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
+    const int nz = std::max(1, m / SB_C);
+    ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
+    TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
+    TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
+    // M = T^T Y^T X
+    hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 256)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
+                       b.pq_part, b.pq_ctl + 1);
+    TG_CHK(hipGetLastError());
+    const int nt = cdiv(m, S2T);
+    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
+    hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                       int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+    prof_end(st, tok);
+    TG_CHK(hipGetLastError());
+    ++pi;
+  }
+  return hipSuccess;
+}
+
+hipError_t sy2sb_timed_out(hipStream_t st, const SbPlan &pl, const SbBufs &b, bool *tmo) {
+  *tmo = false;
+  if (!pl.single || pl.panels.empty()) return hipSuccess;
+  unsigned h = 0;
+  hipError_t e = hipMemcpyAsync(&h, b.pq_ctl, sizeof(unsigned), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  *tmo = h != 0u;
+  if (getenv("TG_PQR_STATS")) {
+    std::vector<unsigned> c(4 + 4 * pl.panels.size());
+    (void)hipMemcpy(c.data(), b.pq_ctl, sizeof(unsigned) * c.size(), hipMemcpyDeviceToHost);
+    int hist[4][NPQ_STAT] = {};
+    for (size_t i = 0; i < pl.panels.size(); ++i) {
+      const unsigned v = c[4 + 4 * i + 1];
+      hist[std::min(3u, v / 16)][std::min(unsigned(NPQ_STAT - 1), v % 16)]++;
+    }
+    fprintf(stderr, "pqr: %zu panels; accept after 2/3/4 passes: %d/%d/%d; fallback: %d\n",
+            pl.panels.size(), hist[2][2], hist[2][3], hist[2][4],
+            hist[3][0] + hist[3][1] + hist[3][2] + hist[3][3] + hist[3][4]);
+  }
+  return e;
+}
+
 hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, const SbBufs &b) {
+  if (pl.single) return sy2sb_single(st, A, lda, n, pl, b);
   SideStream *ss = nullptr;
   TG_CHK(side_stream(ss));
   int pi = 0;
@@ -912,6 +1052,22 @@ hipError_t sy2sb(hipStream_t st, double *A, int lda, int n, const SbPlan &pl, co
 hipError_t sb_apply_q1(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                        const SbBufs &b) {
   (void)n;
+  if (pl.single) {
+    // Z[r0:, :] -= Y (T (Y^T Z[r0:, :])) per panel, last panel first
+    for (auto it = pl.panels.rbegin(); it != pl.panels.rend(); ++it) {
+      const SbPanel &P = *it;
+      double *Zs = Z + int64_t(P.r0) * k;
+      const double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
+      auto tok = prof_begin(st, PROF_Q1, 24.0 * double(P.m) * k, 4.0 * double(P.m) * SB_B * k);
+      const int splits = std::max(1, std::min(pl.ncmax, P.m / SB_C));
+      TG_CHK(dgemm_splitk(st, true, false, SB_B, k, P.m, 1.0, Yp, SB_B, Zs, k, 0.0, b.P, k, splits,
+                          b.Zg));
+      TG_CHK(dgemm(st, false, false, SB_B, k, SB_B, 1.0, Tp, SB_B, b.P, k, 0.0, b.Mz, k));
+      TG_CHK(dgemm(st, false, false, P.m, k, SB_B, -1.0, Yp, SB_B, b.Mz, k, 1.0, Zs, k));
+      prof_end(st, tok);
+    }
+    return hipSuccess;
+  }
   for (auto it = pl.panels.rbegin(); it != pl.panels.rend(); ++it) {
     const SbPanel &P = *it;
     double *Zs = Z + int64_t(P.r0) * k;

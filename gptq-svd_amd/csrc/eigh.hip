@@ -1157,6 +1157,12 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
     TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.tau2, sb.prog, w.d, w.e));
     bool stalled = false;
     TG_HIP(tg::sb2st_stalled(st, n, sb.prog, &stalled));
+    bool ptmo = false;
+    TG_HIP(tg::sy2sb_timed_out(st, pl, sb, &ptmo));
+    if (ptmo) {
+      tg::set_error("tg_eigh_values: panel-QR grid barrier timed out; the band form is invalid");
+      return int(hipErrorLaunchTimeOut);
+    }
     if (stalled) {
       tg::set_error("tg_eigh_values: bulge-chasing pipeline stalled (a hand-off wait timed out); "
                     "the tridiagonal form is invalid");

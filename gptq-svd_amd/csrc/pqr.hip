@@ -1,0 +1,904 @@
+// Panel QR of the two-stage band reduction (band.hip, sy2sb): for the
+// panel P = A[r0:r0+m, p:p+32] it forms ONE compact-WY block,
+//   P = H [R; 0],  H = I - Y T Y^T  (Y m x 32 unit lower trapezoidal),
+// and writes [R; 0] (and its transpose) back into A.
+//
+// Replaces the per-panel Householder QR of the reduction inside
+// `torch.linalg.eigh` (/root/reference/src/TruncGPTQ/gptq_utils.py:93).
+// One persistent launch per panel: NW workgroups (launched 8 NW, the ones
+// with blockIdx % 8 == 0 work, so they share one XCD's L2 under round-robin
+// dispatch; correctness does not depend on it), each holding 256 rows of P in
+// LDS, an in-launch grid barrier between phases (cdna_hip_programming.md §6
+// Guideline 16: write-through sc1 payload stores, every storing wave drains
+// vmcnt, one relaxed counter add per workgroup, bounded relaxed poll, sc1
+// payload loads):
+//  1. CholeskyQR2 (Yamamoto et al. 2015): G = Q^T Q on FP64 MFMA (partials
+//     per workgroup, summed in workgroup order by workgroup 0), L = chol(G)
+//     by one wave, Q <- Q L^-T by row-wise forward substitution (backward
+//     stable).  The first pass is shifted (Fukaya et al. 2020) when its
+//     pivots show a condition number near 1/sqrt(eps); passes repeat until
+//     the Gram matrix of the current Q is within 0.1 of I (at most NPASS).
+//  2. Householder reconstruction (Ballard et al. 2015): LU of I - Q1 S
+//     (S_jj = -sign chosen during the elimination, pivots 1 + |.| >= 1)
+//     gives Y1 = L and U; Y2 = -Q2 S U^-1 (forward substitution with U),
+//     T = U Y1^-T, R = S (L_g^T ... L_1^T).
+//  3. Fallback (rank-deficient or numerically singular panels, m < 64):
+//     Householder column by column over the grid, one barrier per column
+//     (one reduction gives the column norm and every w = P^T v entry).
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
+
+#include "band.h"
+#include "common.h"
+#include "lanes.h"
+
+namespace {
+
+using tg::SB_B;
+constexpr int PT = 256;    // threads per workgroup (4 waves) = rows per workgroup
+constexpr int XS = 34;     // row stride of the LDS row block (16-B aligned rows)
+constexpr int NPASS = 4;   // Gram passes before the Householder fallback
+constexpr int FB_MIN_M = 64;
+
+enum Dec { DEC_CONTINUE = 1, DEC_ACCEPT = 2, DEC_FALLBACK = 3 };
+
+// broadcast block layout (doubles)
+constexpr int BC_DEC = 0, BC_L = 64, BC_RINV = BC_L + 1024, BC_T = BC_RINV + 64,
+              BC_PROW = BC_T + 1024, BC_MB = BC_PROW + 128, BC_SIZE = BC_MB + 2048;
+static_assert(BC_SIZE <= tg::PQR_BC_DOUBLES, "broadcast block");
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+struct PqrArgs {
+  double *A;
+  int64_t lda;
+  int p, r0, m, nw;
+  double *Y, *YT, *T;  // outputs (Y, YT: m x 32 row-major)
+  double *part;        // partials: Gram nw x 1024 | fallback 2 x nw x 32
+  double *bc;          // broadcast block
+  unsigned *cnt;       // [0] barrier counter, [1] path record (zeroed before the launch)
+  unsigned *tmo;       // timeout flag (shared by all panels)
+  unsigned long long timeout;
+  unsigned long long *stats;  // TG_PQR_STATS: per-phase clock stamps of workgroup 0 (or null)
+};
+
+struct PqrSm {
+  double Xs[PT][XS];          // this workgroup's rows (panel row 256 w + t in Xs[t])
+  double Gs[32][33];          // workgroup 0: Gram sum; HR: U^-1; fallback: reduce rows
+  double Lt[32][33];          // this pass's L (Lt[c][i] = L[i][c], i.e. L^T)
+  double Ra[32][33];          // workgroup 0: R = L_g^T ... L_1^T
+  double Ut[32][33], Tm[32][33];
+  double Cq[32][33];          // Q top rows -> Y1 (HR); fallback: T recurrence input
+  double RgI[32][33];         // (L_g^T)^-1; scratch of the R update
+  double MB[32][65];          // [M1 | M1 T] of the final CholeskyQR pass
+  double rinv[32], uinv[32], sv[32];
+  double dsum[32], prow[32], taus[32];
+  double bcast[2][128];        // one-wave broadcast rows (+ a trash slot per lane)
+  int dec;
+  PqrArgs ga;                 // the launch arguments (read by the out-of-line phases)
+};
+
+// Per-workgroup state at file scope, so the out-of-line phases below address
+// it as LDS without pointer arguments.  The phases are kept out of line so
+// that their unrolled address arithmetic is not hoisted across the pass loop
+// (it once held ~700 SGPRs and spilled).
+__shared__ PqrSm s_pq;
+
+#ifdef TG_PQR_DBG
+__device__ unsigned long long g_pq_dbg[64];
+#define DBG_STAMP(k) \
+  if (threadIdx.x == 0) g_pq_dbg[(k)] += __builtin_amdgcn_s_memrealtime();
+#else
+#define DBG_STAMP(k)
+#endif
+
+// threadIdx.x through an empty asm: every phase derives its lane indices and
+// LDS addresses from its own opaque copy, so the compiler neither hoists them
+// out of the pass loop nor shares them between inlined phases (which held
+// hundreds of registers live across the kernel and spilled).
+__device__ __forceinline__ int otid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+typedef __attribute__((address_space(1))) double gf64;
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store((gf64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __hip_atomic_load((gf64 *)const_cast<double *>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double rsq_nr(double x) {  // 1/sqrt(x), ~1 ulp
+  double r = __builtin_amdgcn_rsq(x);
+  r = r * fma(-0.5 * x * r, r, 1.5);
+  return r * fma(-0.5 * x * r, r, 1.5);
+}
+__device__ __forceinline__ double rcp_nr(double x) {  // 1/x, ~1 ulp
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Grid barrier (counter form): every wave's sc1 stores drained, one add per
+// workgroup, a bounded relaxed poll by one lane.
+__device__ __forceinline__ void grid_bar(const PqrArgs &g, unsigned &ep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ++ep;
+  if (threadIdx.x == 0) {
+    gu32 *c = (gu32 *)(g.cnt);
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = unsigned(g.nw) * ep;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > g.timeout) {
+        __hip_atomic_store((gu32 *)(g.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Panel row i (zeros past m) into registers.
+__device__ __forceinline__ void load_row(const PqrArgs &g, int i, double (&x)[32]) {
+  const int ic = min(i, g.m - 1);
+  const double *s = g.A + (g.r0 + int64_t(ic)) * g.lda + g.p;
+  double2 v[16];
+  if ((g.lda & 1) == 0 && (g.p & 1) == 0) {
+    const double2 *s2 = reinterpret_cast<const double2 *>(s);
+#pragma unroll
+    for (int l = 0; l < 16; ++l) v[l] = s2[l];
+  } else {
+#pragma unroll
+    for (int l = 0; l < 16; ++l) v[l] = make_double2(s[2 * l], s[2 * l + 1]);
+  }
+  const bool ok = i < g.m;
+#pragma unroll
+  for (int l = 0; l < 16; ++l) {
+    x[2 * l] = ok ? v[l].x : 0.0;
+    x[2 * l + 1] = ok ? v[l].y : 0.0;
+  }
+}
+__device__ __forceinline__ void row_to_lds(double *dst, const double (&x)[32]) {
+  double2 *d = reinterpret_cast<double2 *>(dst);
+#pragma unroll
+  for (int l = 0; l < 16; ++l) d[l] = make_double2(x[2 * l], x[2 * l + 1]);
+}
+__device__ __forceinline__ void row_from_lds(const double *src, double (&x)[32]) {
+  const double2 *s = reinterpret_cast<const double2 *>(src);
+#pragma unroll
+  for (int l = 0; l < 16; ++l) {
+    const double2 v = s[l];
+    x[2 * l] = v.x;
+    x[2 * l + 1] = v.y;
+  }
+}
+
+// x <- x L^-T (forward substitution; Lt[c][l] = L[l][c] = R[c][l]).  Row
+// c + 1 of Lt is loaded while column c is applied; the empty asm with a
+// memory clobber keeps the compiler from hoisting all 528 uniform LDS loads
+// to the top (they then spill).
+__device__ __forceinline__ void trsm_row(double (&x)[32], const double (*Lt)[33], const double *rinv) {
+  double cur[32], nxt[32];
+#pragma unroll
+  for (int l = 1; l < 32; ++l) cur[l] = Lt[0][l];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    const double rc = rinv[c];
+#pragma unroll
+    for (int l = c + 2; l < 32; ++l) nxt[l] = Lt[c + 1 < 32 ? c + 1 : 31][l];
+    x[c] *= rc;
+#pragma unroll
+    for (int l = c + 1; l < 32; ++l) x[l] = fma(-x[c], cur[l], x[l]);
+#pragma unroll
+    for (int l = c + 2; l < 32; ++l) cur[l] = nxt[l];
+    asm volatile("" ::: "memory");
+  }
+}
+
+// C = A diag(d) B for 32 x 32 LDS matrices on FP64 MFMA (d = null: no
+// scaling): wave w computes the 16 x 16 block (w >> 1, w & 1), K = 32.
+// C may not alias A or B.  All four waves of the workgroup must call it.
+template <int LDA, int LDB, int LDC>
+__device__ __forceinline__ void mm32(double *C, const double *A, const double *B, const double *d) {
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  const int bi = 16 * (wid >> 1), bj = 16 * (wid & 1);
+  doublex4 acc = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 4) {
+    double a = A[(bi + lc) * LDA + k0 + lr];
+    if (d) a *= d[k0 + lr];
+    const double b = B[(k0 + lr) * LDB + bj + lc];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) C[(bi + lr + 4 * q) * LDC + bj + lc] = acc[q];
+}
+
+// This workgroup's Gram partial of its LDS rows -> part[w]: waves 0, 1, 2
+// take the 16 x 16 blocks (0,0), (0,1), (1,1) over all 256 rows (no
+// cross-wave reduction); (1,0) is the transpose of (0,1).
+__device__ __forceinline__ void gram_publish(const PqrArgs &g, PqrSm &sm, int w) {
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  if (wid >= 3) return;
+  const int ia = wid == 2 ? 16 : 0, cb = wid == 0 ? 0 : 16;
+  doublex4 acc[2] = {doublex4{0.0, 0.0, 0.0, 0.0}, doublex4{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll 4
+  for (int k0 = 0; k0 < PT; k0 += 8) {
+    const double a0 = sm.Xs[k0 + lr][ia + lc], b0 = sm.Xs[k0 + lr][cb + lc];
+    const double a1 = sm.Xs[k0 + 4 + lr][ia + lc], b1 = sm.Xs[k0 + 4 + lr][cb + lc];
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1], 0, 0, 0);
+  }
+  double *out = g.part + int64_t(w) * 1024;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double v = acc[0][q] + acc[1][q];
+    const int r = ia + lr + 4 * q, c = cb + lc;
+    st_sc1(out + r * 32 + c, v);
+    if (wid == 1) st_sc1(out + c * 32 + r, v);
+  }
+}
+
+// Workgroup 0: G = sum of the partials in workgroup order -> Gs.
+__device__ __forceinline__ void gram_reduce(const PqrArgs &g, PqrSm &sm) {
+  const int tid = otid();
+  constexpr int NB = 16;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int w0 = 0; w0 < g.nw; w0 += NB) {
+    double v[4][NB];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        v[u][b] = ld_sc1(g.part + int64_t(min(w0 + b, g.nw - 1)) * 1024 + tid + PT * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[u] += (w0 + b < g.nw) ? v[u][b] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + PT * u;
+    sm.Gs[e >> 5][e & 31] = acc[u];
+  }
+}
+
+// One wave: L = chol(Gs + shift I) into Lt (Lt[c][i] = L[i][c]) and rinv;
+// lane (i = lane & 31, h = lane >> 5) holds row i, columns 16h .. 16h + 15;
+// column j is broadcast through LDS at each step.  ok: every pivot positive
+// and finite; minrat = min_j pivot_j / (G_jj + shift).
+__device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
+  PqrSm &sm = s_pq;
+  const int lane = otid() & 63, i = lane & 31, h = lane >> 5;
+  double *buf = sm.bcast[0];
+  double gr[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) gr[c] = sm.Gs[i][16 * h + c] + (16 * h + c == i ? shift : 0.0);
+  bool ok = true;
+  double mr = 1.0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int hj = j >> 4, cj = j & 15;
+    // lanes of column j publish it; the others write a slot nobody reads
+    buf[h == hj ? i : 32 + lane] = gr[cj];
+    wave_lds_sync();
+    double piv = buf[j];
+    const double gij = buf[i];
+    double col[16];
+    const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const double2 v = b2[c];
+      col[2 * c] = v.x;
+      col[2 * c + 1] = v.y;
+    }
+    wave_lds_sync();
+    if (!(piv > 0.0) || !(piv <= DBL_MAX)) {
+      ok = false;
+      piv = 1.0;
+    }
+    mr = fmin(mr, piv * rcp_nr(sm.Gs[j][j] + shift));
+    const double r = rsq_nr(piv);
+    const double lij = (i > j) ? gij * r : (i == j ? piv * r : 0.0);
+    if (h == hj) gr[cj] = lij;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const double ml = (16 * h + c > j) ? -lij : 0.0;
+      gr[c] = fma(ml, col[c] * r, gr[c]);
+    }
+  }
+  double dg = 1.0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    sm.Lt[16 * h + c][i] = (16 * h + c <= i) ? gr[c] : 0.0;
+    dg = (16 * h + c == i) ? gr[c] : dg;
+  }
+  if ((i >> 4) == h) sm.rinv[i] = rcp_nr(dg);
+  minrat = mr;
+  return ok;
+}
+
+// Workgroup 0 after acceptance (Cq = top 32 rows of the final Q, Lt = this
+// pass's factor, Ra = L_g^T ... L_1^T):
+//   wave 0: LU of I - Cq S (Householder reconstruction): U, Y1 (into Cq), S;
+//   wave 1: Rg^-1 (Rg = Lt as a matrix);
+// then T (T Y1^T = U), U^-1 (into Gs), the band block S R written to A, and
+//   MB = [M1 | M1 T],  M1 = Rg^-1 (-S) U^-1,
+// so that a row q of the previous pass gives Y = q M1, Y T = q M1 T.
+__device__ __forceinline__ void hr_top_ool() {
+  PqrSm &sm = s_pq;
+  const PqrArgs &g = sm.ga;
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
+  double(*UI)[33] = sm.Gs;
+  DBG_STAMP(16)
+  if (wid == 0) {
+    const int i = lane & 31, h = lane >> 5;
+    double *buf = sm.bcast[0], *cbuf = sm.bcast[1];
+    double c[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) c[l] = sm.Cq[i][16 * h + l];
+    // L_ij = -S_jj C^(j)_ij / U_jj, U_jj = 1 + |C^(j)_jj|, S_jj = -sign(C^(j)_jj),
+    // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int hj = j >> 4, cj = j & 15;
+      if (i == j) {  // row j (its two half-rows: lanes j and j + 32)
+        double2 *d2 = reinterpret_cast<double2 *>(buf + 16 * h);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) d2[l] = make_double2(c[2 * l], c[2 * l + 1]);
+      }
+      cbuf[h == hj ? i : 32 + lane] = c[cj];  // column j; the other lanes write their own trash slot
+      wave_lds_sync();
+      const double qjj = buf[j], cij = cbuf[i];
+      double rw[16];
+      const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
+#pragma unroll
+      for (int l = 0; l < 8; ++l) {
+        const double2 v = b2[l];
+        rw[2 * l] = v.x;
+        rw[2 * l + 1] = v.y;
+      }
+      wave_lds_sync();
+      const double s = (qjj >= 0.0) ? -1.0 : 1.0;
+      const double ru = rcp_nr(1.0 + fabs(qjj));
+      if (lane == 0) sm.sv[j] = s;
+      const double lij = -s * cij * ru;
+      if (i > j && h == hj) c[cj] = lij;
+#pragma unroll
+      for (int l = 0; l < 16; ++l) {
+        const double ml = (i > j && 16 * h + l > j) ? -lij : 0.0;
+        c[l] = fma(ml, rw[l], c[l]);
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      const int col = 16 * h + l;
+      sm.Ut[i][col] = (col == i) ? 1.0 + fabs(c[l]) : (col > i ? -sm.sv[col] * c[l] : 0.0);
+      sm.Cq[i][col] = (col < i) ? c[l] : (col == i ? 1.0 : 0.0);
+      if (col == i) sm.uinv[i] = rcp_nr(1.0 + fabs(c[l]));
+    }
+  } else if (wid == 1 && lane < 32) {
+    // column c of Rg^-1: Rg x = e_c (upper), back substitution
+    const int cc = lane;
+    double x[32];
+#pragma unroll
+    for (int i2 = 31; i2 >= 0; --i2) {
+      double lr2[32];
+#pragma unroll
+      for (int k = i2 + 1; k < 32; ++k) lr2[k] = sm.Lt[i2][k];
+      double acc[4] = {(i2 == cc) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = i2 + 1; k < 32; ++k) acc[k & 3] = fma(-lr2[k], x[k], acc[k & 3]);
+      x[i2] = (i2 <= cc) ? ((acc[0] + acc[1]) + (acc[2] + acc[3])) * sm.rinv[i2] : 0.0;
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 32; ++i2) sm.RgI[i2][cc] = x[i2];
+  }
+  __syncthreads();
+  DBG_STAMP(17)
+  if (wid == 0 && lane < 32) {
+    // T row i: t[a] = u[a] - sum_{b<a} Y1[a][b] t[b]
+    const int i = lane;
+    double t[32], yr[32];
+#pragma unroll
+    for (int a2 = 0; a2 < 32; ++a2) {
+#pragma unroll
+      for (int b2 = 0; b2 < a2; ++b2) yr[b2] = sm.Cq[a2][b2];
+      double acc[4] = {sm.Ut[i][a2], 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int b2 = 0; b2 < a2; ++b2) acc[b2 & 3] = fma(-yr[b2], t[b2], acc[b2 & 3]);
+      t[a2] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int l = 0; l < 32; ++l) sm.Tm[i][l] = t[l];
+  } else if (wid == 1 && lane < 32) {
+    // column c of U^-1 (back substitution)
+    const int cc = lane;
+    double x[32];
+#pragma unroll
+    for (int i2 = 31; i2 >= 0; --i2) {
+      double ur[32];
+#pragma unroll
+      for (int k = i2 + 1; k < 32; ++k) ur[k] = sm.Ut[i2][k];
+      double acc[4] = {(i2 == cc) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = i2 + 1; k < 32; ++k) acc[k & 3] = fma(-ur[k], x[k], acc[k & 3]);
+      x[i2] = (i2 <= cc) ? ((acc[0] + acc[1]) + (acc[2] + acc[3])) * sm.uinv[i2] : 0.0;
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 32; ++i2) UI[i2][cc] = x[i2];
+  } else if (wid == 2 && lane < 32) {
+    // the band block S R and its transpose
+    const int cc = lane;
+#pragma unroll
+    for (int i2 = 0; i2 < 32; ++i2) {
+      const double rv = (i2 <= cc) ? sm.sv[i2] * sm.Ra[i2][cc] : 0.0;
+      g.A[(g.r0 + int64_t(i2)) * g.lda + g.p + cc] = rv;
+      g.A[(g.p + int64_t(cc)) * g.lda + g.r0 + i2] = rv;
+    }
+  }
+  __syncthreads();
+  DBG_STAMP(18)
+  // M1 = Rg^-1 (-S) U^-1 and Y1 T (into Ut: U is no longer needed)
+  if (tid < 32) sm.dsum[tid] = -sm.sv[tid];
+  __syncthreads();
+  mm32<33, 33, 65>(&sm.MB[0][0], &sm.RgI[0][0], &UI[0][0], sm.dsum);
+  mm32<33, 33, 33>(&sm.Ut[0][0], &sm.Cq[0][0], &sm.Tm[0][0], nullptr);
+  __syncthreads();
+  mm32<65, 33, 65>(&sm.MB[0][32], &sm.MB[0][0], &sm.Tm[0][0], nullptr);
+  __syncthreads();
+  DBG_STAMP(19)
+}
+
+// Final pass of the CholeskyQR path: [Y | Y T] = Q_prev [M1 | M1 T] on FP64
+// MFMA (Q_prev = the LDS rows), rows >= 32; workgroup 0's rows < 32 are Y1
+// (from the LU) and Y1 T.  Also zeroes the panel rows >= 32 in A.
+__device__ __forceinline__ void final_rows(const PqrArgs &g, PqrSm &sm, int w) {
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  doublex4 acc[4][4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 4) {
+    double bf[4], af[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) bf[cb] = sm.MB[k0 + lr][16 * cb + lc];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) af[rb] = sm.Xs[64 * wid + 16 * rb + lc][k0 + lr];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+        acc[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[rb], bf[cb], acc[rb][cb], 0, 0, 0);
+  }
+  const int base = w * PT + 64 * wid;
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = base + 16 * rb + lr + 4 * q;
+      if (i < SB_B || i >= g.m) continue;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+        (cb < 2 ? g.Y : g.YT)[int64_t(i) * SB_B + 16 * (cb & 1) + lc] = acc[rb][cb][q];
+    }
+  const int i = w * PT + tid;
+  if (i >= SB_B && i < g.m) {
+    double *ad = g.A + (g.r0 + int64_t(i)) * g.lda + g.p;
+    if ((g.lda & 1) == 0 && (g.p & 1) == 0) {
+#pragma unroll
+      for (int l = 0; l < 16; ++l) reinterpret_cast<double2 *>(ad)[l] = make_double2(0.0, 0.0);
+    } else {
+#pragma unroll
+      for (int l = 0; l < 32; ++l) ad[l] = 0.0;
+    }
+#pragma unroll
+    for (int l = 0; l < 32; ++l) g.A[(g.p + int64_t(l)) * g.lda + g.r0 + i] = 0.0;
+  }
+  if (w == 0 && tid < 2 * SB_B) {
+    // rows 0..31: Y1 (from the LU) and Y1 T (hr_top), 32 columns per lane
+    const int i2 = tid & 31;
+    const double *src = (tid < SB_B) ? &sm.Cq[i2][0] : &sm.Ut[i2][0];
+    double *dst = ((tid < SB_B) ? g.Y : g.YT) + i2 * SB_B;
+#pragma unroll
+    for (int c = 0; c < 32; ++c) dst[c] = src[c];
+  }
+}
+
+// Fallback: Householder QR over the grid, one barrier per column, from the
+// original panel row of each thread (registers); writes Y, Y T, T and [R; 0].
+__device__ __forceinline__ void householder(const PqrArgs &g, PqrSm &sm, int w, unsigned &ep) {
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
+  const int row = w * PT + tid;
+  double a[32];
+  load_row(g, row, a);
+  double(*red)[32] = reinterpret_cast<double(*)[32]>(&sm.Gs[0][0]);
+  double *fpart = g.part + int64_t(g.nw) * 1024;
+  auto step = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    double d[32];
+    const double x = (row > j) ? a[j] : 0.0;  // rows >= m hold zeros
+#pragma unroll
+    for (int l = 0; l < 32; ++l) d[l] = x * a[l];
+    const double s = tg::lanes::reduce_scatter32(d, lane);
+    if ((lane & 1) == 0) red[wid][tg::lanes::rs_col(lane)] = s;
+    __syncthreads();
+    if (tid < 32)
+      st_sc1(fpart + (int64_t(j & 1) * g.nw + w) * 32 + tid,
+             (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
+    if (w == 0 && tid == j) {
+#pragma unroll
+      for (int l = 0; l < 32; ++l) st_sc1(g.bc + BC_PROW + (j & 1) * 32 + l, a[l]);
+    }
+    grid_bar(g, ep);
+    if (tid < 32) {
+      constexpr int NB = 32;
+      double v[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        v[b] = (b < g.nw) ? ld_sc1(fpart + (int64_t(j & 1) * g.nw + b) * 32 + tid) : 0.0;
+      double acc = 0.0;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc += v[b];
+      sm.dsum[tid] = acc;
+      sm.prow[tid] = ld_sc1(g.bc + BC_PROW + (j & 1) * 32 + tid);
+    }
+    __syncthreads();
+    const double sig = sm.dsum[j], alpha = sm.prow[j];
+    double tau = 0.0, scal = 0.0, beta = alpha;
+    if (sig != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sig), alpha);
+      tau = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    const double v = a[j] * scal;
+    const double tv = row > j ? tau * v : (row == j ? tau : 0.0);
+    a[j] = row > j ? v : (row == j ? beta : a[j]);
+#pragma unroll
+    for (int l = j + 1; l < 32; ++l) a[l] = fma(-tv, fma(scal, sm.dsum[l], sm.prow[l]), a[l]);
+    if (w == 0) {
+      if (tid < j) sm.Cq[tid][j] = fma(scal, sm.dsum[tid], sm.prow[tid]);  // (Y^T v_j)_tid
+      if (tid == 0) sm.taus[j] = tau;
+    }
+  };
+  [&]<int... J>(std::integer_sequence<int, J...>) {
+    (step(std::integral_constant<int, J>{}), ...);
+  }(std::make_integer_sequence<int, SB_B>{});
+  __syncthreads();
+  if (w == 0 && tid < 32) {
+    // T (dlarft forward columnwise), row tid; R rows of the band block
+    double trow[32];
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) {
+      double acc = 0.0;
+#pragma unroll
+      for (int c = 0; c < jj; ++c) acc = fma(trow[c], sm.Cq[c][jj], acc);
+      const double tj = sm.taus[jj];
+      trow[jj] = (tid < jj) ? -tj * acc : (tid == jj ? tj : 0.0);
+    }
+#pragma unroll
+    for (int l = 0; l < 32; ++l) {
+      st_sc1(g.bc + BC_T + tid * 32 + l, trow[l]);
+      g.T[tid * 32 + l] = trow[l];
+    }
+    if (tid < g.m) {
+#pragma unroll
+      for (int l = 0; l < 32; ++l) {
+        const double rv = (l >= tid) ? a[l] : 0.0;
+        g.A[(g.r0 + int64_t(tid)) * g.lda + g.p + l] = rv;
+        g.A[(g.p + int64_t(l)) * g.lda + g.r0 + tid] = rv;
+      }
+    }
+  }
+  if (w == 0 && tid == 0)
+    __hip_atomic_store((gu32 *)(g.cnt + 1), unsigned(DEC_FALLBACK * 16), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  grid_bar(g, ep);
+  {
+    double t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = ld_sc1(g.bc + BC_T + tid + PT * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + PT * u;
+      sm.Tm[e >> 5][e & 31] = t[u];
+    }
+    __syncthreads();
+  }
+  if (row < g.m) {
+    double y[32];
+#pragma unroll
+    for (int l = 0; l < 32; ++l) y[l] = (row > l) ? a[l] : (row == l ? 1.0 : 0.0);
+    double2 *yo = reinterpret_cast<double2 *>(g.Y + int64_t(row) * SB_B);
+    double2 *to = reinterpret_cast<double2 *>(g.YT + int64_t(row) * SB_B);
+#pragma unroll
+    for (int c = 0; c < 32; c += 2) {
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int l = 0; l <= c + 1; ++l) {
+        if (l <= c) t0 = fma(y[l], sm.Tm[l][c], t0);
+        t1 = fma(y[l], sm.Tm[l][c + 1], t1);
+      }
+      yo[c / 2] = make_double2(y[c], y[c + 1]);
+      to[c / 2] = make_double2(t0, t1);
+    }
+    if (row >= SB_B) {
+      double *ad = g.A + (g.r0 + int64_t(row)) * g.lda + g.p;
+#pragma unroll
+      for (int l = 0; l < 32; ++l) ad[l] = 0.0;
+#pragma unroll
+      for (int l = 0; l < 32; ++l) g.A[(g.p + int64_t(l)) * g.lda + g.r0 + row] = 0.0;
+    }
+  }
+}
+
+// Out-of-line phases (state in s_pq).  Phase 1: this workgroup's Gram partial.
+__device__ __forceinline__ void ph_gram(int w) { gram_publish(s_pq.ga, s_pq, w); }
+
+__device__ __forceinline__ void ph_bar(unsigned ep) {
+  unsigned e = ep - 1;
+  grid_bar(s_pq.ga, e);
+}
+
+// Workgroup 0 after Gram pass `npass`: sum, Cholesky, decision; on accept the
+// Householder reconstruction and [M1 | M1 T]; publishes what the other
+// workgroups need.  Returns the decision.
+__device__ __forceinline__ int ph_decide(int npass) {
+  PqrSm &sm = s_pq;
+  const PqrArgs &g = sm.ga;
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
+  const int dk = npass == 1 ? 0 : 8;
+  DBG_STAMP(dk + 0)
+  gram_reduce(g, sm);
+  __syncthreads();
+  DBG_STAMP(dk + 1)
+  if (wid == 0) {
+    double delta = 0.0;
+    if (npass >= 2) {
+      for (int e = lane; e < 1024; e += 64)
+        delta = fmax(delta, fabs(sm.Gs[e >> 5][e & 31] - ((e >> 5) == (e & 31) ? 1.0 : 0.0)));
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) delta = fmax(delta, __shfl_xor(delta, off));
+    }
+    double mr = 0.0;
+    bool ok = chol32_ool(0.0, mr);
+    if (npass == 1 && (!ok || mr < 1e-12)) {
+      double tr = 0.0;
+      for (int c = 0; c < 32; ++c) tr += sm.Gs[c][c];
+      const double shift = 11.0 * (double(g.m) * 32.0 + 32.0 * 33.0) * (0.5 * DBL_EPSILON) * tr;
+      ok = chol32_ool(shift, mr);
+    }
+    const int d = !ok ? DEC_FALLBACK
+                      : (npass >= 2 && delta < 0.1) ? DEC_ACCEPT
+                                                    : (npass >= NPASS ? DEC_FALLBACK : DEC_CONTINUE);
+    if (lane == 0) sm.dec = d;
+  }
+  __syncthreads();
+  DBG_STAMP(dk + 2)
+  const int d = sm.dec;
+  if (d != DEC_FALLBACK) {
+    // Ra <- L^T Ra (upper triangular product; Lt is L^T), via RgI
+    if (npass == 1) {
+      for (int e = tid; e < 1024; e += PT) sm.Ra[e >> 5][e & 31] = sm.Lt[e >> 5][e & 31];
+    } else {
+      mm32<33, 33, 33>(&sm.RgI[0][0], &sm.Lt[0][0], &sm.Ra[0][0], nullptr);
+      __syncthreads();
+      for (int e = tid; e < 1024; e += PT) sm.Ra[e >> 5][e & 31] = sm.RgI[e >> 5][e & 31];
+    }
+    __syncthreads();
+  }
+  DBG_STAMP(dk + 3)
+  if (d == DEC_ACCEPT) {
+    // final Q top rows (rows 0..31 = threads 0..31)
+    if (tid < 32) {
+      double x[32];
+      row_from_lds(&sm.Xs[tid][0], x);
+      trsm_row(x, sm.Lt, sm.rinv);
+#pragma unroll
+      for (int l = 0; l < 32; ++l) sm.Cq[tid][l] = x[l];
+    }
+    __syncthreads();
+    DBG_STAMP(dk + 4)
+    hr_top_ool();
+    DBG_STAMP(dk + 5)
+    for (int e = tid; e < 2048; e += PT) st_sc1(g.bc + BC_MB + e, sm.MB[e >> 6][e & 63]);
+    for (int e = tid; e < 1024; e += PT) g.T[e] = sm.Tm[e >> 5][e & 31];
+  }
+  if (d == DEC_CONTINUE) {
+    for (int e = tid; e < 1024; e += PT) st_sc1(g.bc + BC_L + e, sm.Lt[e >> 5][e & 31]);
+    if (tid < 32) st_sc1(g.bc + BC_RINV + tid, sm.rinv[tid]);
+  }
+  DBG_STAMP(dk + 6)
+  if (tid == 0) {
+    st_sc1(g.bc + BC_DEC, double(d));
+    __hip_atomic_store((gu32 *)(g.cnt + 1), unsigned(d * 16 + npass), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return d;
+}
+
+// Every workgroup but 0: this pass's L; then Q <- Q L^-T on the LDS rows.
+__device__ __forceinline__ void ph_apply(int w) {
+  PqrSm &sm = s_pq;
+  const PqrArgs &g = sm.ga;
+  const int tid = otid();
+  if (w != 0) {
+    double t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = ld_sc1(g.bc + BC_L + tid + PT * u);
+    const double ri = tid < 32 ? ld_sc1(g.bc + BC_RINV + tid) : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + PT * u;
+      sm.Lt[e >> 5][e & 31] = t[u];
+    }
+    if (tid < 32) sm.rinv[tid] = ri;
+    __syncthreads();
+  }
+  double x[32];
+  row_from_lds(&sm.Xs[tid][0], x);
+  trsm_row(x, sm.Lt, sm.rinv);
+  row_to_lds(&sm.Xs[tid][0], x);
+  __syncthreads();
+}
+
+__device__ __forceinline__ void ph_final(int w) {
+  PqrSm &sm = s_pq;
+  const PqrArgs &g = sm.ga;
+  const int tid = otid();
+  if (w != 0) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = ld_sc1(g.bc + BC_MB + tid + PT * u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + PT * u;
+      sm.MB[e >> 6][e & 63] = t[u];
+    }
+    __syncthreads();
+  }
+  final_rows(g, sm, w);
+}
+
+__device__ __noinline__ void ph_householder(int w, unsigned ep) {
+  unsigned e = ep;
+  householder(s_pq.ga, s_pq, w, e);
+}
+
+__global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
+  PqrSm &sm = s_pq;
+  if (blockIdx.x % 8 != 0) return;  // workers: one per 8 (one XCD under round-robin)
+  const int w = blockIdx.x / 8;
+  const int tid = otid();
+  if (tid == 0) sm.ga = ga;
+  unsigned ep = 0;
+  int nst = 0;
+  auto stamp = [&]() {
+    if (ga.stats && w == 0 && tid == 0 && nst < 15) ga.stats[nst] = __builtin_amdgcn_s_memrealtime();
+    ++nst;
+  };
+  stamp();
+  int dec = (ga.m < FB_MIN_M) ? DEC_FALLBACK : DEC_CONTINUE;
+  if (dec == DEC_CONTINUE) {
+    double x[32];
+    load_row(ga, w * PT + tid, x);
+    row_to_lds(&sm.Xs[tid][0], x);
+  }
+  __syncthreads();
+  int npass = 0;
+  while (dec == DEC_CONTINUE) {
+    ph_gram(w);
+    stamp();
+    ph_bar(++ep);
+    stamp();
+    ++npass;
+    if (w == 0) ph_decide(npass);
+    stamp();
+    ph_bar(++ep);
+    stamp();
+    dec = int(ld_sc1(ga.bc + BC_DEC));
+    if (dec == DEC_ACCEPT) {
+      ph_final(w);
+      stamp();
+      return;
+    }
+    if (dec == DEC_CONTINUE) ph_apply(w);
+  }
+  ph_householder(w, ep);
+}
+
+}  // namespace
+
+namespace tg {
+
+int pqr_rows_per_thread(int m) { return m <= PQR_NWMAX * PT ? 1 : 0; }
+
+hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
+                    double *YT, double *T, double *part, double *bc, unsigned *cnt,
+                    unsigned *tmo) {
+  if (m < 1 || pqr_rows_per_thread(m) == 0) return hipErrorInvalidValue;
+  PqrArgs g{};
+  g.A = A;
+  g.lda = lda;
+  g.p = p;
+  g.r0 = r0;
+  g.m = m;
+  g.nw = cdiv(m, PT);
+  g.Y = Y;
+  g.YT = YT;
+  g.T = T;
+  g.part = part;
+  g.bc = bc;
+  g.cnt = cnt;
+  g.tmo = tmo;
+  static const unsigned long long tmo_ticks = [] {
+    const char *tt = getenv("TG_PQR_TIMEOUT_TICKS");
+    return tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
+  }();
+  g.timeout = tmo_ticks;
+  static unsigned long long *stats = nullptr;
+  static int nstat = 0;
+  static double acc[16] = {0};
+  if (getenv("TG_PQR_STATS")) {
+    if (!stats) {
+      (void)hipMalloc(&stats, 16 * sizeof(unsigned long long));
+      atexit([] {
+        if (nstat == 0) return;
+        fprintf(stderr, "pqr phases (us, mean of %d accepted 2-pass panels):", nstat);
+        for (int i = 1; i < 10; ++i) fprintf(stderr, " %.2f", acc[i] / nstat / 100.0);
+        fprintf(stderr, "\n");
+      });
+    }
+    (void)hipMemsetAsync(stats, 0, 16 * sizeof(unsigned long long), st);
+    g.stats = stats;
+  }
+  // 2 Gram passes + the row solve and the final [Y | YT] product: ~10 m 32^2 flops
+  auto tok = prof_begin(st, PROF_TSQR, 8.0 * m * SB_B * 3, 10.0 * m * SB_B * SB_B);
+  hipLaunchKernelGGL(pqr_kernel, dim3(8 * g.nw), dim3(PT), 0, st, g);
+  prof_end(st, tok);
+  if (g.stats) {
+    unsigned long long h[16];
+    (void)hipMemcpyAsync(h, g.stats, sizeof(h), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    if (h[9] != 0 && h[10] == 0) {
+      for (int i = 1; i < 10; ++i) acc[i] += double(h[i] - h[i - 1]);
+      ++nstat;
+    }
+#ifdef TG_PQR_DBG
+    static int ndbg = 0;
+    if (++ndbg == 300) {
+      unsigned long long d[64];
+      (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_pq_dbg), sizeof(d));
+      fprintf(stderr, "pqr decide sub-phases (us, sums over launches): p1 reduce %.1f chol %.1f ra %.1f pub %.1f | p2 reduce %.1f chol %.1f ra %.1f cq %.1f hr %.1f pub %.1f\n",
+              (d[1] - d[0]) / 100.0, (d[2] - d[1]) / 100.0, (d[3] - d[2]) / 100.0, (d[6] - d[3]) / 100.0,
+              (d[9] - d[8]) / 100.0, (d[10] - d[9]) / 100.0, (d[11] - d[10]) / 100.0,
+              (d[12] - d[11]) / 100.0, (d[13] - d[12]) / 100.0, (d[14] - d[13]) / 100.0);
+      fprintf(stderr, "  hr: LU||RgI %.1f  T||UI||R %.1f  M1+Y1T %.1f  (sums)\n", (d[17] - d[16]) / 100.0,
+              (d[18] - d[17]) / 100.0, (d[19] - d[18]) / 100.0);
+    }
+#endif
+  }
+  return hipGetLastError();
+}
+
+}  // namespace tg
