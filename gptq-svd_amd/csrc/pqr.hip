@@ -64,6 +64,7 @@ struct PqrArgs {
   unsigned *tmo;       // timeout flag (shared by all panels)
   unsigned long long timeout;
   unsigned long long *stats;  // TG_PQR_STATS: per-phase clock stamps of workgroup 0 (or null)
+  int force_fb;               // TG_PQR_FALLBACK=1: every panel through the Householder path (tests)
 };
 
 struct PqrSm {
@@ -92,8 +93,11 @@ __shared__ PqrSm s_pq;
 __device__ unsigned long long g_pq_dbg[64];
 #define DBG_STAMP(k) \
   if (threadIdx.x == 0) g_pq_dbg[(k)] += __builtin_amdgcn_s_memrealtime();
+#define DBG_STAMP_T(k, t) \
+  if (threadIdx.x == (t)) g_pq_dbg[(k)] += __builtin_amdgcn_s_memrealtime();
 #else
 #define DBG_STAMP(k)
+#define DBG_STAMP_T(k, t)
 #endif
 
 // threadIdx.x through an empty asm: every phase derives its lane indices and
@@ -279,8 +283,10 @@ __device__ __forceinline__ void gram_reduce(const PqrArgs &g, PqrSm &sm) {
 
 // One wave: L = chol(Gs + shift I) into Lt (Lt[c][i] = L[i][c]) and rinv;
 // lane (i = lane & 31, h = lane >> 5) holds row i, columns 16h .. 16h + 15;
-// column j is broadcast through LDS at each step.  ok: every pivot positive
-// and finite; minrat = min_j pivot_j / (G_jj + shift).
+// column j is broadcast through LDS at each step.  The pivot chain is kept
+// free of compares and selects (lanes above the pivot compute unused upper
+// entries); ok (every pivot positive and finite) and minrat = min_j
+// pivot_j / (G_jj + shift) are evaluated once at the end from L's diagonal.
 __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
   PqrSm &sm = s_pq;
   const int lane = otid() & 63, i = lane & 31, h = lane >> 5;
@@ -288,15 +294,13 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
   double gr[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) gr[c] = sm.Gs[i][16 * h + c] + (16 * h + c == i ? shift : 0.0);
-  bool ok = true;
-  double mr = 1.0;
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     const int hj = j >> 4, cj = j & 15;
     // lanes of column j publish it; the others write a slot nobody reads
     buf[h == hj ? i : 32 + lane] = gr[cj];
     wave_lds_sync();
-    double piv = buf[j];
+    const double piv = buf[j];
     const double gij = buf[i];
     double col[16];
     const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
@@ -307,13 +311,8 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
       col[2 * c + 1] = v.y;
     }
     wave_lds_sync();
-    if (!(piv > 0.0) || !(piv <= DBL_MAX)) {
-      ok = false;
-      piv = 1.0;
-    }
-    mr = fmin(mr, piv * rcp_nr(sm.Gs[j][j] + shift));
     const double r = rsq_nr(piv);
-    const double lij = (i > j) ? gij * r : (i == j ? piv * r : 0.0);
+    const double lij = gij * r;  // L[i][j] for i >= j (i == j: sqrt(piv))
     if (h == hj) gr[cj] = lij;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -327,9 +326,16 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
     sm.Lt[16 * h + c][i] = (16 * h + c <= i) ? gr[c] : 0.0;
     dg = (16 * h + c == i) ? gr[c] : dg;
   }
-  if ((i >> 4) == h) sm.rinv[i] = rcp_nr(dg);
-  minrat = mr;
-  return ok;
+  // lane i (its diagonal half): L_ii > 0 finite, pivot ratio L_ii^2 / (G_ii + shift)
+  const bool mine = (i >> 4) == h;
+  if (mine) sm.rinv[i] = rcp_nr(dg);
+  const bool good = !mine || (dg > 0.0 && dg <= DBL_MAX);
+  double rat = mine ? dg * dg / (sm.Gs[i][i] + shift) : 1.0;
+  if (!(rat == rat)) rat = 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rat = fmin(rat, __shfl_xor(rat, off));
+  minrat = rat;
+  return __all(good);
 }
 
 // Workgroup 0 after acceptance (Cq = top 32 rows of the final Q, Lt = this
@@ -373,10 +379,11 @@ __device__ __forceinline__ void hr_top_ool() {
         rw[2 * l + 1] = v.y;
       }
       wave_lds_sync();
-      const double s = (qjj >= 0.0) ? -1.0 : 1.0;
+      // S_jj = -sign(C_jj) (as a sign copy, no compare on the chain)
+      const double ms = copysign(1.0, qjj);
       const double ru = rcp_nr(1.0 + fabs(qjj));
-      if (lane == 0) sm.sv[j] = s;
-      const double lij = -s * cij * ru;
+      if (lane == 0) sm.sv[j] = -ms;
+      const double lij = ms * cij * ru;
       if (i > j && h == hj) c[cj] = lij;
 #pragma unroll
       for (int l = 0; l < 16; ++l) {
@@ -385,6 +392,7 @@ __device__ __forceinline__ void hr_top_ool() {
       }
     }
     wave_lds_sync();
+    DBG_STAMP_T(20, 0)
 #pragma unroll
     for (int l = 0; l < 16; ++l) {
       const int col = 16 * h + l;
@@ -409,6 +417,7 @@ __device__ __forceinline__ void hr_top_ool() {
     }
 #pragma unroll
     for (int i2 = 0; i2 < 32; ++i2) sm.RgI[i2][cc] = x[i2];
+    DBG_STAMP_T(21, 64)
   }
   __syncthreads();
   DBG_STAMP(17)
@@ -798,7 +807,7 @@ __global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
     ++nst;
   };
   stamp();
-  int dec = (ga.m < FB_MIN_M) ? DEC_FALLBACK : DEC_CONTINUE;
+  int dec = (ga.m < FB_MIN_M || ga.force_fb) ? DEC_FALLBACK : DEC_CONTINUE;
   if (dec == DEC_CONTINUE) {
     double x[32];
     load_row(ga, w * PT + tid, x);
@@ -856,6 +865,10 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
     return tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
   }();
   g.timeout = tmo_ticks;
+  {
+    const char *fb = getenv("TG_PQR_FALLBACK");
+    g.force_fb = (fb && fb[0] == '1') ? 1 : 0;
+  }
   static unsigned long long *stats = nullptr;
   static int nstat = 0;
   static double acc[16] = {0};
@@ -893,8 +906,9 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
               (d[1] - d[0]) / 100.0, (d[2] - d[1]) / 100.0, (d[3] - d[2]) / 100.0, (d[6] - d[3]) / 100.0,
               (d[9] - d[8]) / 100.0, (d[10] - d[9]) / 100.0, (d[11] - d[10]) / 100.0,
               (d[12] - d[11]) / 100.0, (d[13] - d[12]) / 100.0, (d[14] - d[13]) / 100.0);
-      fprintf(stderr, "  hr: LU||RgI %.1f  T||UI||R %.1f  M1+Y1T %.1f  (sums)\n", (d[17] - d[16]) / 100.0,
-              (d[18] - d[17]) / 100.0, (d[19] - d[18]) / 100.0);
+      fprintf(stderr, "  hr: LU||RgI %.1f  T||UI||R %.1f  M1+Y1T %.1f  (sums); LU %.1f RgI %.1f\n",
+              (d[17] - d[16]) / 100.0, (d[18] - d[17]) / 100.0, (d[19] - d[18]) / 100.0,
+              (d[20] - d[16]) / 100.0, (d[21] - d[16]) / 100.0);
     }
 #endif
   }
