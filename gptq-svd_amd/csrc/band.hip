@@ -839,6 +839,53 @@ __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y
   if (tid == 0) *ticket = 0u;
 }
 
+// Look-ahead strip of the single-level update: the first 32 columns of A22
+// (and their transpose) get  A22 -= Y X^T + X Y^T - Y S Y^T  (S = (M + M^T)/2)
+// ahead of the rest, so the next panel can be factored while syr2k_bs_kernel
+// updates A22[32:, 32:].  Delta[i][j] = Y_i . (X_j - S Y_j) + X_i . Y_j;
+// the 32 x 32 corner is computed for i >= j and mirrored (bitwise symmetric).
+__global__ __launch_bounds__(256) void strip_update_kernel(double *__restrict__ A, int64_t lda,
+                                                           int m, const double *__restrict__ Y,
+                                                           const double *__restrict__ X,
+                                                           const double *__restrict__ M) {
+  __shared__ double Ss[SB_B][SB_B + 1], Wj[SB_B][SB_B + 1], Yj[SB_B][SB_B + 1];
+  const int tid = threadIdx.x;
+  const int nj = min(SB_B, m);
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    const int x = e >> 5, y = e & 31;
+    Ss[x][y] = 0.5 * (M[x * SB_B + y] + M[y * SB_B + x]);
+    Yj[x][y] = x < nj ? Y[x * SB_B + y] : 0.0;
+  }
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    const int j = e >> 5, l = e & 31;  // W_j = X_j - S Y_j
+    double z = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < SB_B; ++k) z = fma(Ss[l][k], Yj[j][k], z);
+    Wj[j][l] = (j < nj ? X[j * SB_B + l] : 0.0) - z;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 64 + (tid >> 2), j0 = (tid & 3) * 8;
+  if (i >= m) return;
+  double yi[SB_B], xi[SB_B];
+#pragma unroll
+  for (int l = 0; l < SB_B; ++l) {
+    yi[l] = Y[int64_t(i) * SB_B + l];
+    xi[l] = X[int64_t(i) * SB_B + l];
+  }
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int j = j0 + jj;
+    if (j >= nj || (i < SB_B && j > i)) continue;
+    double d = 0.0;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) d = fma(yi[l], Wj[j][l], fma(xi[l], Yj[j][l], d));
+    const double v = A[int64_t(i) * lda + j] - d;
+    A[int64_t(i) * lda + j] = v;
+    if (i != j) A[int64_t(j) * lda + i] = v;
+  }
+}
+
 // A[r0+i][p+l] = [R; 0] and the transpose (i < m, l < 32).
 __global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, int r0, int m,
                                    const double *__restrict__ R) {
@@ -887,16 +934,34 @@ static hipError_t side_stream(SideStream *&out) {
 }
 
 // One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
+// Look-ahead (TG_SB_LOOKAHEAD=1; off by default: measured +5 ms at n = 4096,
+// the panel QR's workgroups need a whole CU's LDS and wait for the trailing
+// update to drain, so nothing overlaps and the events cost): after M, the strip kernel
+// updates the next panel's 32 columns (and rows), the side stream factors the
+// next panel while syr2k_bs_kernel updates A22[32:, 32:] on the main stream;
+// the next X waits for both.  Buffers: YT is only read by X (done before the
+// next panel QR writes it); X, M, U and the partials are main-stream only
+// while the side stream runs (the panel QR's partials region is idle then).
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
-  int pi = 0;
-  for (const SbPanel &P : pl.panels) {
-    const int m = P.m, r0 = P.r0;
+  const char *la = getenv("TG_SB_LOOKAHEAD");
+  const bool look = la && la[0] == '1';
+  SideStream *ss = nullptr;
+  if (look) TG_CHK(side_stream(ss));
+  const int np = int(pl.panels.size());
+  auto pqr = [&](hipStream_t s, int pi) {
+    const SbPanel &P = pl.panels[pi];
+    return panel_qr(s, A, lda, P.p, P.r0, P.m, b.Y + P.L[0].yoff, b.YT, b.T + P.L[0].toff,
+                    b.pq_part, b.pq_bc, b.pq_ctl + 4 + 4 * pi, b.pq_ctl);
+  };
+  if (np > 0) TG_CHK(pqr(st, 0));
+  for (int pi = 0; pi < np; ++pi) {
+    const SbPanel &P = pl.panels[pi];
+    const int m = P.m, r0 = P.r0, ph = pi & 1;
     double *A22 = A + int64_t(r0) * lda + r0;
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
-    TG_CHK(panel_qr(st, A, lda, P.p, r0, m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
-                    b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
+    if (look && pi > 0) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));  // panel QR pi done
     // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
     const int nz = std::max(1, m / SB_C);
     ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
@@ -906,13 +971,34 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 256)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
                        b.pq_part, b.pq_ctl + 1);
     TG_CHK(hipGetLastError());
-    const int nt = cdiv(m, S2T);
-    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
-    hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                       int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
-    prof_end(st, tok);
-    TG_CHK(hipGetLastError());
-    ++pi;
+    const bool next = pi + 1 < np;
+    if (look && next) {
+      hipLaunchKernelGGL(strip_update_kernel, dim3(cdiv(m, 64)), dim3(256), 0, st, A22,
+                         int64_t(lda), m, Yp, b.X, b.M);
+      TG_CHK(hipGetLastError());
+      TG_CHK(hipEventRecord(ss->ev0[ph], st));
+      TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[ph], 0));
+      TG_CHK(pqr(ss->s, pi + 1));
+      TG_CHK(hipEventRecord(ss->ev1[ph ^ 1], ss->s));
+      const int mr = m - SB_B;
+      if (mr > 0) {
+        const int nt = cdiv(mr, S2T);
+        auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(mr) * mr, 96.0 * double(mr) * mr);
+        hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st,
+                           A22 + int64_t(SB_B) * lda + SB_B, int64_t(lda), mr, mr, 1,
+                           Yp + SB_B * SB_B, b.X + SB_B * SB_B, int64_t(SB_B), b.M, int64_t(SB_B));
+        prof_end(st, tok);
+        TG_CHK(hipGetLastError());
+      }
+    } else {
+      const int nt = cdiv(m, S2T);
+      auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
+      hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                         int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+      prof_end(st, tok);
+      TG_CHK(hipGetLastError());
+      if (next) TG_CHK(pqr(st, pi + 1));
+    }
   }
   return hipSuccess;
 }
