@@ -818,22 +818,31 @@ __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y
   __syncthreads();
   if (!tg::publish_partials(Ps, SB_B * SB_B, part, ticket)) return;
   const int G = int(gridDim.x);
-  for (int e = tid; e < SB_B * SB_B; e += 256) {
-    double v = 0.0;
-    for (int g0 = 0; g0 < G; g0 += 8) {
-      double t[8];
+  {
+    // all of this thread's partials in flight at once (G <= 16 per batch)
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int g0 = 0; g0 < G; g0 += 16) {
+      double t[4][16];
 #pragma unroll
-      for (int b = 0; b < 8; ++b) t[b] = g0 + b < G ? tg::load_partial(&part[size_t(e) * G + g0 + b]) : 0.0;
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) v += t[b];
+        for (int b = 0; b < 16; ++b)
+          t[u][b] = tg::load_partial(&part[size_t(tid + 256 * u) * G + min(g0 + b, G - 1)]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int b = 0; b < 16; ++b) v[u] += (g0 + b < G) ? t[u][b] : 0.0;
     }
-    red[0][e >> 5][e & 31] = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[0][(tid + 256 * u) >> 5][(tid + 256 * u) & 31] = v[u];
   }
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 256) Ps[e] = T[e];  // T staged in LDS
   __syncthreads();
   for (int e = tid; e < SB_B * SB_B; e += 256) {
     const int a = e >> 5, c = e & 31;
     double v = 0.0;
-    for (int k = 0; k <= a; ++k) v = fma(T[k * SB_B + a], red[0][k][c], v);
+    for (int k = 0; k <= a; ++k) v = fma(Ps[k * SB_B + a], red[0][k][c], v);
     M[e] = v;
   }
   if (tid == 0) *ticket = 0u;

@@ -42,6 +42,7 @@ constexpr int PT = 256;    // threads per workgroup (4 waves) = rows per workgro
 constexpr int XS = 34;     // row stride of the LDS row block (16-B aligned rows)
 constexpr int NPASS = 4;   // Gram passes before the Householder fallback
 constexpr int FB_MIN_M = 64;
+constexpr double SERIES_TOL = 1e-5;  // |G - I| below which the last factor is a series
 
 enum Dec { DEC_CONTINUE = 1, DEC_ACCEPT = 2, DEC_FALLBACK = 3 };
 
@@ -78,6 +79,7 @@ struct PqrSm {
   double MB[32][65];          // [M1 | M1 T] of the final CholeskyQR pass
   double rinv[32], uinv[32], sv[32];
   double dsum[32], prow[32], taus[32];
+  double delta;
   double bcast[2][128];        // one-wave broadcast rows (+ a trash slot per lane)
   int dec;
   PqrArgs ga;                 // the launch arguments (read by the out-of-line phases)
@@ -338,20 +340,63 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
   return __all(good);
 }
 
-// Workgroup 0 after acceptance (Cq = top 32 rows of the final Q, Lt = this
-// pass's factor, Ra = L_g^T ... L_1^T):
-//   wave 0: LU of I - Cq S (Householder reconstruction): U, Y1 (into Cq), S;
-//   wave 1: Rg^-1 (Rg = Lt as a matrix);
-// then T (T Y1^T = U), U^-1 (into Gs), the band block S R written to A, and
-//   MB = [M1 | M1 T],  M1 = Rg^-1 (-S) U^-1,
-// so that a row q of the previous pass gives Y = q M1, Y T = q M1 T.
-__device__ __forceinline__ void hr_top_ool() {
+// X = R^-1 for a 32 x 32 upper triangular R = get(i, k) (i <= k) with
+// reciprocal diagonal rd (unit: rd = null), by blocks: the four 8 x 8
+// diagonal blocks by back substitution (one thread per column), then two
+// levels of  X12 = -A^-1 B D^-1.  All threads of the workgroup; X is LDS
+// (stride 33), lower part zeroed; `tmp` is 32 x 33 LDS scratch.
+template <class Get>
+__device__ __forceinline__ void trinv_upper32(Get get, const double *rd, double (*X)[33],
+                                              double (*tmp)[33]) {
+  const int tid = otid();
+  for (int e = tid; e < 1024; e += PT) X[e >> 5][e & 31] = 0.0;
+  __syncthreads();
+  if (tid < 32) {
+    const int bb = 8 * (tid >> 3), c = tid & 7;
+    double x[8];
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      double acc = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = i + 1; k < 8; ++k) acc = fma(-get(bb + i, bb + k), x[k], acc);
+      x[i] = (i <= c) ? acc * (rd ? rd[bb + i] : 1.0) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) X[bb + i][bb + c] = x[i];
+  }
+  __syncthreads();
+  // level 1 (16 x 16 blocks at 0 and 16): T1 = B D^-1, then X12 = -A^-1 T1
+#pragma unroll
+  for (int lev = 0; lev < 2; ++lev) {
+    const int hb = lev == 0 ? 8 : 16;        // half block size
+    const int nblk = lev == 0 ? 2 : 1;       // blocks of size 2 hb
+    const int cnt = nblk * hb * hb;
+    if (tid < cnt) {
+      const int blk = tid / (hb * hb), r = (tid / hb) % hb, c = tid % hb;
+      const int o = blk * 2 * hb;
+      double acc = 0.0;
+      for (int k = 0; k <= c; ++k) acc = fma(get(o + r, o + hb + k), X[o + hb + k][o + hb + c], acc);
+      tmp[o + r][o + hb + c] = acc;
+    }
+    __syncthreads();
+    if (tid < cnt) {
+      const int blk = tid / (hb * hb), r = (tid / hb) % hb, c = tid % hb;
+      const int o = blk * 2 * hb;
+      double acc = 0.0;
+      for (int k = r; k < hb; ++k) acc = fma(X[o + r][o + k], tmp[o + k][o + hb + c], acc);
+      X[o + r][o + hb + c] = -acc;
+    }
+    __syncthreads();
+  }
+}
+
+// Wave 0 of workgroup 0: LU of I - Cq S (Householder reconstruction) into
+// Ut (U), Cq (Y1, unit lower), sv (S), uinv; out of line so that its pivot
+// chain is scheduled on its own.
+__device__ __forceinline__ void lu_hr() {
   PqrSm &sm = s_pq;
-  const PqrArgs &g = sm.ga;
-  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
-  double(*UI)[33] = sm.Gs;
-  DBG_STAMP(16)
-  if (wid == 0) {
+  const int lane = otid() & 63;
+  {
     const int i = lane & 31, h = lane >> 5;
     double *buf = sm.bcast[0], *cbuf = sm.bcast[1];
     double c[16];
@@ -400,77 +445,65 @@ __device__ __forceinline__ void hr_top_ool() {
       sm.Cq[i][col] = (col < i) ? c[l] : (col == i ? 1.0 : 0.0);
       if (col == i) sm.uinv[i] = rcp_nr(1.0 + fabs(c[l]));
     }
-  } else if (wid == 1 && lane < 32) {
-    // column c of Rg^-1: Rg x = e_c (upper), back substitution
-    const int cc = lane;
-    double x[32];
-#pragma unroll
-    for (int i2 = 31; i2 >= 0; --i2) {
-      double lr2[32];
-#pragma unroll
-      for (int k = i2 + 1; k < 32; ++k) lr2[k] = sm.Lt[i2][k];
-      double acc[4] = {(i2 == cc) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k = i2 + 1; k < 32; ++k) acc[k & 3] = fma(-lr2[k], x[k], acc[k & 3]);
-      x[i2] = (i2 <= cc) ? ((acc[0] + acc[1]) + (acc[2] + acc[3])) * sm.rinv[i2] : 0.0;
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int i2 = 0; i2 < 32; ++i2) sm.RgI[i2][cc] = x[i2];
-    DBG_STAMP_T(21, 64)
   }
+}
+
+// Workgroup 0 after acceptance (Lt = this pass's factor L_g, Ra = L_g^T ...
+// L_1^T, the LDS rows = Q_{g-1}):
+//   RgI = (L_g^T)^-1 (trinv_upper32), Cq = the final Q's top rows = Xs[0:32] RgI;
+//   wave 0: LU of I - Cq S (Householder reconstruction): U, Y1 (into Cq), S;
+//   U^-1 and Y1^-T (trinv_upper32), T = U Y1^-T, the band block S R written
+//   to A, MB = [M1 | M1 T] with M1 = RgI (-S) U^-1, and Y1 T (into Ut)
+// so that a row q of the previous pass gives Y = q M1, Y T = q M1 T.
+__device__ __forceinline__ void hr_top_ool() {
+  PqrSm &sm = s_pq;
+  const PqrArgs &g = sm.ga;
+  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
+  double(*UI)[33] = sm.Gs;
+  double(*Tmp)[33] = reinterpret_cast<double(*)[33]>(&sm.MB[0][0]);  // MB is written last
+  DBG_STAMP(16)
+  if (sm.delta <= SERIES_TOL) {
+    // R = I + F with |F| <= ~1e-5: R^-1 = I - F + F^2 - F^3 (error |F|^4)
+    for (int e = tid; e < 1024; e += PT) {
+      const int i2 = e >> 5, j2 = e & 31;
+      sm.Ut[i2][j2] = sm.Lt[i2][j2] - (i2 == j2 ? 1.0 : 0.0);  // F
+    }
+    __syncthreads();
+    mm32<33, 33, 33>(&sm.Cq[0][0], &sm.Ut[0][0], &sm.Ut[0][0], nullptr);  // F^2
+    __syncthreads();
+    mm32<33, 33, 33>(&Tmp[0][0], &sm.Cq[0][0], &sm.Ut[0][0], nullptr);  // F^3
+    __syncthreads();
+    for (int e = tid; e < 1024; e += PT) {
+      const int i2 = e >> 5, j2 = e & 31;
+      sm.RgI[i2][j2] = (i2 == j2 ? 1.0 : 0.0) - sm.Ut[i2][j2] + sm.Cq[i2][j2] - Tmp[i2][j2];
+    }
+    __syncthreads();
+  } else {
+    trinv_upper32([&](int i, int k) { return sm.Lt[i][k]; }, sm.rinv, sm.RgI, Tmp);
+  }
+  mm32<XS, 33, 33>(&sm.Cq[0][0], &sm.Xs[0][0], &sm.RgI[0][0], nullptr);
+  __syncthreads();
+  if (wid == 0) lu_hr();
   __syncthreads();
   DBG_STAMP(17)
-  if (wid == 0 && lane < 32) {
-    // T row i: t[a] = u[a] - sum_{b<a} Y1[a][b] t[b]
-    const int i = lane;
-    double t[32], yr[32];
-#pragma unroll
-    for (int a2 = 0; a2 < 32; ++a2) {
-#pragma unroll
-      for (int b2 = 0; b2 < a2; ++b2) yr[b2] = sm.Cq[a2][b2];
-      double acc[4] = {sm.Ut[i][a2], 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int b2 = 0; b2 < a2; ++b2) acc[b2 & 3] = fma(-yr[b2], t[b2], acc[b2 & 3]);
-      t[a2] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int l = 0; l < 32; ++l) sm.Tm[i][l] = t[l];
-  } else if (wid == 1 && lane < 32) {
-    // column c of U^-1 (back substitution)
-    const int cc = lane;
-    double x[32];
-#pragma unroll
-    for (int i2 = 31; i2 >= 0; --i2) {
-      double ur[32];
-#pragma unroll
-      for (int k = i2 + 1; k < 32; ++k) ur[k] = sm.Ut[i2][k];
-      double acc[4] = {(i2 == cc) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k = i2 + 1; k < 32; ++k) acc[k & 3] = fma(-ur[k], x[k], acc[k & 3]);
-      x[i2] = (i2 <= cc) ? ((acc[0] + acc[1]) + (acc[2] + acc[3])) * sm.uinv[i2] : 0.0;
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int i2 = 0; i2 < 32; ++i2) UI[i2][cc] = x[i2];
-  } else if (wid == 2 && lane < 32) {
-    // the band block S R and its transpose
-    const int cc = lane;
-#pragma unroll
-    for (int i2 = 0; i2 < 32; ++i2) {
-      const double rv = (i2 <= cc) ? sm.sv[i2] * sm.Ra[i2][cc] : 0.0;
-      g.A[(g.r0 + int64_t(i2)) * g.lda + g.p + cc] = rv;
-      g.A[(g.p + int64_t(cc)) * g.lda + g.r0 + i2] = rv;
-    }
+  // the band block S R (lower storage: the upper part of A is never read again)
+  for (int e = tid; e < 1024; e += PT) {
+    const int i2 = e >> 5, cc = e & 31;
+    g.A[(g.r0 + int64_t(i2)) * g.lda + g.p + cc] = (i2 <= cc) ? sm.sv[i2] * sm.Ra[i2][cc] : 0.0;
   }
+  trinv_upper32([&](int i, int k) { return sm.Ut[i][k]; }, sm.uinv, UI, Tmp);
+  // Y1^-T = (Y1^T)^-1 (unit upper), into RgI's slot? RgI is still needed: use Tm for it
+  trinv_upper32([&](int i, int k) { return sm.Cq[k][i]; }, nullptr, sm.Tm, Tmp);
   __syncthreads();
   DBG_STAMP(18)
-  // M1 = Rg^-1 (-S) U^-1 and Y1 T (into Ut: U is no longer needed)
   if (tid < 32) sm.dsum[tid] = -sm.sv[tid];
+  // T = U Y1^-T (into Tmp, then Tm), M1 = RgI (-S) U^-1
+  mm32<33, 33, 33>(&Tmp[0][0], &sm.Ut[0][0], &sm.Tm[0][0], nullptr);
+  __syncthreads();
+  for (int e = tid; e < 1024; e += PT) sm.Tm[e >> 5][e & 31] = Tmp[e >> 5][e & 31];
   __syncthreads();
   mm32<33, 33, 65>(&sm.MB[0][0], &sm.RgI[0][0], &UI[0][0], sm.dsum);
-  mm32<33, 33, 33>(&sm.Ut[0][0], &sm.Cq[0][0], &sm.Tm[0][0], nullptr);
+  mm32<33, 33, 33>(&sm.Ut[0][0], &sm.Cq[0][0], &sm.Tm[0][0], nullptr);  // Y1 T (U done)
   __syncthreads();
   mm32<65, 33, 65>(&sm.MB[0][32], &sm.MB[0][0], &sm.Tm[0][0], nullptr);
   __syncthreads();
@@ -511,19 +544,7 @@ __device__ __forceinline__ void final_rows(const PqrArgs &g, PqrSm &sm, int w) {
       for (int cb = 0; cb < 4; ++cb)
         (cb < 2 ? g.Y : g.YT)[int64_t(i) * SB_B + 16 * (cb & 1) + lc] = acc[rb][cb][q];
     }
-  const int i = w * PT + tid;
-  if (i >= SB_B && i < g.m) {
-    double *ad = g.A + (g.r0 + int64_t(i)) * g.lda + g.p;
-    if ((g.lda & 1) == 0 && (g.p & 1) == 0) {
-#pragma unroll
-      for (int l = 0; l < 16; ++l) reinterpret_cast<double2 *>(ad)[l] = make_double2(0.0, 0.0);
-    } else {
-#pragma unroll
-      for (int l = 0; l < 32; ++l) ad[l] = 0.0;
-    }
-#pragma unroll
-    for (int l = 0; l < 32; ++l) g.A[(g.p + int64_t(l)) * g.lda + g.r0 + i] = 0.0;
-  }
+  // (the panel's rows below the band block are never read again: A is destroyed)
   if (w == 0 && tid < 2 * SB_B) {
     // rows 0..31: Y1 (from the LU) and Y1 T (hr_top), 32 columns per lane
     const int i2 = tid & 31;
@@ -689,6 +710,35 @@ __device__ __forceinline__ int ph_decide(int npass) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) delta = fmax(delta, __shfl_xor(delta, off));
     }
+    if (lane == 0) sm.delta = delta;
+  }
+  __syncthreads();
+  // G within 1e-5 of I (the usual second pass): its Cholesky factor by the
+  // series R = I + F, F = Phi(E - F^T F), E = G - I (Phi: strict upper + half
+  // diagonal), two terms: error O(|E|^3) <= 1e-15, all 32 x 32 products on
+  // MFMA instead of a 32-step pivot chain.
+  const bool series = npass >= 2 && sm.delta <= SERIES_TOL;
+  if (series) {
+    for (int e = tid; e < 1024; e += PT) {
+      const int i2 = e >> 5, j2 = e & 31;
+      const double ev = sm.Gs[i2][j2] - (i2 == j2 ? 1.0 : 0.0);
+      const double f = (i2 < j2) ? ev : (i2 == j2 ? 0.5 * ev : 0.0);
+      sm.RgI[i2][j2] = f;  // F1
+      sm.Ut[j2][i2] = f;   // F1^T
+    }
+    __syncthreads();
+    mm32<33, 33, 33>(&sm.Cq[0][0], &sm.Ut[0][0], &sm.RgI[0][0], nullptr);  // F1^T F1
+    __syncthreads();
+    for (int e = tid; e < 1024; e += PT) {
+      const int i2 = e >> 5, j2 = e & 31;
+      const double ev = sm.Gs[i2][j2] - (i2 == j2 ? 1.0 : 0.0) - sm.Cq[i2][j2];
+      const double f = (i2 < j2) ? ev : (i2 == j2 ? 0.5 * ev : 0.0);
+      sm.Lt[i2][j2] = (i2 == j2 ? 1.0 : 0.0) + f;  // R = L^T (upper)
+      if (i2 == j2) sm.rinv[i2] = rcp_nr(1.0 + f);
+    }
+    if (tid == 0) sm.dec = DEC_ACCEPT;
+  } else if (wid == 0) {
+    const double delta = sm.delta;
     double mr = 0.0;
     bool ok = chol32_ool(0.0, mr);
     if (npass == 1 && (!ok || mr < 1e-12)) {
@@ -718,15 +768,6 @@ __device__ __forceinline__ int ph_decide(int npass) {
   }
   DBG_STAMP(dk + 3)
   if (d == DEC_ACCEPT) {
-    // final Q top rows (rows 0..31 = threads 0..31)
-    if (tid < 32) {
-      double x[32];
-      row_from_lds(&sm.Xs[tid][0], x);
-      trsm_row(x, sm.Lt, sm.rinv);
-#pragma unroll
-      for (int l = 0; l < 32; ++l) sm.Cq[tid][l] = x[l];
-    }
-    __syncthreads();
     DBG_STAMP(dk + 4)
     hr_top_ool();
     DBG_STAMP(dk + 5)
