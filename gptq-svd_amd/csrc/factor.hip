@@ -22,6 +22,7 @@
 // factor in LDS, triangular solve across all n columns, MFMA trailing update).
 #include <algorithm>
 #include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -547,11 +548,16 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
 // for bit.  Selection: two 11-bit radix passes on the diagonal's bit pattern
 // (positive doubles order like their bits), set = rows strictly above the
 // crossing bin (|set| <= SEL).
+// The candidate-set path keeps only the lower triangle of H_k current (the
+// Schur updates skip the mirror writes): element (a, b) is read at (max, min).
+__device__ inline size_t lower_idx(int a, int b, int n) {
+  return size_t(max(a, b)) * n + min(a, b);
+}
 constexpr int SEL = 1024;         // candidates
 constexpr int SEL_LDS_N = 8192;  // n up to which piv_sel_kernel stages diagonals in LDS
 
 #ifdef TG_SEL_PHASES
-__device__ unsigned long long g_selph[8];
+__device__ unsigned long long g_selph[16];
 #define SELT(i)                                                     \
   {                                                                 \
     const uint64_t tt = __builtin_amdgcn_s_memtime();               \
@@ -569,102 +575,139 @@ __device__ inline unsigned long long dkey(double d) {
 constexpr int STH = 512;        // threads of piv_sel_kernel (8 waves)
 constexpr int CPT = SEL / STH;  // candidates per thread
 
-// wave argmax of (v desc, p asc) carrying a row id r (positions are unique)
-template <int S>
-__device__ inline void argmax2_stage(double &v, int &p, int &r) {
-  const double ov = __hiloint2double(partner<S>(__double2hiint(v)), partner<S>(__double2loint(v)));
-  const int op = partner<S>(p), orr = partner<S>(r);
-  if (ov > v || (ov == v && op < p)) {
-    v = ov;
-    p = op;
-    r = orr;
-  }
+// Block argmax of (v desc, p asc) carrying a row id r (positions are
+// unique).  Wave stage: the maximum of v alone through six exchange stages
+// (v_permlane{32,16}_swap pairs, DPP row mirrors / quad perms) with v_max_f64,
+// then the holder found by a ballot; only a tie on v (rare: exhausted
+// candidates at -inf) takes the slower min-position pass.  One barrier; the
+// eight wave records are merged by every thread with selects.
+// v_max_f64 without the operand canonicalisation fmax() adds for values that
+// come out of lane exchanges
+__device__ inline double vmax_d(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
-// block argmax over STH threads; one barrier; the result in every thread
+__device__ inline double sel_pair_max(double x, bool half16) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  if (half16) {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return vmax_d(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+  }
+  const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return vmax_d(__hiloint2double(h[0], l[0]), __hiloint2double(h[1], l[1]));
+}
+template <int CTRL>
+__device__ inline double sel_dpp(double x) {
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
+}
+__device__ inline double wave_max_d(double x) {
+  x = sel_pair_max(x, false);
+  x = sel_pair_max(x, true);
+  x = vmax_d(x, sel_dpp<0x140>(x));  // lane ^ 15
+  x = vmax_d(x, sel_dpp<0x141>(x));  // lane ^ 7
+  x = vmax_d(x, sel_dpp<0x1B>(x));   // lane ^ 3
+  return vmax_d(x, sel_dpp<0xB1>(x));  // lane ^ 1
+}
+template <int S>
+__device__ inline int wave_min_stage(int x) {
+  return min(x, partner<S>(x));
+}
 __device__ inline void block_argmax_sel(double &v, int &p, int &r, double2 *rec) {
-  argmax2_stage<0>(v, p, r);
-  argmax2_stage<1>(v, p, r);
-  argmax2_stage<2>(v, p, r);
-  argmax2_stage<3>(v, p, r);
-  argmax2_stage<4>(v, p, r);
-  argmax2_stage<5>(v, p, r);
-  if ((threadIdx.x & 63) == 0) rec[threadIdx.x >> 6] = make_double2(v, __hiloint2double(p, r));
+  const double m = wave_max_d(v);
+  const bool hold = v == m;
+  const unsigned long long b = __ballot(hold);
+  int L = __ffsll(static_cast<long long>(b)) - 1;
+  if (__popcll(b) > 1) {  // tie on v: smallest position among the holders (uniform branch)
+    int pp = hold ? p : INT_MAX;
+    pp = wave_min_stage<0>(pp);
+    pp = wave_min_stage<1>(pp);
+    pp = wave_min_stage<2>(pp);
+    pp = wave_min_stage<3>(pp);
+    pp = wave_min_stage<4>(pp);
+    pp = wave_min_stage<5>(pp);
+    L = __ffsll(static_cast<long long>(__ballot(hold & (p == pp)))) - 1;
+  }
+  const int wp = __builtin_amdgcn_readlane(p, L), wr = __builtin_amdgcn_readlane(r, L);
+  if ((threadIdx.x & 63) == 0) rec[threadIdx.x >> 6] = make_double2(m, __hiloint2double(wp, wr));
   __syncthreads();
-  double2 x = rec[0];
-  v = x.x;
-  p = __double2hiint(x.y);
-  r = __double2loint(x.y);
+  double2 x[STH / 64];
 #pragma unroll
-  for (int q = 1; q < STH / 64; ++q) {
-    x = rec[q];
-    const int op = __double2hiint(x.y);
-    if (x.x > v || (x.x == v && op < p)) {
-      v = x.x;
-      p = op;
-      r = __double2loint(x.y);
-    }
+  for (int q = 0; q < STH / 64; ++q) x[q] = rec[q];
+  v = x[0].x;
+#pragma unroll
+  for (int q = 1; q < STH / 64; ++q) v = vmax_d(v, x[q].x);
+  p = INT_MAX;
+  r = 0;
+#pragma unroll
+  for (int q = 0; q < STH / 64; ++q) {
+    const int op = __double2hiint(x[q].y);
+    const bool take = (x[q].x == v) & (op < p);
+    p = take ? op : p;
+    r = take ? __double2loint(x[q].y) : r;
   }
 }
 
-// Radix pass over the keys of unpivoted rows (prefix filter (key >> 52) == b1
-// when pass == 2): crossing bin of the `target`-th largest, and the count
-// strictly above it, to out[0..1] (LDS).
-__device__ inline void radix_pass(const double *__restrict__ dsc, const int32_t *__restrict__ pos,
-                                  int n, int ps, int pass, int b1, int target, unsigned *hist,
-                                  int *out) {
-  const int tid = threadIdx.x;
-  for (int x = tid; x < 2048; x += STH) hist[x] = 0u;
-  __syncthreads();
-  for (int r0 = tid; r0 < n; r0 += 4 * STH) {
-    double dv[4];
-    int pv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {  // one batch of loads in flight
-      const int r = min(r0 + u * STH, n - 1);
-      dv[u] = dsc[r];
-      pv[u] = pos[r];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (r0 + u * STH >= n || pv[u] < ps) continue;
-      const unsigned long long key = dkey(dv[u]);
-      if (key == 0ull) continue;
-      const int d1 = int(key >> 52);
-      if (pass == 1) atomicAdd(&hist[d1], 1u);
-      else if (d1 == b1) atomicAdd(&hist[int(key >> 41) & 2047], 1u);
-    }
+// Radix-select histograms: 2048 bins padded by one word per 32 (bin b at
+// b + b / 32), so the scan's lanes (one 32-bin block each) read conflict-free.
+constexpr int HPAD = 2048 + 64;
+__device__ inline int hidx(int b) { return b + (b >> 5); }
+
+// Wave-aggregated histogram increment: the exponent bins of one wave's keys
+// are few (diagonals of similar scale), so one atomic per distinct bin instead
+// of 64 same-address atomics.  Uniform loop over the distinct bins.
+__device__ inline void hist_add_agg(unsigned *hist, int bin, bool ok, int lane) {
+  unsigned long long pend = __ballot(ok);
+  while (pend) {
+    const int L = __ffsll(static_cast<long long>(pend)) - 1;
+    const int b = __builtin_amdgcn_readlane(bin, L);
+    const unsigned long long same = __ballot(ok & (bin == b));
+    if (lane == L) atomicAdd(&hist[hidx(b)], unsigned(__popcll(same)));
+    pend &= ~same;
   }
-  __syncthreads();
-  if (tid < 64) {  // lane L covers bins [2047 - 32L - 31, 2047 - 32L], scanned top-down
-    const int top = 2047 - 32 * tid;
-    int sum = 0;
-    for (int b = 0; b < 32; ++b) sum += int(hist[top - b]);
-    int pre = sum;  // inclusive prefix over lanes (top bins first)
+}
+
+// Wave 0: crossing bin of the `target`-th largest key (bins scanned top-down;
+// lane L holds block 63 - L in registers) and the count strictly above it, to
+// out[0..1] (LDS).  Written only when the target is reached.
+__device__ inline void hist_scan(const unsigned *hist, int target, int *out) {
+  const int lane = threadIdx.x & 63, blk = 63 - lane;
+  int c[32];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(pre, off);
-      if (tid >= off) pre += o;
-    }
-    int before = pre - sum;
-    if (before < target && pre >= target) {
-      for (int b = 0; b < 32; ++b) {
-        const int c = int(hist[top - b]);
-        if (before + c >= target) {
-          out[0] = top - b;
-          out[1] = before;
-          break;
-        }
-        before += c;
-      }
-    }
+  for (int j = 0; j < 32; ++j) c[j] = int(hist[blk * 33 + 31 - j]);  // bin 32 blk + 31 - j
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) sum += c[j];
+  int pre = sum;  // inclusive prefix over lanes (top blocks first)
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(pre, off);
+    pre += lane >= off ? o : 0;
   }
-  __syncthreads();
+  int acc = pre - sum;
+  if (acc < target && pre >= target) {
+    int cb = 0, cbefore = 0;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const bool hit = !found & (acc + c[j] >= target);
+      cb = hit ? j : cb;
+      cbefore = hit ? acc : cbefore;
+      found = found | hit;
+      acc += c[j];
+    }
+    out[0] = blk * 32 + 31 - cb;
+    out[1] = cbefore;
+  }
 }
 
 __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   extern __shared__ int permL[];  // n: position -> row
-  __shared__ unsigned hist[2048];
-  __shared__ int cand[SEL];
+  __shared__ unsigned hist[HPAD];
+  __shared__ int cand[SEL + 1];  // + trash slot for branch-free compaction
   __shared__ double2 rec[STH / 64];
   __shared__ double sv[STH / 64];
   __shared__ int scnt[STH / 64];
@@ -681,72 +724,126 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   uint64_t selt_last = 0;
 #endif
   SELT(0)
-  for (int x = tid; x < n; x += STH) permL[x] = w.perm[x];
   // Schur diagonals and positions: staged in LDS once for n <= SEL_LDS_N (the
-  // selection passes below read them five times), else read from HBM/L2
+  // selection passes below read them three times), else read from HBM/L2
   const bool staged = n <= SEL_LDS_N;
   double *dsh = reinterpret_cast<double *>(permL + ((n + 1) & ~1));
   int *posh = reinterpret_cast<int *>(dsh + n);
   if (staged) {
     for (int r0 = tid; r0 < n; r0 += 8 * STH) {
       double dv[8];
-      int pv[8];
+      int pv[8], mv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {  // one batch of loads in flight
         const int r = min(r0 + u * STH, n - 1);
         dv[u] = w.dsc[r];
         pv[u] = w.pos[r];
+        mv[u] = w.perm[r];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (r0 + u * STH < n) {
           dsh[r0 + u * STH] = dv[u];
           posh[r0 + u * STH] = pv[u];
+          permL[r0 + u * STH] = mv[u];
         }
     }
-    __syncthreads();
+  } else {
+    for (int x = tid; x < n; x += STH) permL[x] = w.perm[x];
   }
-  const double *dS = staged ? dsh : w.dsc;
-  const int32_t *pS = staged ? posh : w.pos;
-  // --- candidate set ---------------------------------------------------------
-  int valid = 0;
-  for (int r = tid; r < n; r += STH) valid += (pS[r] >= ps && dkey(dS[r]) != 0ull);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) valid += __shfl_xor(valid, off);
-  if (lane == 0) scnt[wid] = valid;
+  for (int x = tid; x < HPAD; x += STH) hist[x] = 0u;
   if (tid == 0) {
     sel[0] = -1;  // b1 (-1: every positive key is a candidate)
     sel[2] = -1;  // b2
   }
   __syncthreads();
+  SELT(9)
+  const double *dS = staged ? dsh : w.dsc;
+  const int32_t *pS = staged ? posh : w.pos;
+  // --- candidate set ---------------------------------------------------------
+  // one sweep: count of unpivoted rows with positive keys + exponent histogram
+  int valid = 0;
+  for (int r0 = tid; r0 < n; r0 += 8 * STH) {
+    double dv[8];
+    int pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + u * STH, n - 1);
+      dv[u] = dS[r];
+      pv[u] = pS[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const unsigned long long key = dkey(dv[u]);
+      const bool ok = (r0 + u * STH < n) & (pv[u] >= ps) & (key != 0ull);
+      valid += ok;
+      hist_add_agg(hist, int(key >> 52), ok, lane);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) valid += __shfl_xor(valid, off);
+  if (lane == 0) scnt[wid] = valid;
+  __syncthreads();
   valid = 0;
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) valid += scnt[q];
-  if (valid > SEL) {
-    radix_pass(dS, pS, n, ps, 1, 0, SEL, hist, sel);  // sel[0] = b1, sel[1] = above
-    radix_pass(dS, pS, n, ps, 2, sel[0], SEL - sel[1], hist, sel + 2);
+  SELT(10)
+  if (valid > SEL) {  // uniform
+    if (wid == 0) hist_scan(hist, SEL, sel);  // sel[0] = b1, sel[1] = count above
+    __syncthreads();
+    for (int x = tid; x < HPAD; x += STH) hist[x] = 0u;
+    __syncthreads();
+    const int b1 = sel[0];
+    for (int r0 = tid; r0 < n; r0 += 8 * STH) {
+      double dv[8];
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = min(r0 + u * STH, n - 1);
+        dv[u] = dS[r];
+        pv[u] = pS[r];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const unsigned long long key = dkey(dv[u]);
+        if ((r0 + u * STH < n) & (pv[u] >= ps) & (int(key >> 52) == b1))
+          atomicAdd(&hist[hidx(int(key >> 41) & 2047)], 1u);  // mantissa bins: spread
+      }
+    }
+    __syncthreads();
+    if (wid == 0) hist_scan(hist, SEL - sel[1], sel + 2);
+    __syncthreads();
   }
+  SELT(11)
   const int b1 = sel[0], b2 = sel[2];
-  auto inset = [&](unsigned long long key) {
-    if (key == 0ull) return false;
-    if (b1 < 0) return true;
-    const int d1 = int(key >> 52);
-    return d1 > b1 || (d1 == b1 && (int(key >> 41) & 2047) > b2);
-  };
-  // compaction of the set, tau over the rest, full argmax for step 0
+  // compaction of the set, tau over the rest, full argmax for step 0 (branch-free;
+  // membership kept as one bit per row of this thread: n <= 64 STH)
   int mine = 0;
   double tau = -INFINITY, bv = -INFINITY;
   int bp = n, brow = 0;
-  for (int r = tid; r < n; r += STH) {
-    const int pr = pS[r];
-    if (pr < ps) continue;
-    const double d = dS[r];
-    if (inset(dkey(d))) ++mine;
-    else tau = fmax(tau, d);
-    if (d > bv || (d == bv && pr < bp)) {
-      bv = d;
-      bp = pr;
-      brow = r;
+  unsigned long long insm = 0ull;
+  for (int r0 = tid, bi = 0; r0 < n; r0 += 8 * STH, bi += 8) {
+    double dv[8];
+    int pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + u * STH, n - 1);
+      dv[u] = dS[r];
+      pv[u] = pS[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool un = (r0 + u * STH < n) & (pv[u] >= ps);
+      const unsigned long long key = dkey(dv[u]);
+      const int d1 = int(key >> 52), d2 = int(key >> 41) & 2047;
+      const bool ins = un & (key != 0ull) & ((b1 < 0) | (d1 > b1) | ((d1 == b1) & (d2 > b2)));
+      mine += ins;
+      insm |= static_cast<unsigned long long>(ins) << (bi + u);
+      tau = (un & !ins) ? fmax(tau, dv[u]) : tau;
+      const bool take = un & ((dv[u] > bv) | ((dv[u] == bv) & (pv[u] < bp)));
+      bv = take ? dv[u] : bv;
+      bp = take ? pv[u] : bp;
+      brow = take ? r0 + u * STH : brow;
     }
   }
   {
@@ -754,7 +851,7 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const int o = __shfl_up(pre, off);
-      if (lane >= off) pre += o;
+      pre += lane >= off ? o : 0;
     }
     double t2 = tau;
 #pragma unroll
@@ -767,16 +864,21 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
     tau = -INFINITY;
 #pragma unroll
     for (int q = 0; q < STH / 64; ++q) {
-      if (q < wid) base += scnt[q];
+      base += q < wid ? scnt[q] : 0;
       tau = fmax(tau, sv[q]);
     }
     int slot = base + pre - mine;
-    for (int r = tid; r < n; r += STH) {
-      if (pS[r] < ps) continue;
-      if (inset(dkey(dS[r]))) cand[slot++] = r;
+    for (int r0 = tid, bi = 0; r0 < n; r0 += 8 * STH, bi += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool ins = (insm >> (bi + u)) & 1ull;
+        cand[ins ? slot : SEL] = r0 + u * STH;  // non-members to the trash slot
+        slot += ins;
+      }
     }
   }
   __syncthreads();
+  SELT(12)
   int nset = 0;
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) nset += scnt[q];
@@ -810,12 +912,12 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
       double v = -INFINITY;
       int p = n, r = -1;
 #pragma unroll
-      for (int u = 0; u < CPT; ++u)
-        if (!done[u] && (dc[u] > v || (dc[u] == v && posc[u] < p))) {
-          v = dc[u];
-          p = posc[u];
-          r = rc[u];
-        }
+      for (int u = 0; u < CPT; ++u) {
+        const bool take = !done[u] & ((dc[u] > v) | ((dc[u] == v) & (posc[u] < p)));
+        v = take ? dc[u] : v;
+        p = take ? posc[u] : p;
+        r = take ? rc[u] : r;
+      }
       SELT(4)
       block_argmax_sel(v, p, r, rec);
       SELT(5)
@@ -825,12 +927,10 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
       q = p;
       piv = r;
     }
-    const double ljj = sqrt(fmax(dpiv, 0.0));
-    const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
     double hv[CPT];
 #pragma unroll
     for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
-      hv[u] = (!done[u] && rc[u] != piv) ? w.Hk[size_t(piv) * n + rc[u]] : 0.0;
+      hv[u] = w.Hk[lower_idx(piv, max(rc[u], 0), n)];  // unconditional; masked below
 #pragma unroll
     for (int u = 0; u < CPT; ++u)
       if (rc[u] == piv) {
@@ -844,32 +944,37 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
         permL[q] = a;
       }
       w.prow[t] = piv;
-      w.pinv[t] = inv;
     }
     SELT(2)
     __syncthreads();
     SELT(3)
+    // the pivot's sqrt / reciprocal after the barrier: their latency overlaps
+    // the update's fma chains below, which need inv only at their end
+    const double ljj = sqrt(fmax(dpiv, 0.0));
+    const double inv = ljj > 0.0 ? 1.0 / ljj : 0.0;
+    if (tid == 0) w.pinv[t] = inv;
     if (tid <= t) w.Lpp[t * PB + tid] = tid < t ? lrow[tid] : ljj;
     double lrw[PB > 1 ? PB : 1];
 #pragma unroll
     for (int l = 0; l < t; ++l) lrw[l] = lrow[l];
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-      if (rc[u] == piv) {  // dgeqp3 swap of positions i and q
-        posc[u] = i;
-        lr[u][t] = ljj;
-        done[u] = true;
-      } else if (!done[u]) {
-        if (posc[u] == i && q != i) posc[u] = q;
-        double v = hv[u];
+    for (int u = 0; u < CPT; ++u) {  // branch-free: every slot computes, selects keep
+      const bool isp = rc[u] == piv;  // the pivot: dgeqp3 swap of positions i and q
+      const bool upd = !done[u] & !isp;
+      double v = hv[u];
 #pragma unroll
-        for (int l = 0; l < t; ++l) v = fma(-lr[u][l], lrw[l], v);
-        const double lv = v * inv;
-        lr[u][t] = lv;
-        dc[u] = fma(-lv, lv, dc[u]);
-      }
+      for (int l = 0; l < t; ++l) v = fma(-lr[u][l], lrw[l], v);
+      const double lv = v * inv;
+      lr[u][t] = isp ? ljj : (upd ? lv : lr[u][t]);
+      dc[u] = upd ? fma(-lv, lv, dc[u]) : dc[u];
+      const int pswap = ((posc[u] == i) & (q != i)) ? q : posc[u];
+      posc[u] = isp ? i : (upd ? pswap : posc[u]);
+      done[u] = done[u] | isp;
     }
     tdone = t + 1;
+#ifdef TG_SEL_PHASES
+    if (tid == 0) atomicAdd(g_selph + 15, 1ull);
+#endif
   };
   [&]<int... Ts>(std::integer_sequence<int, Ts...>) __attribute__((always_inline)) {
     (step(std::integral_constant<int, Ts>{}), ...);
@@ -916,7 +1021,7 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w) {
   }
   double hv[PB];
 #pragma unroll
-  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? w.Hk[size_t(prow[i]) * n + r] : 0.0;
+  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? w.Hk[lower_idx(prow[i], r, n)] : 0.0;
   double d = w.dsc[r];
   double lr[PB];
   bool done = false;
@@ -1618,11 +1723,13 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   if (!reg) {
     reg = true;
     atexit([] {
-      unsigned long long h[8];
+      unsigned long long h[16];
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_selph), sizeof(h));
-      const char *nm[7] = {"select", "head", "barrier2", "compute+wargmax", "blockargmax", "?", "tail"};
+      const char *nm[12] = {"sel:argmax+cand", "head", "barrier2", "compute+wargmax", "blockargmax",
+                            "?", "tail", "?", "sel:stage", "sel:count", "sel:radix", "sel:compact"};
       fprintf(stderr, "sel phases (cycles, thread 0):");
-      for (int q = 0; q < 7; ++q) fprintf(stderr, " %s %.3g", nm[q], double(h[q]));
+      for (int q = 0; q < 12; ++q) fprintf(stderr, " %s %.3g", nm[q], double(h[q]));
+      fprintf(stderr, " steps %llu", h[15]);
       fprintf(stderr, "\n");
     });
   }
@@ -1647,14 +1754,14 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
       hipLaunchKernelGGL(piv_fill_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, n, k, w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
-      if (p + 1 < P) TG_HIP(tg::dsyrk_tn(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
+      if (p + 1 < P) TG_HIP(tg::dsyrk_tn_lower(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
     }
     int32_t h = 0;
     TG_HIP(hipMemcpyAsync(&h, w.sstate, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     TG_HIP(hipStreamSynchronize(st));
     if (h >= k) break;
     done = h;
-    TG_HIP(tg::dsyrk_tn(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
+    TG_HIP(tg::dsyrk_tn_lower(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
   }
   return 0;
 }

@@ -22,6 +22,9 @@ hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, d
 // Symmetric rank-K updates (lower tiles computed, mirrored to the upper triangle).
 hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc);  // C = a X^T X + b C, X: K x n
+hipError_t dsyrk_tn_lower(hipStream_t st, int n, int K, double alpha, const double *X,
+                          int64_t ldx, double beta, double *C,
+                          int64_t ldc);  // lower tiles of C only, no mirror
 hipError_t dsyrk_nt(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc);  // C = a X X^T + b C, X: n x K
 // Chunked (grouped) GEMM over z = 0..nc-1.  Chunk z covers rows

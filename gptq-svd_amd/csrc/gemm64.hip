@@ -142,7 +142,7 @@ __device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
 
 // C = alpha acc + beta C for the 4-wave tile; the beta != 0 reads are issued
 // together (clamped addresses) so they overlap instead of serialising.
-template <int BM, int BN, bool SYRK>
+template <int BM, int BN, bool SYRK, bool MIRROR = true>
 __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double alpha, double beta,
                                 double *__restrict__ C, int64_t ldc, int M, int N, int tm,
                                 int tn) {
@@ -174,12 +174,12 @@ __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double 
         if (gi < M && gj < N) {
           const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * cv[i][j][r];
           C[int64_t(gi) * ldc + gj] = v;
-          if (SYRK && tm != tn) C[int64_t(gj) * ldc + gi] = v;
+          if (SYRK && MIRROR && tm != tn) C[int64_t(gj) * ldc + gi] = v;
         }
       }
 }
 
-template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK>
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK, bool MIRROR = true>
 __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha,
                                                     const TA_ *__restrict__ A, int64_t lda,
                                                     const TB_ *__restrict__ B, int64_t ldb,
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
   const int ke = min(K, kb + kchunk);
   C += int64_t(blockIdx.z) * zstride;
   mainloop<TA_, TB_, BM, BN, TA, TB>(A, lda, B, ldb, M, N, kb, ke, tm, tn, As, Bs, acc);
-  epilogue<BM, BN, SYRK>(acc, alpha, beta, C, ldc, M, N, tm, tn);
+  epilogue<BM, BN, SYRK, MIRROR>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
 // Chunked variant: blockIdx.z = chunk; offsets/dims from ChunkSpec.
@@ -431,6 +431,19 @@ hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X,
   constexpr int BT = 64;
   const int nt = cdiv(n, BT);
   hipLaunchKernelGGL((dgemm_kernel<double, double, BT, BT, true, false, true>),
+                     dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X, ldx,
+                     beta, C, ldc, K > 0 ? K : 1, int64_t(0));
+  return hipGetLastError();
+}
+
+// As dsyrk_tn, lower tiles only and not mirrored: the strict upper triangle
+// outside the diagonal tiles is left stale (readers index (max, min)).
+hipError_t dsyrk_tn_lower(hipStream_t st, int n, int K, double alpha, const double *X,
+                          int64_t ldx, double beta, double *C, int64_t ldc) {
+  if (n <= 0) return hipSuccess;
+  constexpr int BT = 64;
+  const int nt = cdiv(n, BT);
+  hipLaunchKernelGGL((dgemm_kernel<double, double, BT, BT, true, false, true, false>),
                      dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X, ldx,
                      beta, C, ldc, K > 0 ? K : 1, int64_t(0));
   return hipGetLastError();
