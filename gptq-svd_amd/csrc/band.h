@@ -59,6 +59,8 @@ struct SbBufs {
 int pqr_rows_per_thread(int m);
 // Panel A[r0:r0+m, p:p+32] -> Y (m x 32), YT = Y T, T (32 x 32); writes
 // [R; 0] and its transpose into A.  cnt: 2 words zeroed before the launch.
+bool pqr_spread();
+void pqr_set_spread(bool on);
 hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
                     double *YT, double *T, double *part, double *bc, unsigned *cnt,
                     unsigned *tmo);

@@ -942,6 +942,124 @@ static hipError_t side_stream(SideStream *&out) {
   return hipSuccess;
 }
 
+// CU-partitioned streams for the overlapped band reduction (created once per
+// device and size class): `sp` may use only r CUs on every XCD (mask bits k
+// map to XCD k % 8, so bits [0, 8 r) are r CUs per XCD), `su` every other CU.
+// The panel QR's workers (one CU each: their LDS fills it) are spread one
+// block per XCD in turn, so r >= workers / 8 keeps them all resident while
+// the trailing update owns the rest of the chip.
+struct CuStreams {
+  hipStream_t su = nullptr, sp = nullptr;
+  int r = 0;
+  hipEvent_t evq[2] = {nullptr, nullptr}, evs[2] = {nullptr, nullptr}, evj = nullptr, evd = nullptr;
+};
+static hipError_t cu_streams(int r, CuStreams *&out) {
+  static CuStreams cs[64][4];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipDeviceProp_t pr;
+  if ((e = hipGetDeviceProperties(&pr, dev)) != hipSuccess) return e;
+  const int ncu = pr.multiProcessorCount;
+  int slot = 0;
+  while (slot < 3 && (1 << slot) < r) ++slot;
+  r = 1 << slot;
+  if (ncu % 8 != 0 || 8 * r * 4 > ncu) return hipErrorNotSupported;
+  CuStreams &x = cs[dev & 63][slot];
+  if (!x.su) {
+    const int nw = (ncu + 31) / 32;
+    std::vector<uint32_t> mu(nw, 0u), mp(nw, 0u);
+    for (int k = 0; k < ncu; ++k) (k < 8 * r ? mp : mu)[k / 32] |= 1u << (k % 32);
+    if ((e = hipExtStreamCreateWithCUMask(&x.su, nw, mu.data())) != hipSuccess) return e;
+    if ((e = hipExtStreamCreateWithCUMask(&x.sp, nw, mp.data())) != hipSuccess) return e;
+    for (int i = 0; i < 2; ++i) {
+      if ((e = hipEventCreateWithFlags(&x.evq[i], hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&x.evs[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    if ((e = hipEventCreateWithFlags(&x.evj, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&x.evd, hipEventDisableTiming)) != hipSuccess) return e;
+    x.r = r;
+  }
+  out = &x;
+  return hipSuccess;
+}
+
+// Overlapped form: panel pi + 1's QR (on the reserved CUs) runs while panel
+// pi's trailing update A22[32:, 32:] runs on the other CUs.  Per panel, on su:
+// wait QR(pi) -> X, M -> strip update (the next panel's 32 rows / columns) ->
+// event -> syr2k of the rest; on sp: wait strip(pi) -> QR(pi + 1) -> event.
+// Buffer use as in the look-ahead form below (the QR's partials region is
+// idle between ytx_m and the strip event; YT is read only by X).
+static hipError_t sy2sb_overlap(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
+                                const SbBufs &b, CuStreams &cs) {
+  const int np = int(pl.panels.size());
+  TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
+  TG_CHK(hipEventRecord(cs.evj, st));
+  TG_CHK(hipStreamWaitEvent(cs.su, cs.evj, 0));
+  TG_CHK(hipStreamWaitEvent(cs.sp, cs.evj, 0));
+  const bool spread0 = pqr_spread();
+  pqr_set_spread(true);
+  auto pqr = [&](hipStream_t s, int pi) {
+    const SbPanel &P = pl.panels[pi];
+    return panel_qr(s, A, lda, P.p, P.r0, P.m, b.Y + P.L[0].yoff, b.YT, b.T + P.L[0].toff,
+                    b.pq_part, b.pq_bc, b.pq_ctl + 4 + 4 * pi, b.pq_ctl);
+  };
+  hipError_t err = hipSuccess;
+  auto run = [&]() -> hipError_t {
+    TG_CHK(pqr(cs.sp, 0));
+    TG_CHK(hipEventRecord(cs.evq[0], cs.sp));
+    for (int pi = 0; pi < np; ++pi) {
+      const SbPanel &P = pl.panels[pi];
+      const int m = P.m, r0 = P.r0, ph = pi & 1;
+      double *A22 = A + int64_t(r0) * lda + r0;
+      double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
+      TG_CHK(hipStreamWaitEvent(cs.su, cs.evq[ph], 0));  // panel QR pi done
+      const int nz = std::max(1, m / SB_C);
+      ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
+      TG_CHK(dgemm_chunked(cs.su, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
+      TG_CHK(sum_partials(cs.su, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
+      hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 256)), dim3(256), 0, cs.su, Yp, b.X, m, Tp,
+                         b.M, b.pq_part, b.pq_ctl + 1);
+      TG_CHK(hipGetLastError());
+      if (pi + 1 < np) {
+        hipLaunchKernelGGL(strip_update_kernel, dim3(cdiv(m, 64)), dim3(256), 0, cs.su, A22,
+                           int64_t(lda), m, Yp, b.X, b.M);
+        TG_CHK(hipGetLastError());
+        TG_CHK(hipEventRecord(cs.evs[ph], cs.su));
+        TG_CHK(hipStreamWaitEvent(cs.sp, cs.evs[ph], 0));
+        TG_CHK(pqr(cs.sp, pi + 1));
+        TG_CHK(hipEventRecord(cs.evq[ph ^ 1], cs.sp));
+        const int mr = m - SB_B;
+        if (mr > 0) {
+          const int nt = cdiv(mr, S2T);
+          auto tok = prof_begin(cs.su, PROF_SBUPD, 12.0 * double(mr) * mr, 96.0 * double(mr) * mr);
+          hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, cs.su,
+                             A22 + int64_t(SB_B) * lda + SB_B, int64_t(lda), mr, mr, 1,
+                             Yp + SB_B * SB_B, b.X + SB_B * SB_B, int64_t(SB_B), b.M, int64_t(SB_B));
+          prof_end(cs.su, tok);
+          TG_CHK(hipGetLastError());
+        }
+      } else {
+        const int nt = cdiv(m, S2T);
+        auto tok = prof_begin(cs.su, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
+        hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, cs.su, A22,
+                           int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+        prof_end(cs.su, tok);
+        TG_CHK(hipGetLastError());
+      }
+    }
+    return hipSuccess;
+  };
+  err = run();
+  pqr_set_spread(spread0);
+  TG_CHK(err);
+  TG_CHK(hipEventRecord(cs.evd, cs.su));
+  TG_CHK(hipStreamWaitEvent(st, cs.evd, 0));
+  TG_CHK(hipEventRecord(cs.evj, cs.sp));
+  TG_CHK(hipStreamWaitEvent(st, cs.evj, 0));
+  return hipSuccess;
+}
+
 // One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
 // Look-ahead (TG_SB_LOOKAHEAD=1; off by default: measured +5 ms at n = 4096,
 // the panel QR's workgroups need a whole CU's LDS and wait for the trailing
@@ -953,6 +1071,22 @@ static hipError_t side_stream(SideStream *&out) {
 // while the side stream runs (the panel QR's partials region is idle then).
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
+  static const int cumask = [] {
+    const char *v = getenv("TG_SB_CUMASK");
+    return v ? atoi(v) : 0;
+  }();
+  if (cumask && !pl.panels.empty()) {
+    const int nwmax = cdiv(pl.panels[0].m, 256);
+    CuStreams *cs = nullptr;
+    if (cu_streams(cdiv(nwmax, 8), cs) == hipSuccess && 8 * cs->r >= nwmax) {
+      if (cumask == 2) {  // diagnostic: both on the update stream (mask cost alone)
+        CuStreams one = *cs;
+        one.sp = one.su;
+        return sy2sb_overlap(st, A, lda, n, pl, b, one);
+      }
+      return sy2sb_overlap(st, A, lda, n, pl, b, *cs);
+    }
+  }
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
   const char *la = getenv("TG_SB_LOOKAHEAD");
   const bool look = la && la[0] == '1';

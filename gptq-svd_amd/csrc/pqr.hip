@@ -66,6 +66,7 @@ struct PqrArgs {
   unsigned long long timeout;
   unsigned long long *stats;  // TG_PQR_STATS: per-phase clock stamps of workgroup 0 (or null)
   int force_fb;               // TG_PQR_FALLBACK=1: every panel through the Householder path (tests)
+  int wstride;                // blocks per worker: 8 (workers on one XCD) or 1 (spread over XCDs)
 };
 
 struct PqrSm {
@@ -80,7 +81,7 @@ struct PqrSm {
   double rinv[32], uinv[32], sv[32];
   double dsum[32], prow[32], taus[32];
   double delta;
-  double bcast[2][128];        // one-wave broadcast rows (+ a trash slot per lane)
+  double bcast[4][128];        // one-wave broadcast rows (+ a trash slot per lane), 2 x double-buffered
   int dec;
   PqrArgs ga;                 // the launch arguments (read by the out-of-line phases)
 };
@@ -292,19 +293,18 @@ __device__ __forceinline__ void gram_reduce(const PqrArgs &g, PqrSm &sm) {
 __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
   PqrSm &sm = s_pq;
   const int lane = otid() & 63, i = lane & 31, h = lane >> 5;
-  double *buf = sm.bcast[0];
   double gr[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) gr[c] = sm.Gs[i][16 * h + c] + (16 * h + c == i ? shift : 0.0);
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const int hj = j >> 4, cj = j & 15;
-    // lanes of column j publish it; the others write a slot nobody reads
-    buf[h == hj ? i : 32 + lane] = gr[cj];
+  // Software-pipelined: column 0 is published and read up front; step j
+  // updates column j + 1 first, publishes it (double-buffered LDS) and issues
+  // the next step's reads before the rest of its own update, so the LDS round
+  // trip overlaps the remaining fma.
+  auto read_col = [&](int j, double &piv, double &gij, double (&col)[16]) {
+    const double *buf = sm.bcast[j & 1];
     wave_lds_sync();
-    const double piv = buf[j];
-    const double gij = buf[i];
-    double col[16];
+    piv = buf[j];
+    gij = buf[i];
     const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -312,16 +312,39 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
       col[2 * c] = v.x;
       col[2 * c + 1] = v.y;
     }
-    wave_lds_sync();
-    const double r = rsq_nr(piv);
-    const double lij = gij * r;  // L[i][j] for i >= j (i == j: sqrt(piv))
-    if (h == hj) gr[cj] = lij;
+  };
+  double piv, gij, col[16];
+  DBG_STAMP(24)
+  sm.bcast[0][h == 0 ? i : 32 + lane] = gr[0];
+  read_col(0, piv, gij, col);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const double ml = (16 * h + c > j) ? -lij : 0.0;
-      gr[c] = fma(ml, col[c] * r, gr[c]);
+  for (int j = 0; j < 32; ++j) {
+    const int hj = j >> 4, cj = j & 15;
+    const double r = rsq_nr(piv);
+    const double lij = gij * r;  // L[i][j] for i >= j (i == j: sqrt(piv)); 0 above
+    const double mlr = -lij * r;
+    double pn = 0.0, gn = 0.0, cn2[16];
+    if (j + 1 < 32) {
+      // lanes of column j + 1 publish its rows >= j + 1 (rows above as 0, so
+      // that the update needs no per-entry mask: those rows get l = 0 and no
+      // row's finished columns are touched); the others write a slot nobody reads
+      const int hn = (j + 1) >> 4, cn = (j + 1) & 15;
+      gr[cn] = fma(mlr, col[cn], gr[cn]);
+      sm.bcast[(j + 1) & 1][h == hn ? i : 32 + lane] = i >= j + 1 ? gr[cn] : 0.0;
+      read_col(j + 1, pn, gn, cn2);
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c)  // column j itself: reset below
+      if (c != ((j + 1) & 15) || j + 1 >= 32) gr[c] = fma(mlr, col[c], gr[c]);
+    if (h == hj) gr[cj] = lij;
+    if (j + 1 < 32) {
+      piv = pn;
+      gij = gn;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) col[c] = cn2[c];
     }
   }
+  DBG_STAMP(25)
   double dg = 1.0;
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
@@ -337,7 +360,9 @@ __device__ __forceinline__ bool chol32_ool(double shift, double &minrat) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) rat = fmin(rat, __shfl_xor(rat, off));
   minrat = rat;
-  return __all(good);
+  const bool allgood = __all(good);
+  DBG_STAMP(26)
+  return allgood;
 }
 
 // X = R^-1 for a 32 x 32 upper triangular R = get(i, k) (i <= k) with
@@ -398,15 +423,21 @@ __device__ __forceinline__ void lu_hr() {
   const int lane = otid() & 63;
   {
     const int i = lane & 31, h = lane >> 5;
-    double *buf = sm.bcast[0], *cbuf = sm.bcast[1];
-    double c[16];
+    double c[16], lw[16];  // working rows (U part live) and the L entries of row i
 #pragma unroll
-    for (int l = 0; l < 16; ++l) c[l] = sm.Cq[i][16 * h + l];
+    for (int l = 0; l < 16; ++l) {
+      c[l] = sm.Cq[i][16 * h + l];
+      lw[l] = 0.0;
+    }
     // L_ij = -S_jj C^(j)_ij / U_jj, U_jj = 1 + |C^(j)_jj|, S_jj = -sign(C^(j)_jj),
-    // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl
+    // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl.  No per-entry masks: rows <= j take
+    // l = 0; the working columns < j (and j, once L_ij is in lw) are dead and
+    // only ever feed dead columns.
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       const int hj = j >> 4, cj = j & 15;
+      // double-buffered row / column: the next step's writes need not wait for these reads
+      double *buf = sm.bcast[2 * (j & 1)], *cbuf = sm.bcast[2 * (j & 1) + 1];
       if (i == j) {  // row j (its two half-rows: lanes j and j + 32)
         double2 *d2 = reinterpret_cast<double2 *>(buf + 16 * h);
 #pragma unroll
@@ -423,18 +454,14 @@ __device__ __forceinline__ void lu_hr() {
         rw[2 * l] = v.x;
         rw[2 * l + 1] = v.y;
       }
-      wave_lds_sync();
       // S_jj = -sign(C_jj) (as a sign copy, no compare on the chain)
       const double ms = copysign(1.0, qjj);
       const double ru = rcp_nr(1.0 + fabs(qjj));
       if (lane == 0) sm.sv[j] = -ms;
-      const double lij = ms * cij * ru;
-      if (i > j && h == hj) c[cj] = lij;
+      const double lij = i > j ? ms * cij * ru : 0.0;
+      if (h == hj) lw[cj] = lij;
 #pragma unroll
-      for (int l = 0; l < 16; ++l) {
-        const double ml = (i > j && 16 * h + l > j) ? -lij : 0.0;
-        c[l] = fma(ml, rw[l], c[l]);
-      }
+      for (int l = 0; l < 16; ++l) c[l] = fma(-lij, rw[l], c[l]);
     }
     wave_lds_sync();
     DBG_STAMP_T(20, 0)
@@ -442,7 +469,7 @@ __device__ __forceinline__ void lu_hr() {
     for (int l = 0; l < 16; ++l) {
       const int col = 16 * h + l;
       sm.Ut[i][col] = (col == i) ? 1.0 + fabs(c[l]) : (col > i ? -sm.sv[col] * c[l] : 0.0);
-      sm.Cq[i][col] = (col < i) ? c[l] : (col == i ? 1.0 : 0.0);
+      sm.Cq[i][col] = (col < i) ? lw[l] : (col == i ? 1.0 : 0.0);
       if (col == i) sm.uinv[i] = rcp_nr(1.0 + fabs(c[l]));
     }
   }
@@ -745,6 +772,9 @@ __device__ __forceinline__ int ph_decide(int npass) {
       double tr = 0.0;
       for (int c = 0; c < 32; ++c) tr += sm.Gs[c][c];
       const double shift = 11.0 * (double(g.m) * 32.0 + 32.0 * 33.0) * (0.5 * DBL_EPSILON) * tr;
+#ifdef TG_PQR_DBG
+      if (lane == 0) g_pq_dbg[30] += 1;
+#endif
       ok = chol32_ool(shift, mr);
     }
     const int d = !ok ? DEC_FALLBACK
@@ -837,8 +867,8 @@ __device__ __noinline__ void ph_householder(int w, unsigned ep) {
 
 __global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
   PqrSm &sm = s_pq;
-  if (blockIdx.x % 8 != 0) return;  // workers: one per 8 (one XCD under round-robin)
-  const int w = blockIdx.x / 8;
+  if (blockIdx.x % ga.wstride != 0) return;  // workers: one per 8 (one XCD under round-robin)
+  const int w = blockIdx.x / ga.wstride;
   const int tid = otid();
   if (tid == 0) sm.ga = ga;
   unsigned ep = 0;
@@ -880,6 +910,12 @@ __global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
 }  // namespace
 
 namespace tg {
+
+// Workers spread over the XCDs (one block each) instead of packed on one XCD:
+// for a CU-masked side stream that reserves a few CUs on every XCD.
+static bool g_pqr_spread = getenv("TG_PQR_SPREAD") != nullptr;
+bool pqr_spread() { return g_pqr_spread; }
+void pqr_set_spread(bool on) { g_pqr_spread = on; }
 
 int pqr_rows_per_thread(int m) { return m <= PQR_NWMAX * PT ? 1 : 0; }
 
@@ -928,7 +964,8 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
   }
   // 2 Gram passes + the row solve and the final [Y | YT] product: ~10 m 32^2 flops
   auto tok = prof_begin(st, PROF_TSQR, 8.0 * m * SB_B * 3, 10.0 * m * SB_B * SB_B);
-  hipLaunchKernelGGL(pqr_kernel, dim3(8 * g.nw), dim3(PT), 0, st, g);
+  g.wstride = pqr_spread() ? 1 : 8;
+  hipLaunchKernelGGL(pqr_kernel, dim3(g.wstride * g.nw), dim3(PT), 0, st, g);
   prof_end(st, tok);
   if (g.stats) {
     unsigned long long h[16];
@@ -940,13 +977,15 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
     }
 #ifdef TG_PQR_DBG
     static int ndbg = 0;
-    if (++ndbg == 300) {
+    if (++ndbg == 250) {
       unsigned long long d[64];
       (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_pq_dbg), sizeof(d));
       fprintf(stderr, "pqr decide sub-phases (us, sums over launches): p1 reduce %.1f chol %.1f ra %.1f pub %.1f | p2 reduce %.1f chol %.1f ra %.1f cq %.1f hr %.1f pub %.1f\n",
               (d[1] - d[0]) / 100.0, (d[2] - d[1]) / 100.0, (d[3] - d[2]) / 100.0, (d[6] - d[3]) / 100.0,
               (d[9] - d[8]) / 100.0, (d[10] - d[9]) / 100.0, (d[11] - d[10]) / 100.0,
               (d[12] - d[11]) / 100.0, (d[13] - d[12]) / 100.0, (d[14] - d[13]) / 100.0);
+      fprintf(stderr, "  shifted first passes: %llu; chol32: loop %.1f tail %.1f (sums)\n", d[30],
+              (d[25] - d[24]) / 100.0, (d[26] - d[25]) / 100.0);
       fprintf(stderr, "  hr: LU||RgI %.1f  T||UI||R %.1f  M1+Y1T %.1f  (sums); LU %.1f RgI %.1f\n",
               (d[17] - d[16]) / 100.0, (d[18] - d[17]) / 100.0, (d[19] - d[18]) / 100.0,
               (d[20] - d[16]) / 100.0, (d[21] - d[16]) / 100.0);
