@@ -1,6 +1,6 @@
-// CU-mask layout probe: for streams masked to a single CU bit k, report where
-// a workgroup runs (XCC id, SE id, CU id from the hardware id registers), and
-// how round-robin workgroup placement over XCDs interacts with the mask.
+// CU-mask layout probe: for streams masked to 16 CU bits, report where
+// workgroups run (XCC id, SE id, CU id from the hardware id registers): bit k
+// selects a CU of XCD k % 8.  Then copy bandwidth on masked streams.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/cumask_probe.hip -o tools/cumask_probe
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -45,23 +45,8 @@ int main() {
   unsigned *d;
   (void)hipMalloc(&d, 3 * 64 * sizeof(unsigned));
   const int nw = (p.multiProcessorCount + 31) / 32;
-  for (int k : {0, 1, 2, 3, 7, 8, 31, 32, 33, 64, 100, 255}) {
-    std::vector<uint32_t> m(nw, 0u);
-    m[k / 32] = 1u << (k % 32);
-    hipStream_t s;
-    if (hipExtStreamCreateWithCUMask(&s, nw, m.data()) != hipSuccess) {
-      printf("mask %d: create failed\n", k);
-      continue;
-    }
-    hipLaunchKernelGGL(where, dim3(16), dim3(64), 0, s, d);
-    (void)hipStreamSynchronize(s);
-    unsigned h[48];
-    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    printf("bit %3d:", k);
-    for (int b = 0; b < 16; ++b) printf(" %u/%u/%u", h[3 * b], h[3 * b + 1], h[3 * b + 2]);
-    printf("\n");
-    (void)hipStreamDestroy(s);
-  }
+  // (single-bit masks leave XCDs without CUs: workgroups dispatched there may
+  // never run, so every mask below keeps CUs on all eight XCDs)
   // 16 bits 0..15 (first word): where do 64 workgroups land?
   for (int first : {0, 8}) {
     std::vector<uint32_t> m(nw, 0u);
@@ -86,6 +71,18 @@ int main() {
     (void)hipMemset(a, 0, n * sizeof(double4));
     hipStream_t s0;
     (void)hipStreamCreate(&s0);
+    for (size_t ns : {size_t(1) << 19, size_t(1) << 21}) {  // short kernels: 1 element per thread
+      const int grid = int(ns / 256);
+      printf("short grid %5d default: %.4f ms\n", grid, time_copy(s0, a, b, ns, grid));
+      for (int skip : {0, 16}) {
+        std::vector<uint32_t> m(nw, 0u);
+        for (int k = skip; k < p.multiProcessorCount; ++k) m[k / 32] |= 1u << (k % 32);
+        hipStream_t s;
+        (void)hipExtStreamCreateWithCUMask(&s, nw, m.data());
+        printf("short grid %5d mask without bits [0,%d): %.4f ms\n", grid, skip, time_copy(s, a, b, ns, grid));
+        (void)hipStreamDestroy(s);
+      }
+    }
     for (int grid : {1024, 4096, 16384}) {
       printf("grid %5d default: %.3f ms\n", grid, time_copy(s0, a, b, n, grid));
       for (int skip : {0, 16, 64}) {
