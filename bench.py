@@ -209,7 +209,7 @@ def cpu_baseline(H, W, args):
                         f"factorisation {t1 - t0:.2f}s + quantize/pack {t2 - t1:.2f}s"))
 
 
-PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02",
                         "pmc_traffic.json")
 
 

@@ -548,11 +548,20 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
 // for bit.  Selection: two 11-bit radix passes on the diagonal's bit pattern
 // (positive doubles order like their bits), set = rows strictly above the
 // crossing bin (|set| <= SEL).
-// The candidate-set path keeps only the lower triangle of H_k current (the
-// Schur updates skip the mirror writes): element (a, b) is read at (max, min).
+// H_k element (a, b) as the candidate-set path reads it.  Default: the Schur
+// updates mirror, reads go along row a.  TG_PIV_LOWER builds keep only the
+// lower triangle current (no mirror writes: Schur update 50 -> 29 us per
+// panel) and read (max, min): measured 0.07 ms slower per solve overall, the
+// column reads cost the selection and fill kernels what the update saves.
+#ifdef TG_PIV_LOWER
 __device__ inline size_t lower_idx(int a, int b, int n) {
   return size_t(max(a, b)) * n + min(a, b);
 }
+#define TG_PIV_SYRK tg::dsyrk_tn_lower
+#else
+__device__ inline size_t lower_idx(int a, int b, int n) { return size_t(a) * n + b; }
+#define TG_PIV_SYRK tg::dsyrk_tn
+#endif
 constexpr int SEL = 1024;         // candidates
 constexpr int SEL_LDS_N = 8192;  // n up to which piv_sel_kernel stages diagonals in LDS
 
@@ -1754,14 +1763,14 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
       hipLaunchKernelGGL(piv_fill_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, n, k, w);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
-      if (p + 1 < P) TG_HIP(tg::dsyrk_tn_lower(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
+      if (p + 1 < P) TG_HIP(TG_PIV_SYRK(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
     }
     int32_t h = 0;
     TG_HIP(hipMemcpyAsync(&h, w.sstate, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     TG_HIP(hipStreamSynchronize(st));
     if (h >= k) break;
     done = h;
-    TG_HIP(tg::dsyrk_tn_lower(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
+    TG_HIP(TG_PIV_SYRK(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
   }
   return 0;
 }
