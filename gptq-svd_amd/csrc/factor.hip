@@ -1278,6 +1278,118 @@ __global__ __launch_bounds__(64) void potrf_inv_w_kernel(double *__restrict__ U,
   for (int r = 0; r < NU; ++r) Wout[r * NU + c] = wt[r][c];
 }
 
+// Same contract as potrf_inv_w_kernel on four waves: lane c = column c, wave
+// g holds rows 16g .. 16g + 15 (a[q] = A[16g + q][c]), so each wave issues a
+// quarter of the update (the one-wave kernel is bound by its ≈17k issued
+// instructions).  Step j: the owner wave publishes row j (columns < j as 0,
+// so the update needs no mask: rows above j take multiplier 0, finished
+// columns factor 0), one barrier, every wave updates its rows.  The inverse
+// runs right-looking over U's columns: step l (descending) finalises row l of
+// X = U^-1 in its owner, publishes it, and every wave subtracts
+// U[i][l] X[l][:] from its rows i < l (U's diagonal held apart as 1/U_ll, so
+// the stored column has zeros at i >= l).  Broadcast rows double-buffered:
+// one barrier per step.
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restrict__ U, int ldu,
+                                                                int p, int pb,
+                                                                double *__restrict__ Wout,
+                                                                int *__restrict__ info) {
+  constexpr int RW = NU / NWV;  // rows per wave
+  __shared__ double rowb[2][NU];
+  __shared__ double ut[NU][NU + 2];  // ut[l][i] = U[i][l] for i < l (0 elsewhere); then W staging
+  __shared__ double rinv[NU];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  double a[RW];
+  double *base = U + size_t(p) * ldu + p;
+  {
+    const int cc = min(c, pb - 1);
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int r = RW * g + q;
+      const double v = base[size_t(min(r, pb - 1)) * ldu + cc];  // clamped: no guarded loads
+      a[q] = (r < pb && c < pb) ? v : (r == c ? 1.0 : 0.0);
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < NU; ++j) {
+    const int gj = j / RW, qj = j % RW;
+    if (g == gj) rowb[j & 1][c] = c >= j ? a[qj] : 0.0;
+    __syncthreads();
+    const double d = rowb[j & 1][j];
+    const double vc = rowb[j & 1][c];
+    double rv[RW];
+    const double2 *r2 = reinterpret_cast<const double2 *>(&rowb[j & 1][RW * g]);
+#pragma unroll
+    for (int q = 0; q < RW / 2; ++q) {
+      const double2 t = r2[q];
+      rv[2 * q] = t.x;
+      rv[2 * q + 1] = t.y;
+    }
+    // 1/sqrt(d) by v_rsq_f64 + two Newton steps (the IEEE sqrt and division
+    // are ~30 dependent instructions on the chain)
+    double inv = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    inv = inv * fma(-hd * inv, inv, 1.5);
+    inv = inv * fma(-hd * inv, inv, 1.5);
+    const double piv = d * inv;
+    bad |= !(d > 0.0) && j < pb;
+    const double ujc = vc * inv;  // U[j][c] for c > j, 0 for c < j
+    const double f = ujc * inv;
+#pragma unroll
+    for (int q = 0; q < RW; ++q) a[q] = fma(-rv[q], f, a[q]);  // rows <= j: rv = 0 or reset below
+    if (g == gj) {
+      a[qj] = c > j ? ujc : (c == j ? piv : 0.0);
+      ut[c][j] = c > j ? ujc : 0.0;  // column c of U at row j (diagonal apart)
+    }
+    if (c == j && g == 0) rinv[j] = inv;
+  }
+  if (threadIdx.x == 0 && bad) atomicAdd(info, 1);
+  // U block (upper) back in place
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int r = RW * g + q;
+    if (r < pb && c < pb) base[size_t(r) * ldu + c] = c >= r ? a[q] : 0.0;
+  }
+  // X = U^-1: s = I, then for l = 63 .. 0: X[l] = s[l] / U_ll (owner), s[i] -= U[i][l] X[l]
+#pragma unroll
+  for (int q = 0; q < RW; ++q) a[q] = (RW * g + q == c) ? 1.0 : 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int l = NU - 1; l >= 0; --l) {
+    const int gl = l / RW, ql = l % RW;
+    if (g == gl) {
+      a[ql] *= rinv[l];
+      rowb[l & 1][c] = a[ql];
+    }
+    __syncthreads();
+    const double xl = rowb[l & 1][c];
+    double uv[RW];
+    const double2 *u2 = reinterpret_cast<const double2 *>(&ut[l][RW * g]);
+#pragma unroll
+    for (int q = 0; q < RW / 2; ++q) {
+      const double2 t = u2[q];
+      uv[2 * q] = t.x;
+      uv[2 * q + 1] = t.y;
+    }
+#pragma unroll
+    for (int q = 0; q < RW; ++q) a[q] = fma(-uv[q], xl, a[q]);  // U[i][l] = 0 for i >= l
+  }
+  __syncthreads();  // ut is reused as the W staging buffer
+  // W = X^T (lower) through LDS for coalesced rows: wt[c][r] = X[r][c]
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int r = RW * g + q;
+    ut[c][r] = (r < pb && c < pb) ? a[q] : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int r = RW * g + q;
+    Wout[r * NU + c] = ut[r][c];
+  }
+}
+
 // Row-panel triangular solve: X = Ubb^{-T} G[p:p+pb, c] for c in [c0, n).
 // One thread per column; the column's pb unknowns live in LDS (xs[j][tid]).
 __global__ __launch_bounds__(256) void trsm_rows_kernel(double *__restrict__ U, int ldu, int p, int pb,
@@ -1315,6 +1427,22 @@ __global__ void zero_lower_kernel(double *__restrict__ U, int ldu, int k) {
 // diagonal block and its inverse in LDS (potrf_inv_kernel), the panel rows as
 // one MFMA GEMM U12 = U11^-T G12, the trailing update as a second GEMM.
 // info[0] counts non-positive pivots.
+// Diagonal-block factor + inverse: the four-wave kernel (TG_POTRF_WAVES=1 / 8:
+// the one-wave kernel / eight waves, for A/B).
+static void launch_potrf_inv(hipStream_t st, double *U, int ldu, int p, int pb, double *Wb,
+                             int *info) {
+  static const int waves = [] {
+    const char *v = getenv("TG_POTRF_WAVES");
+    return v ? atoi(v) : 4;
+  }();
+  if (waves == 1)
+    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, st, U, ldu, p, pb, Wb, info);
+  else if (waves == 8)
+    hipLaunchKernelGGL(potrf_inv_4w_kernel<8>, dim3(1), dim3(512), 0, st, U, ldu, p, pb, Wb, info);
+  else
+    hipLaunchKernelGGL(potrf_inv_4w_kernel<4>, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
+}
+
 // Low-priority side stream + events for the look-ahead (once per device).
 struct LaStream {
   hipStream_t s = nullptr;
@@ -1355,7 +1483,7 @@ static hipError_t chol_upper_rows_la(hipStream_t st, LaStream &ls, double *U, in
                                      int n, double *Wb, int *info) {
   auto factor_solve = [&](hipStream_t s, int p) -> hipError_t {
     const int pb = std::min(NU, k - p), c0 = p + pb;
-    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, s, U, ldu, p, pb, Wb, info);
+    launch_potrf_inv(s, U, ldu, p, pb, Wb, info);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || c0 >= n) return e;
     double *P = U + size_t(p) * ldu + c0;
@@ -1396,7 +1524,7 @@ hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, dou
     return chol_upper_rows_la(st, *ls, U, ldu, k, n, Wb, info);
   for (int p = 0; p < k; p += NU) {
     const int pb = std::min(NU, k - p);
-    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, st, U, ldu, p, pb, Wb, info);
+    launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int c0 = p + pb;
