@@ -58,6 +58,8 @@ struct PivWs {
   int32_t *prow;    // PB  pivot rows of the panel
   double *pinv;     // PB  1 / L[piv][step]
   double *Lpp;      // PB x PB  L rows of the panel's pivots (panel columns)
+  double *Hk2;      // n x n  second buffer: the compacted Schur complements alternate
+  int32_t *oidx;    // n  new position ps + x -> its compact index in the panel's H_k
 };
 constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
 static_assert(PGMAX * PPS % 256 == 0, "slot copy assumes whole rounds of 256 threads");
@@ -87,6 +89,8 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.prow, PB);
   take(q.pinv, PB);
   take(q.Lpp, PB * PB);
+  take(q.Hk2, size_t(n) * n);
+  take(q.oidx, n);
 }
 
 // B[t][c] = S[t] * Vh[t][c]    (gptq_utils.py:112)
@@ -548,20 +552,12 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
 // for bit.  Selection: two 11-bit radix passes on the diagonal's bit pattern
 // (positive doubles order like their bits), set = rows strictly above the
 // crossing bin (|set| <= SEL).
-// H_k element (a, b) as the candidate-set path reads it.  Default: the Schur
-// updates mirror, reads go along row a.  TG_PIV_LOWER builds keep only the
-// lower triangle current (no mirror writes: Schur update 50 -> 29 us per
-// panel) and read (max, min): measured 0.07 ms slower per solve overall, the
-// column reads cost the selection and fill kernels what the update saves.
-#ifdef TG_PIV_LOWER
-__device__ inline size_t lower_idx(int a, int b, int n) {
-  return size_t(max(a, b)) * n + min(a, b);
-}
-#define TG_PIV_SYRK tg::dsyrk_tn_lower
-#else
-__device__ inline size_t lower_idx(int a, int b, int n) { return size_t(a) * n + b; }
-#define TG_PIV_SYRK tg::dsyrk_tn
-#endif
+// The candidate-set path keeps H_k compacted: at a panel starting at step ps
+// the Schur complement of the unpivoted rows is the leading (n - ps)^2 block,
+// row / column x holding the row at position ps + x (leading dimension n).
+// Each panel's Schur update writes the next compacted block into the other
+// buffer (syrk_compact_kernel), so the update touches (n - ps)^2 entries
+// instead of n^2 and a pivot's row is contiguous.
 constexpr int SEL = 1024;         // candidates
 constexpr int SEL_LDS_N = 8192;  // n up to which piv_sel_kernel stages diagonals in LDS
 
@@ -625,7 +621,8 @@ template <int S>
 __device__ inline int wave_min_stage(int x) {
   return min(x, partner<S>(x));
 }
-__device__ inline void block_argmax_sel(double &v, int &p, int &r, double2 *rec) {
+__device__ inline void block_argmax_sel(double &v, int &p, int &r, int &o, double2 *rec,
+                                        int *reco) {
   const double m = wave_max_d(v);
   const bool hold = v == m;
   const unsigned long long b = __ballot(hold);
@@ -641,7 +638,11 @@ __device__ inline void block_argmax_sel(double &v, int &p, int &r, double2 *rec)
     L = __ffsll(static_cast<long long>(__ballot(hold & (p == pp)))) - 1;
   }
   const int wp = __builtin_amdgcn_readlane(p, L), wr = __builtin_amdgcn_readlane(r, L);
-  if ((threadIdx.x & 63) == 0) rec[threadIdx.x >> 6] = make_double2(m, __hiloint2double(wp, wr));
+  const int wo = __builtin_amdgcn_readlane(o, L);
+  if ((threadIdx.x & 63) == 0) {
+    rec[threadIdx.x >> 6] = make_double2(m, __hiloint2double(wp, wr));
+    reco[threadIdx.x >> 6] = wo;
+  }
   __syncthreads();
   double2 x[STH / 64];
 #pragma unroll
@@ -651,12 +652,14 @@ __device__ inline void block_argmax_sel(double &v, int &p, int &r, double2 *rec)
   for (int q = 1; q < STH / 64; ++q) v = vmax_d(v, x[q].x);
   p = INT_MAX;
   r = 0;
+  o = 0;
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) {
     const int op = __double2hiint(x[q].y);
     const bool take = (x[q].x == v) & (op < p);
     p = take ? op : p;
     r = take ? __double2loint(x[q].y) : r;
+    o = take ? reco[q] : o;
   }
 }
 
@@ -713,11 +716,13 @@ __device__ inline void hist_scan(const unsigned *hist, int target, int *out) {
   }
 }
 
-__global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
+__global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
+                                                      const double *__restrict__ Hc) {
   extern __shared__ int permL[];  // n: position -> row
   __shared__ unsigned hist[HPAD];
   __shared__ int cand[SEL + 1];  // + trash slot for branch-free compaction
   __shared__ double2 rec[STH / 64];
+  __shared__ int reco[STH / 64];
   __shared__ double sv[STH / 64];
   __shared__ int scnt[STH / 64];
   __shared__ int sel[4];
@@ -891,8 +896,9 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   int nset = 0;
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) nset += scnt[q];
-  block_argmax_sel(bv, bp, brow, rec);
-  int rc[CPT], posc[CPT];
+  int bo = bp - ps;  // compact index of the step-0 pivot (positions unchanged so far)
+  block_argmax_sel(bv, bp, brow, bo, rec, reco);
+  int rc[CPT], posc[CPT], oc[CPT];
   double dc[CPT];
   bool done[CPT];
   double lr[CPT][PB];
@@ -901,12 +907,13 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
     const int c = tid + u * STH;
     rc[u] = c < nset ? cand[c] : -1;
     posc[u] = rc[u] >= 0 ? pS[rc[u]] : n;
+    oc[u] = rc[u] >= 0 ? posc[u] - ps : 0;  // compact index in this panel's H_k
     dc[u] = rc[u] >= 0 ? dS[rc[u]] : -INFINITY;
     done[u] = rc[u] < 0;
 #pragma unroll
     for (int l = 0; l < PB; ++l) lr[u][l] = 0.0;
   }
-  int piv = brow, q = bp;
+  int piv = brow, q = bp, opiv = bo;
   double dpiv = bv;
   int tdone = 0;
   SELT(1)
@@ -919,27 +926,29 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
     if (!active) return;
     if (t > 0) {  // candidate argmax; exact only above tau
       double v = -INFINITY;
-      int p = n, r = -1;
+      int p = n, r = -1, o = 0;
 #pragma unroll
       for (int u = 0; u < CPT; ++u) {
         const bool take = !done[u] & ((dc[u] > v) | ((dc[u] == v) & (posc[u] < p)));
         v = take ? dc[u] : v;
         p = take ? posc[u] : p;
         r = take ? rc[u] : r;
+        o = take ? oc[u] : o;
       }
       SELT(4)
-      block_argmax_sel(v, p, r, rec);
+      block_argmax_sel(v, p, r, o, rec, reco);
       SELT(5)
       active = v > tau;
       if (!active) return;
       dpiv = v;
       q = p;
       piv = r;
+      opiv = o;
     }
     double hv[CPT];
 #pragma unroll
     for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
-      hv[u] = w.Hk[lower_idx(piv, max(rc[u], 0), n)];  // unconditional; masked below
+      hv[u] = Hc[size_t(opiv) * n + oc[u]];  // unconditional; masked below
 #pragma unroll
     for (int u = 0; u < CPT; ++u)
       if (rc[u] == piv) {
@@ -990,6 +999,10 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   }(std::make_integer_sequence<int, PB>{});
   SELT(6)
   __syncthreads();
+  // compact index (in this panel's H_k) of the row now at position x >= ps:
+  // read from the panel-start positions before they are overwritten
+  for (int x = ps + tid; x < n; x += STH) w.oidx[x - ps] = pS[permL[x]] - ps;
+  __syncthreads();
   for (int x = tid; x < n; x += STH) {
     const int r = permL[x];
     w.perm[x] = r;
@@ -1001,17 +1014,21 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w) {
   }
 }
 
-// The last panel's L columns (L row-major, LT panel column-major) and Schur
-// diagonals of every row, with piv_sel_kernel's operation sequence.  Rows
-// pivoted in earlier panels keep LT = 0; LT rows past the panel's steps are 0.
-__global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w) {
+// The last panel's L columns (L row-major by row; LT panel column-major by
+// the NEXT panel's compact index) and Schur diagonals of every row still
+// unpivoted at the panel start, with piv_sel_kernel's operation sequence.
+// One thread per position x >= ps (row perm[x], compact index oidx[x - ps]
+// in the panel's H_k block Hc); rows pivoted in the panel (x < ps + tn) get
+// their L entries and no LT column.
+__global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
+                                                       const double *__restrict__ Hc) {
   __shared__ double lpp[PB][PB + 1];
   __shared__ double pinv[PB];
-  __shared__ int prow[PB];
+  __shared__ int prow[PB], poi[PB];
   const int tid = threadIdx.x;
   const int tn = w.sstate[1];
   if (tn <= 0) return;
-  const int ps = w.sstate[0] - tn;
+  const int ps = w.sstate[0] - tn, ps2 = ps + tn;
   for (int x = tid; x < PB * PB; x += 256) {
     const int i = x / PB, l = x % PB;
     lpp[i][l] = (i < tn && l <= i) ? w.Lpp[x] : 0.0;
@@ -1019,18 +1036,15 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w) {
   if (tid < PB) {
     pinv[tid] = tid < tn ? w.pinv[tid] : 0.0;
     prow[tid] = tid < tn ? w.prow[tid] : -1;
+    poi[tid] = tid < tn ? w.oidx[tid] : 0;  // pivot i sits at position ps + i
   }
   __syncthreads();
-  const int r = blockIdx.x * 256 + tid;
-  if (r >= n) return;
-  if (w.pos[r] < ps) {  // pivoted in an earlier panel
-#pragma unroll
-    for (int l = 0; l < PB; ++l) w.LT[size_t(l) * n + r] = 0.0;
-    return;
-  }
+  const int x = ps + blockIdx.x * 256 + tid;
+  if (x >= n) return;
+  const int r = w.perm[x], oi = w.oidx[x - ps];
   double hv[PB];
 #pragma unroll
-  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? w.Hk[lower_idx(prow[i], r, n)] : 0.0;
+  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? Hc[size_t(poi[i]) * n + oi] : 0.0;
   double d = w.dsc[r];
   double lr[PB];
   bool done = false;
@@ -1055,8 +1069,79 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w) {
 #pragma unroll
   for (int l = 0; l < PB; ++l) {
     if (l < tn) w.L[size_t(r) * k + ps + l] = lr[l];
-    w.LT[size_t(l) * n + r] = lr[l];
+    if (x >= ps2) w.LT[size_t(l) * n + (x - ps2)] = lr[l];
   }
+}
+
+// Next panel's compacted H_k: Hn[i][j] = Hc[oidx[tn + i]][oidx[tn + j]]
+// - sum_l LT[l][i] LT[l][j] for i, j < n - ps2 (ps2 = steps done after the
+// panel, tn its steps), 64 x 64 lower tiles mirrored through LDS.  The grid
+// covers the whole n x n lower triangle; tiles past the block exit.
+__global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
+                                                           const double *__restrict__ Hc,
+                                                           double *__restrict__ Hn) {
+  __shared__ double li[PB][64], lj[PB][64];
+  __shared__ double tt[64][65];
+  __shared__ int orow[64], ocol[64];
+  const int tid = threadIdx.x;
+  const int ps2 = w.sstate[0], tn = max(w.sstate[1], 0);
+  const int nc = n - ps2;
+  const int b = blockIdx.x;
+  int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= b) ++I;
+  while (I * (I + 1) / 2 > b) --I;
+  const int J = b - I * (I + 1) / 2;
+  const int i0 = 64 * I, j0 = 64 * J;
+  if (i0 >= nc) return;
+  if (tid < 64) {
+    orow[tid] = w.oidx[tn + min(i0 + tid, nc - 1)];
+  } else if (tid < 128) {
+    ocol[tid - 64] = w.oidx[tn + min(j0 + tid - 64, nc - 1)];
+  }
+  for (int e = tid; e < PB * 64; e += 256) {
+    const int l = e >> 6, c = e & 63;
+    li[l][c] = w.LT[size_t(l) * n + min(i0 + c, nc - 1)];
+    lj[l][c] = w.LT[size_t(l) * n + min(j0 + c, nc - 1)];
+  }
+  __syncthreads();
+  const int tx = tid & 15, ty = tid >> 4;  // columns tx + 16 jj, rows ty + 16 ii
+  double acc[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      acc[ii][jj] = Hc[size_t(orow[ty + 16 * ii]) * n + ocol[tx + 16 * jj]];
+#pragma unroll 8
+  for (int l = 0; l < PB; ++l) {
+    double a4[4], b4[4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) a4[ii] = li[l][ty + 16 * ii];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) b4[jj] = lj[l][tx + 16 * jj];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fma(-a4[ii], b4[jj], acc[ii][jj]);
+  }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int gi = i0 + ty + 16 * ii, gj = j0 + tx + 16 * jj;
+      if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ii][jj];
+      tt[tx + 16 * jj][ty + 16 * ii] = acc[ii][jj];
+    }
+  if (I == J) return;  // uniform
+  __syncthreads();
+  // mirror: rows j0 .. j0 + 63 of the block, columns i0 .. i0 + 63, row-contiguous
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int rr = ty + 16 * ii, cc = tx + 16 * jj;
+      const int gi = j0 + rr, gj = i0 + cc;
+      if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = tt[rr][cc];
+    }
 }
 
 // dsc = diag(Hk), perm = pos = identity, no pivot chosen yet.
@@ -1878,6 +1963,18 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   if (lds > 48 * 1024)
     TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  // compacted Schur complements alternate between the two buffers
+  const double *hc = w.Hk;
+  double *hn = w.Hk2;
+  auto schur_compact = [&](int rows) -> hipError_t {
+    const int nt = tg::cdiv(rows, 64);
+    hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc, hn);
+    const hipError_t e = hipGetLastError();
+    double *t = const_cast<double *>(hc);
+    hc = hn;
+    hn = t;
+    return e;
+  };
   int done = 0;
   for (int round = 0;; ++round) {
     if (round > 4 * (k / PB + 2)) {
@@ -1885,20 +1982,22 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
       return int(hipErrorUnknown);
     }
     const int P = tg::cdiv(k - done, PB);
+    // every panel starts at or after `done + p` steps: grids sized for that bound
     for (int p = 0; p < P; ++p) {
+      const int rows = n - (done + p);
       auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n) * PB * 3, 0.0);
-      hipLaunchKernelGGL(piv_sel_kernel, dim3(1), dim3(STH), lds, st, n, k, w);
-      hipLaunchKernelGGL(piv_fill_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, n, k, w);
+      hipLaunchKernelGGL(piv_sel_kernel, dim3(1), dim3(STH), lds, st, n, k, w, hc);
+      hipLaunchKernelGGL(piv_fill_kernel, dim3(tg::cdiv(rows, 256)), dim3(256), 0, st, n, k, w, hc);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
-      if (p + 1 < P) TG_HIP(TG_PIV_SYRK(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));
+      if (p + 1 < P) TG_HIP(schur_compact(rows));
     }
     int32_t h = 0;
     TG_HIP(hipMemcpyAsync(&h, w.sstate, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     TG_HIP(hipStreamSynchronize(st));
     if (h >= k) break;
+    TG_HIP(schur_compact(n - (done + P - 1)));  // the round's last panel
     done = h;
-    TG_HIP(TG_PIV_SYRK(st, n, PB, -1.0, w.LT, n, 1.0, w.Hk, n));  // the round's last panel
   }
   return 0;
 }
