@@ -398,15 +398,22 @@ __device__ void q1_chunk(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
   __syncthreads();  // red / Ps / Ms reused by the next chunk
 }
 
+// Q1 sub-chunk rows of the single-level back-transform: one 16-row block
+// per wave (more workgroups, no serial row blocks: 512-row sub-chunks left
+// 8 of 16 workers idle and each worker four load -> MFMA rounds).
+constexpr int Q1S = 128;
+constexpr int Q1RB = Q1S / (16 * BW);
+static_assert(Q1RB >= 1 && Q1S % (16 * BW) == 0, "sub-chunk = whole 16-row blocks per wave");
+
 // Single-level panels (one compact-WY block of m rows, band.h SbPlan::single):
-// sub-chunks of 512 rows, two phases with a grid barrier between them.
+// sub-chunks of Q1S rows, two phases with a grid barrier between them.
 // Phase A: sub-chunk I publishes P_I = Y_I^T Z_I (32 x k) to part[I].
 template <int NCB>
 __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
                          SmQ1 &sm) {
   const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane >> 4, lc = lane & 15;
-  const int kb = I * 512, h = min(512, d.rows - kb);
+  const int kb = I * Q1S, h = min(Q1S, d.rows - kb);
   const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
   doublex4 Pa[2][NCB];
 #pragma unroll
@@ -414,11 +421,11 @@ __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) {
+  for (int rb = 0; rb < Q1RB; ++rb) {
     double zl[4][NCB], ya[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * 64 + rb * 16 + 4 * q + lr, rc = min(rl, h - 1);
+      const int rl = wid * (16 * Q1RB) + rb * 16 + 4 * q + lr, rc = min(rl, h - 1);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         zl[q][cb] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
@@ -427,7 +434,7 @@ __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * 64 + rb * 16 + 4 * q + lr;
+      const int rl = wid * (16 * Q1RB) + rb * 16 + 4 * q + lr;
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
@@ -462,15 +469,15 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
                          int nsub, SmQ1 &sm) {
   const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane >> 4, lc = lane & 15;
-  const int kb = I * 512, h = min(512, d.rows - kb);
+  const int kb = I * Q1S, h = min(Q1S, d.rows - kb);
   const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
   double *Zs = a.Z + int64_t(d.r0 + kb) * k;
-  doublex4 F[4][NCB];
+  doublex4 F[Q1RB][NCB];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < Q1RB; ++rb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * 64 + rb * 16 + lr + 4 * q, rc = min(rl, h - 1);
+      const int rl = wid * (16 * Q1RB) + rb * 16 + lr + 4 * q, rc = min(rl, h - 1);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         F[rb][cb][q] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
@@ -508,8 +515,8 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) bm[cb] = sm.Ms[k0 + lr][cb * 16 + lc];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const int rl = wid * 64 + rb * 16 + lc;
+    for (int rb = 0; rb < Q1RB; ++rb) {
+      const int rl = wid * (16 * Q1RB) + rb * 16 + lc;
       const double yl = Y[int64_t(min(rl, h - 1)) * SB_B + k0 + lr];
       const double ya = rl < h ? -yl : 0.0;
 #pragma unroll
@@ -518,10 +525,10 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
     }
   }
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < Q1RB; ++rb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * 64 + rb * 16 + lr + 4 * q;
+      const int rl = wid * (16 * Q1RB) + rb * 16 + lr + 4 * q;
       if (rl >= h) continue;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
@@ -617,13 +624,28 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
   }
   if (a.single) {
     for (int o = 0; o < a.nops; ++o) {
+      BT_T(t0)
       const Q1Op d = a.ops[o];
-      const int nsub = (d.rows + 511) / 512;
+      const int nsub = (d.rows + Q1S - 1) / Q1S;
       for (int I = me; I < nsub; I += W) q1_big_a<NCB>(a, rz, d, I, sm.q1);
+      BT_T(t1)
       grid_barrier(a, unsigned(W) * ++step);
+      BT_T(t2)
       for (int I = me; I < nsub; I += W) q1_big_b<NCB>(a, rz, d, I, nsub, sm.q1);
+      BT_T(t3)
       if (o + 1 < a.nops) grid_barrier(a, unsigned(W) * ++step);
+      BT_T(t4)
+#ifdef TG_BT_STATS
+      st_q1 += (t1 - t0) + (t3 - t2);
+      st_b1 += (t2 - t1) + (t4 - t3);
+#endif
     }
+#ifdef TG_BT_STATS
+    if (me == 0 && threadIdx.x == 0) {
+      unsigned long long *o = reinterpret_cast<unsigned long long *>(a.cnt + 8);
+      o[0] = st_q2; o[1] = st_b2; o[2] = st_q1; o[3] = st_b1;
+    }
+#endif
     return;
   }
   Q1Pre p1;
@@ -669,7 +691,7 @@ static size_t few_ops_bytes(const SbPlan &pl) {
   return (64 + c * sizeof(Q1Op) + 255) & ~size_t(255);
 }
 static int few_nsub(const SbPlan &pl) {
-  return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, 512) : 0;
+  return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) : 0;
 }
 size_t sb_apply_few_scratch(const SbPlan &pl) {
   return few_ops_bytes(pl) + size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double);
