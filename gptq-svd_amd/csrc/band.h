@@ -103,7 +103,9 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   // per-group progress + 4 control words (XCD, group queue, stall flag)
   if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw + 4);
   else ar.template take<unsigned>(nsw + 4);
-  const size_t npart = std::max<size_t>(2 * PQR_NWMAX + 2, size_t(n) / SB_C + 2) * 1024;
+  // partials: panel QR (2 per worker), X row blocks, M (one per 128 rows)
+  const size_t npart = std::max<size_t>(std::max<size_t>(2 * PQR_NWMAX + 2, size_t(n) / SB_C + 2),
+                                        size_t(n) / 128 + 2) * 1024;
   take(b.pq_part, npart);
   take(b.pq_bc, PQR_BC_DOUBLES);
   if constexpr (std::is_same_v<A, Arena>) b.pq_ctl = ar.template take<unsigned>(pq_ctl_words(n));

@@ -770,6 +770,10 @@ __global__ void sym_scatter_kernel(double *__restrict__ A, int64_t lda, int m, i
 // Single-level panels: M = T^T (Y^T X)  (32 x 32, K = m rows).  One
 // workgroup per 256 rows (wave w: rows 64w..64w+63 on FP64 MFMA), partials
 // summed in workgroup order by the last arriver (reduce.h hand-off).
+// rows per wave of ytx_m_kernel (a workgroup covers 4 YTX_RW rows): 32 gives
+// m / 128 workgroups, i.e. twice the parallelism of whole 64-row waves for
+// half the serial load -> MFMA rounds, with at most 32 partials to sum
+constexpr int YTX_RW = 32;
 __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y,
                                                     const double *__restrict__ X, int m,
                                                     const double *__restrict__ T,
@@ -778,14 +782,14 @@ __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y
   __shared__ double red[4][SB_B][SB_B + 1];
   __shared__ double Ps[SB_B * SB_B];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
-  const int base = blockIdx.x * 256 + wid * 64;
+  const int base = blockIdx.x * (4 * YTX_RW) + wid * YTX_RW;
   doublex4 acc[2][2];
 #pragma unroll
   for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) acc[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int g4 = 0; g4 < 4; ++g4) {
+  for (int g4 = 0; g4 < YTX_RW / 16; ++g4) {
     double ya[4][2], xb[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1018,7 +1022,7 @@ static hipError_t sy2sb_overlap(hipStream_t st, double *A, int lda, int n, const
       ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
       TG_CHK(dgemm_chunked(cs.su, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
       TG_CHK(sum_partials(cs.su, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
-      hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 256)), dim3(256), 0, cs.su, Yp, b.X, m, Tp,
+      hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, cs.su, Yp, b.X, m, Tp,
                          b.M, b.pq_part, b.pq_ctl + 1);
       TG_CHK(hipGetLastError());
       if (pi + 1 < np) {
@@ -1111,7 +1115,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
     TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
     // M = T^T Y^T X
-    hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 256)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
+    hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
                        b.pq_part, b.pq_ctl + 1);
     TG_CHK(hipGetLastError());
     const bool next = pi + 1 < np;
