@@ -770,10 +770,10 @@ __global__ void sym_scatter_kernel(double *__restrict__ A, int64_t lda, int m, i
 // Single-level panels: M = T^T (Y^T X)  (32 x 32, K = m rows).  One
 // workgroup per 256 rows (wave w: rows 64w..64w+63 on FP64 MFMA), partials
 // summed in workgroup order by the last arriver (reduce.h hand-off).
-// rows per wave of ytx_m_kernel (a workgroup covers 4 YTX_RW rows): 32 gives
-// m / 128 workgroups, i.e. twice the parallelism of whole 64-row waves for
-// half the serial load -> MFMA rounds, with at most 32 partials to sum
-constexpr int YTX_RW = 32;
+// rows per wave of ytx_m_kernel (a workgroup covers 4 YTX_RW rows); 32 rows
+// (m / 128 workgroups) measured 17.5 -> 23.2 us: the last arriver's partial
+// sum grows faster than the first phase shrinks
+constexpr int YTX_RW = 64;
 __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y,
                                                     const double *__restrict__ X, int m,
                                                     const double *__restrict__ T,
