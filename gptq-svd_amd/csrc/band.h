@@ -90,7 +90,7 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.R[0], w * SB_B);
   take(b.R[1], w * SB_B);
   take(b.Gr, w * n);
-  take(b.U, w * n);
+  take(b.U, std::max(w * n, size_t((n + 127) / 128) * SB_B * size_t(n)));  // X partials
   take(b.Xs, w * w);
   take(b.Zg, w * kmax);
   take(b.P, w * kmax);

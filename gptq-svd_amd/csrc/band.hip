@@ -550,6 +550,114 @@ __global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
     }
 }
 
+// X = A22 YT from the lower triangle of A22 only (the single-level path keeps
+// A22's strict upper part stale: syr2k without mirror writes).  Lower tiles
+// (z, c) of XB x XB, c <= z; an off-diagonal tile is read once and used
+// twice: T1 = A_zc^T YT_z -> rows of block c, T2 = A_zc YT_c -> rows of block
+// z; a diagonal tile as the symmetric block (upper entries read mirrored).
+// Partials: slot s of block b holds T1 of tile (s, b) for s > b, the diagonal
+// for s = b and T2 of tile (b, s) for s < b, so every (slot, block) pair is
+// written once and X = sum over the nb = ceil(m / XB) slots (sum_partials).
+constexpr int XB = 128, XK = 32;
+__global__ __launch_bounds__(256) void symx_kernel(const double *__restrict__ A, int64_t lda, int m,
+                                                   const double *__restrict__ YT,
+                                                   double *__restrict__ part) {
+  __shared__ double As[XK][XB + 2];   // rows k0 .. k0 + 31 of block z, columns of block c
+  __shared__ double Yc[XB][SB_B + 2];  // YT rows of block c
+  __shared__ double Yz[XK][SB_B + 2];  // YT rows k0 .. k0 + 31 of block z
+  const int b = blockIdx.x;
+  int z = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((z + 1) * (z + 2) / 2 <= b) ++z;
+  while (z * (z + 1) / 2 > b) --z;
+  const int c = b - z * (z + 1) / 2;
+  const bool diag = z == c;
+  const int z0 = z * XB, c0 = c * XB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  for (int e = tid; e < XB * SB_B; e += 256) {
+    const int j = e >> 5, l = e & 31;
+    Yc[j][l] = c0 + j < m ? YT[int64_t(c0 + j) * SB_B + l] : 0.0;
+  }
+  doublex4 t1[2][2];  // T1 rows 32 wid .. + 31 (columns of block c), 32 columns
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) t1[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  const int ar = tid >> 3, ac = (tid & 7) * 16;  // loader: row ar, columns ac .. ac + 15
+  for (int k0 = 0; k0 < XB; k0 += XK) {
+    {
+      const int gi = z0 + k0 + ar;
+      double v[16];
+      if (!diag) {
+        const double *src = A + int64_t(min(gi, m - 1)) * lda + c0 + ac;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = (gi < m && c0 + ac + q < m) ? src[q] : 0.0;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int gj = c0 + ac + q;
+          const int r = max(gi, gj), cc = min(gi, gj);
+          v[q] = (gi < m && gj < m) ? A[int64_t(r) * lda + cc] : 0.0;
+        }
+      }
+      const int yi = tid >> 3, yl = (tid & 7) * 4;
+      double yv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yv[q] = z0 + k0 + yi < m ? YT[int64_t(z0 + k0 + yi) * SB_B + yl + q] : 0.0;
+      __syncthreads();  // previous chunk's reads done
+#pragma unroll
+      for (int q = 0; q < 16; ++q) As[ar][ac + q] = v[q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Yz[yi][yl + q] = yv[q];
+      __syncthreads();
+    }
+    // T2 rows k0 .. k0 + 31 of block z: wave (rb, cb) = (wid >> 1, wid & 1), K = XB
+    {
+      const int rb = wid >> 1, cb = wid & 1;
+      doublex4 t2 = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 8
+      for (int kq = 0; kq < XB; kq += 4) {
+        const double af = As[rb * 16 + lr][kq + lk];
+        const double bf = Yc[kq + lk][cb * 16 + lr];
+        t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, t2, 0, 0, 0);
+      }
+      // slot c (z for the diagonal), rows of block z
+      double *dst = part + int64_t(c) * m * SB_B;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = z0 + k0 + rb * 16 + lk + 4 * q;  // acc[q]: row (lane >> 4) + 4 q
+        if (gi < m) dst[int64_t(gi) * SB_B + cb * 16 + lr] = t2[q];
+      }
+    }
+    if (!diag) {  // T1 += A_chunk^T Yz_chunk
+#pragma unroll
+      for (int kq = 0; kq < XK; kq += 4) {
+        double af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[kq + lk][wid * 32 + i * 16 + lr];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = Yz[kq + lk][j * 16 + lr];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            t1[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], t1[i][j], 0, 0, 0);
+      }
+    }
+  }
+  if (diag) return;
+  double *dst = part + int64_t(z) * m * SB_B;  // slot z, rows of block c
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gj = c0 + wid * 32 + i * 16 + lk + 4 * q;
+        if (gj < m) dst[int64_t(gj) * SB_B + j * 16 + lr] = t1[i][j][q];
+      }
+}
+
 // A22 -= Yd X^T + X Yd^T - Yd S Yd^T,  S = (M + M^T)/2  (== Yd W^T + W Yd^T
 // with W = X - Yd M / 2).  Yd block-diagonal over chunks of c rows:
 //   (Yd X^T)[r][c'] = sum_l Y[r][l] X[c'][I(r)*32 + l]
@@ -564,7 +672,7 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
                                                        const double *__restrict__ X,
                                                        int64_t ldx,
                                                        const double *__restrict__ M,
-                                                       int64_t ldm) {
+                                                       int64_t ldm, int mirror = 1) {
   // one LDS block: As, Bs, YS during the K loop, then the 64 x 65 tile for the
   // coalesced mirror stores
   constexpr int SMN = (2 * S2K + SB_B) * (S2T + S2P);
@@ -678,7 +786,7 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
           else if (gi != gj) A[int64_t(gj) * lda + gi] = v;
         }
       }
-  if (tm != tn) {
+  if (tm != tn && mirror) {
     __syncthreads();
     for (int idx = tid; idx < S2T * S2T; idx += 256) {
       const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
@@ -1094,6 +1202,11 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
   const char *la = getenv("TG_SB_LOOKAHEAD");
   const bool look = la && la[0] == '1';
+  // TG_SB_LOWER=1: A22 kept as its lower triangle (X from lower tiles by
+  // symx_kernel, syr2k without mirror writes).  Measured slower: syr2k
+  // 38 -> 35 us but X 27 -> 35 us and twice the partials (per panel at m = 4096).
+  static const bool lower_env = getenv("TG_SB_LOWER") != nullptr;
+  const bool lower = !look && lower_env;
   SideStream *ss = nullptr;
   if (look) TG_CHK(side_stream(ss));
   const int np = int(pl.panels.size());
@@ -1109,11 +1222,20 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     double *A22 = A + int64_t(r0) * lda + r0;
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
     if (look && pi > 0) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));  // panel QR pi done
-    // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
-    const int nz = std::max(1, m / SB_C);
-    ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
-    TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
-    TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
+    if (lower) {
+      // X = A22 YT from A22's lower triangle (tiles read once, used twice)
+      const int nb = cdiv(m, XB);
+      hipLaunchKernelGGL(symx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, A22,
+                         int64_t(lda), m, b.YT, b.U);
+      TG_CHK(hipGetLastError());
+      TG_CHK(sum_partials(st, b.U, nb, m, SB_B, 1.0, 0.0, b.X, SB_B));
+    } else {
+      // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
+      const int nz = std::max(1, m / SB_C);
+      ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
+      TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
+      TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
+    }
     // M = T^T Y^T X
     hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
                        b.pq_part, b.pq_ctl + 1);
@@ -1141,7 +1263,8 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
       const int nt = cdiv(m, S2T);
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
       hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                         int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+                         int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B),
+                         lower ? 0 : 1);
       prof_end(st, tok);
       TG_CHK(hipGetLastError());
       if (next) TG_CHK(pqr(st, pi + 1));
