@@ -18,6 +18,7 @@ import ctypes
 import logging
 from typing import NamedTuple, Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -81,17 +82,18 @@ class SpectrumSplit(NamedTuple):
     left: float      # max |lambda| of the dropped eigenvalues at or below tau
 
 
-def _complement_count(w_asc: torch.Tensor, k: int) -> SpectrumSplit:
-    """One 8n-byte copy of the eigenvalues; the caller has already
-    synchronised on k."""
-    w = w_asc.double().cpu()
-    n = w.numel()
+def _complement_count(w_asc, k: int) -> SpectrumSplit:
+    """Split of the ascending spectrum at rank k (a device tensor: one 8n-byte
+    copy; or a host numpy array).  numpy on the host copy: a handful of torch
+    CPU ops cost ~0.3 ms of host time between two GPU phases."""
+    w = w_asc.double().cpu().numpy() if isinstance(w_asc, torch.Tensor) else np.asarray(w_asc)
+    n = w.shape[0]
     tau = n * 2.220446049250313e-16 * max(float(w[-1]), 0.0)
     dropped = w[:n - k]
     low = dropped[dropped <= tau]
-    return SpectrumSplit(int((dropped > tau).sum()), float(w[n - k]),
+    return SpectrumSplit(int(np.count_nonzero(dropped > tau)), float(w[n - k]),
                          bool(float(w[0]) >= -tau),
-                         float(low.abs().max()) if low.numel() else 0.0)
+                         float(np.abs(low).max()) if low.size else 0.0)
 
 
 def spectral_path(n: int, k: int, sp: SpectrumSplit) -> str:
@@ -143,12 +145,15 @@ def truncated_spectral_factor(H: torch.Tensor, threshold: float = 0.0005,
         S = torch.empty(n, dtype=torch.float64, device=dev)
         kdev = torch.empty(1, dtype=torch.int32, device=dev)
         call("tg_truncation_rank", stream(), ptr(w), n, float(threshold), rule, ptr(S), ptr(kdev))
-        k = int(kdev.item())  # the reference syncs here too (gptq_utils.py:100, :106)
+        # one host sync for the rank and the spectrum split (the reference syncs
+        # here too, gptq_utils.py:100, :106)
+        wk = torch.cat((w, kdev.to(torch.float64))).cpu().numpy()
+        k = int(wk[n])
         if k < 1:
             raise RuntimeError("process_hessian_alt: truncation rank is 0 "
                                "(threshold keeps no eigenvalue)")
         del A
-        sp = _complement_count(w, k)
+        sp = _complement_count(wk[:n], k)
         nc = sp.nc
         path = spectral_path(n, k, sp)
         perm = torch.empty(n, dtype=torch.int64, device=dev)
