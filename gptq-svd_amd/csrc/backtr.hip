@@ -735,7 +735,18 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   const char *tt = getenv("TG_BT_TIMEOUT_TICKS");
   a.timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
-  const int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
+  int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
+  // the workers (one CU each: BtShared fills the LDS) must all be resident:
+  // in the XCD form they are the workgroups of one XCD, so at most its CUs
+  // (sub-chunks beyond W are taken in turn by the loops)
+  static const int cu_xcd = [] {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 32;
+    return std::max(1, ncu / 8);
+  }();
+  if (TG_BT_XCD) W = std::min(W, cu_xcd);
   auto tok = prof_begin(st, PROF_Q2, 0.0, 0.0);
   const int grid = TG_BT_XCD ? 8 * W : W;  // XCD form: ~W land on each XCD
   if (k <= 16)
