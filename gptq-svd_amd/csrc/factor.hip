@@ -1073,6 +1073,8 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
   }
 }
 
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
 // Next panel's compacted H_k: Hn[i][j] = Hc[oidx[tn + i]][oidx[tn + j]]
 // - sum_l LT[l][i] LT[l][j] for i, j < n - ps2 (ps2 = steps done after the
 // panel, tn its steps), 64 x 64 lower tiles mirrored through LDS.  The grid
@@ -1104,44 +1106,50 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
     lj[l][c] = w.LT[size_t(l) * n + min(j0 + c, nc - 1)];
   }
   __syncthreads();
-  const int tx = tid & 15, ty = tid >> 4;  // columns tx + 16 jj, rows ty + 16 ii
-  double acc[4][4];
+  // rank-PB update on FP64 MFMA: waves 2 x 2 over the tile, 2 x 2 blocks of
+  // 16 x 16 each; the accumulators start from the gathered old values
+  const int lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  doublex4 acc[2][2];
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
+  for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-      acc[ii][jj] = Hc[size_t(orow[ty + 16 * ii]) * n + ocol[tx + 16 * jj]];
-#pragma unroll 8
-  for (int l = 0; l < PB; ++l) {
-    double a4[4], b4[4];
+    for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) a4[ii] = li[l][ty + 16 * ii];
+      for (int q = 0; q < 4; ++q)
+        acc[ib][jb][q] = Hc[size_t(orow[wm * 32 + ib * 16 + lk + 4 * q]) * n + ocol[wn * 32 + jb * 16 + lr]];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) b4[jj] = lj[l][tx + 16 * jj];
+  for (int kq = 0; kq < PB; kq += 4) {
+    double af[2], bf[2];
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
+    for (int ib = 0; ib < 2; ++ib) af[ib] = -li[kq + lk][wm * 32 + ib * 16 + lr];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fma(-a4[ii], b4[jj], acc[ii][jj]);
+    for (int jb = 0; jb < 2; ++jb) bf[jb] = lj[kq + lk][wn * 32 + jb * 16 + lr];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+        acc[ib][jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[ib], bf[jb], acc[ib][jb], 0, 0, 0);
   }
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
+  for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int gi = i0 + ty + 16 * ii, gj = j0 + tx + 16 * jj;
-      if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ii][jj];
-      tt[tx + 16 * jj][ty + 16 * ii] = acc[ii][jj];
-    }
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = wm * 32 + ib * 16 + lk + 4 * q, cl = wn * 32 + jb * 16 + lr;
+        const int gi = i0 + rl, gj = j0 + cl;
+        if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
+        tt[cl][rl] = acc[ib][jb][q];
+      }
   if (I == J) return;  // uniform
   __syncthreads();
   // mirror: rows j0 .. j0 + 63 of the block, columns i0 .. i0 + 63, row-contiguous
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int rr = ty + 16 * ii, cc = tx + 16 * jj;
-      const int gi = j0 + rr, gj = i0 + cc;
-      if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = tt[rr][cc];
-    }
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int rr = e >> 6, cc = e & 63;
+    const int gi = j0 + rr, gj = i0 + cc;
+    if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = tt[rr][cc];
+  }
 }
 
 // dsc = diag(Hk), perm = pos = identity, no pivot chosen yet.
