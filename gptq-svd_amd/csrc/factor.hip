@@ -1025,6 +1025,8 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
   __shared__ double lpp[PB][PB + 1];
   __shared__ double pinv[PB];
   __shared__ int prow[PB], poi[PB];
+  __shared__ double lst[256][PB + 1];  // the block's L rows, for row-contiguous stores
+  __shared__ int rst[256];
   const int tid = threadIdx.x;
   const int tn = w.sstate[1];
   if (tn <= 0) return;
@@ -1040,8 +1042,9 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
   }
   __syncthreads();
   const int x = ps + blockIdx.x * 256 + tid;
-  if (x >= n) return;
-  const int r = w.perm[x], oi = w.oidx[x - ps];
+  const bool valid = x < n;  // no early exit: the L rows go out through LDS below
+  const int xc = valid ? x : n - 1;
+  const int r = w.perm[xc], oi = w.oidx[xc - ps];
   double hv[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) hv[i] = i < tn ? Hc[size_t(poi[i]) * n + oi] : 0.0;
@@ -1065,11 +1068,20 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
     lr[i] = lv;
     d = fma(-lv, lv, d);
   }
-  w.dsc[r] = d;
+  if (valid) w.dsc[r] = d;
 #pragma unroll
   for (int l = 0; l < PB; ++l) {
-    if (l < tn) w.L[size_t(r) * k + ps + l] = lr[l];
-    if (x >= ps2) w.LT[size_t(l) * n + (x - ps2)] = lr[l];
+    if (valid && x >= ps2) w.LT[size_t(l) * n + (x - ps2)] = lr[l];
+    lst[tid][l] = lr[l];
+  }
+  rst[tid] = valid ? r : -1;
+  __syncthreads();
+  // L is row-major by row id (rows scattered): 32 lanes write one row's
+  // panel segment contiguously instead of every lane striding k apart
+  const int hw = tid >> 5, l = tid & 31;
+  for (int t = hw; t < 256; t += 8) {
+    const int rr = rst[t];
+    if (rr >= 0 && l < tn) w.L[size_t(rr) * k + ps + l] = lst[t][l];
   }
 }
 
