@@ -9,7 +9,9 @@ runs, and shaped to hit its edge cases:
            dgeqp3 position;
   groups   groups of 8 near-identical heavy columns: one pivot per group knocks
            its 7 siblings to the bottom, so candidates run out against the
-           bound of the non-candidates and panels end early (re-selection).
+           bound of the non-candidates and panels end early (re-selection);
+  full     k = n, n not a multiple of the 64-row tiles: the compacted Schur
+           complement shrinks to its last partial tiles.
 Bars: perm identical; R_x relative Frobenius <= 1e-10.
 """
 import numpy as np
@@ -30,6 +32,9 @@ def _case(kind, rng):
         n, k = 1280, 500
         B = rng.standard_normal((900, n // 2))
         X = np.repeat(B, 2, axis=1)
+    elif kind == "full":
+        n, k = 1300, 1300
+        X = rng.standard_normal((1700, n))
     else:  # groups
         ng, g, nsmall = 150, 8, 1000
         base = 10.0 * rng.standard_normal((1500, ng))
@@ -42,7 +47,7 @@ def _case(kind, rng):
     return H, k
 
 
-@pytest.mark.parametrize("kind", ["generic", "ties", "groups"])
+@pytest.mark.parametrize("kind", ["generic", "ties", "groups", "full"])
 def test_pivot_order_candidate_sets(kind):
     from gptq_svd_amd import _lib as lib
     rng = np.random.default_rng(7)
