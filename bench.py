@@ -230,8 +230,46 @@ def pmc_traffic(cls, args):
                 traffic_source=os.path.relpath(PMC_FILE, os.path.dirname(PMC_FILE) + "/../.."))
 
 
+def launch_plan(gpus: int, env=None):
+    """How `bench.py --gpus N` runs (driver contract).  Under a launcher
+    (WORLD_SIZE set) the world size must equal --gpus.  Without one, N > 1
+    spawns N fresh processes (one per GPU) before anything touches the GPU
+    in this one.  Returns ("run", world) or ("spawn", N); raises on a mismatch."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} "
+                             "ranks; they must agree")
+        return "run", world
+    return ("spawn", gpus) if gpus > 1 else ("run", 1)
+
+
+def _spawned(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = argv
+    run(parse())
+
+
 def main():
     args = parse()
+    mode, world = launch_plan(args.gpus)
+    if mode == "spawn":
+        import socket
+        import torch.multiprocessing as mp
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        # fresh interpreters (start method "spawn"): this process never touches the GPU
+        mp.spawn(_spawned, args=(world, port, list(sys.argv)), nprocs=world, join=True)
+        return
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -239,6 +277,9 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
 
     import gptq_svd_amd.gptq_utils as g
     from gptq_svd_amd import _lib
@@ -251,9 +292,15 @@ def main():
     del acc
 
     gather = None
+    gathered = {"calls": 0, "bytes": 0}
     if world > 1:
         from gptq_svd_amd.dist import gather_packed
-        gather = gather_packed
+
+        def gather(t):
+            out = gather_packed(t)
+            gathered["calls"] += 1
+            gathered["bytes"] += out.numel() * out.element_size()
+            return out
 
     for _ in range(args.warmup):
         solve(g, H, W, args, gather)
@@ -271,6 +318,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    gather_bytes_per_step = gathered["bytes"] // max(1, gathered["calls"])
     _lib.profile_enable(False)
     prof = _lib.profile_query()
     if world > 1:
@@ -328,6 +376,7 @@ def main():
             "value": round(value, 2),
             "unit": "cols/s",
             "n_gpus": world,
+            "world_size": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
@@ -344,6 +393,7 @@ def main():
                 "eps": args.eps, "threshold_method": "energy", "block_size": args.block,
                 "parallelism": (f"independent layer per rank x{world}"
                                 + (", RCCL all_gather of packed weights" if world > 1 else "")),
+                "allgather_bytes_per_step": gather_bytes_per_step if world > 1 else 0,
             },
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -40,6 +40,8 @@ _SIGS = {
     "tg_eigh_values": ([_vp, _vp, _i, _i, _vp, _vp, _sz], _i),
     "tg_eigh_vectors": ([_vp, _i, _vp, _i, _vp, _i, _vp, _sz], _i),
     "tg_eigh_vectors_range": ([_vp, _i, _vp, _i, _i, _vp, _i, _vp, _sz], _i),
+    "tg_band_tridiag_workspace_size": ([_i], _sz),
+    "tg_band_tridiag": ([_vp, _vp, _i, _i, _vp, _vp, _vp, _sz], _i),
     "tg_truncation_rank": ([_vp, _vp, _i, _d, _i, _vp, _vp], _i),
     "tg_pivot_workspace_size": ([_i, _i], _sz),
     "tg_pivoted_factor": ([_vp, _vp, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _sz], _i),
@@ -60,6 +62,8 @@ _SIGS = {
                                _vp, _vp, _vp, _sz], _i),
     "tg_hinv_chol_workspace_size": ([_i], _sz),
     "tg_hinv_chol": ([_vp, _vp, _i, _i, _vp, _d, _i, _vp, _i, ctypes.POINTER(_i), _vp, _sz], _i),
+    "tg_pred_error_workspace_size": ([_i, _i, _i], _sz),
+    "tg_pred_error": ([_vp, _vp, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _sz], _i),
     "tg_pack_codes": ([_vp, _vp, _i, _i, _i, _vp], _i),
     "tg_pack_zeros": ([_vp, _vp, _i, _i, _i, _i, _vp], _i),
 }

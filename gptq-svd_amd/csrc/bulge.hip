@@ -21,12 +21,17 @@
 // Band storage (lower, with bulge room): Bst[c * LDB + d] = B[c + d][c],
 // d < 2b.  Reflectors of (j, s): V2[(j * smax + s) * b + i], tau2[j * smax + s].
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <unistd.h>
 
+#include "../../include/truncgptq.h"
 #include "band.h"
 #include "common.h"
+#include "spin.h"
 
 namespace {
 
@@ -72,33 +77,57 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // ---------------------------------------------------------------------------
 // LDS-resident pipeline.  A workgroup owns G_SW consecutive sweeps; at step t
 // pair q runs task t - LAG q.  The band columns the group touches at step t
-// span [low(t), high(t)) with high(t) - low(t) < 8b, so the group keeps them in an
-// LDS ring of RING band columns (64 doubles each): each step it prefetches the
-// b columns step t+1 adds, and writes back the columns no later task of the
-// group touches.  Hand-off to the next group: the write-backs are plain stores
-// (they stay in the XCD's L2), drained with vmcnt(0) and a barrier before one
-// lane publishes the step count with an sc1 store; the consumer polls with sc1
-// loads and reads columns with sc1 buffer loads (L1 bypassed, L2-served).
-// This is coherent because every worker runs on the same XCD: workgroups read
-// HW_REG_XCC_ID, the first arrival fixes the XCD, the others exit, and the
-// workers take sweep groups from a queue in increasing order (dependencies
+// span [low(t), high(t)), so the group keeps them in an LDS ring of RING band
+// columns (64 doubles each): each step the loader wave brings in the b
+// columns step t+1 adds, and the writer wave writes back the columns no later
+// task of the group touches.
+//
+// Hand-off to the next group (progress word prog[G] = steps whose retired
+// columns are in memory):
+//   producer (writer wave): plain 16-B stores of the retired columns ->
+//     s_waitcnt vmcnt(0) (every store acknowledged by the XCD's L2) ->
+//     progress store (TG_BULGE_FLAG_L2=1: plain `sc0` store, the line stays
+//     in that L2; 0: relaxed agent `sc1` store, written through);
+//   consumer (loader wave): relaxed agent `sc1` poll of prog[G-1] (L1
+//     bypassed) until it covers the columns of the next step, then `sc1`
+//     16-B buffer loads of those columns (L1 bypassed, served by the L2).
+// Every store of the band and every load of it go through ONE L2: the
+// workgroups read HW_REG_XCC_ID, the first arrival fixes the XCD and the
+// workgroups of the other XCDs exit before touching the band.  The XCD's L2
+// is the point of coherence of all its CUs and nothing in this hand-off is
+// cached in an L1, so no agent-scope release (an L2 write-back to HBM, >= 1.7
+// us per step, MI355X_MICROARCH.md price list) or acquire (an L1 invalidate
+// the sc1 loads make unnecessary) is needed.  The order is enforced where the
+// compiler could break it: the vmcnt wait is an asm with a memory clobber
+// before the progress store, and the column loads are issued after the poll
+// returns (they depend on it through the wave barrier).
+// Workers take sweep groups from a queue in increasing order (dependencies
 // point only to lower groups, so any number of resident workers is safe).
+// Waits are bounded (spin.h): the first wait past the timeout sets the stall
+// word, every later wait of the launch gives up at once, and the host
+// poisons (d, e) with NaN.
 // ---------------------------------------------------------------------------
-constexpr int G_SW = 2;              // sweeps per group (wave triples per workgroup)
-constexpr int LAG = 2;               // pipeline lag between consecutive sweeps (tasks)
-constexpr int RING = 256;            // power of two >= (3 G_SW + 3) b - 2 columns
-constexpr int NCW = 3 * G_SW;        // compute waves (three per sweep: left, diagonal, lower block)
-constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
-// TG_BULGE_WDEFER: the writer publishes step t-1 at step t (its stores had a
-// step to drain) instead of waiting for step t's stores inside step t.
-// TG_BULGE_PF2: the loader issues the global loads of step t+2's columns at
-// step t (registers), and stores them to LDS at step t+1 (same ring timing).
+#ifndef TG_BULGE_GSW
+#define TG_BULGE_GSW 2
+#endif
+#ifndef TG_BULGE_FLAG_L2
+#define TG_BULGE_FLAG_L2 1
+#endif
 #ifndef TG_BULGE_WDEFER
 #define TG_BULGE_WDEFER 0
 #endif
-#ifndef TG_BULGE_PF2
-#define TG_BULGE_PF2 0
+#ifndef TG_BULGE_STATS
+#define TG_BULGE_STATS 1  // per-step s_memrealtime stamps (TEMPORARY default: see DESIGN.md §8)
 #endif
+constexpr int G_SW = TG_BULGE_GSW;   // sweeps per group (wave triples per workgroup)
+constexpr int LAG = 2;               // pipeline lag between consecutive sweeps (tasks)
+constexpr int RING = 256;            // ring slots (power of two)
+// live columns: the tasks of step t, the columns step t-1 retired (being
+// written back) and the columns step t+1 adds (being loaded):
+// high(t+1) - low(t-1) = (4 + LAG (G_SW - 1)) b - G_SW
+static_assert((4 + LAG * (G_SW - 1)) * 32 - G_SW <= RING, "LDS ring too small for G_SW");
+constexpr int NCW = 3 * G_SW;        // compute waves (three per sweep: left, diagonal, lower block)
+constexpr int BT = 64 * (NCW + 2);   // + a writer wave and a loader wave
 
 struct WaveScratch {
   double ws[SB_B];
@@ -161,12 +190,6 @@ __device__ __forceinline__ void first_refl(double (*R)[LDB], int n, int j, Refl 
   }
 }
 
-#ifdef TG_BULGE_PHASES
-__device__ unsigned long long g_ph[8];
-#define PH(i) const uint64_t ph##i = __builtin_amdgcn_s_memrealtime();
-#else
-#define PH(i)
-#endif
 
 template <bool FULL>
 __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, int s, int role,
@@ -189,7 +212,6 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
     if (lane == 0) tau2[int64_t(j) * smax] = rin.tau;
     return;
   }
-  PH(0)
   // block loads (issued before the reflector is needed)
   double e[16];  // role 0: A (lane column c = li, rows hf + 2q); role 1: D (lane row li,
                  // k = hf + 2q); role 2: G (lane row li, k = hf + 2q)
@@ -296,15 +318,12 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       p3 += e[q + 3] * vk[q + 3];
     }
     double p = (p0 + p1) + (p2 + p3);
-    PH(1)
     p = hsum32(p);
     p *= tau;
     const double pv = wsum(hf == 0 ? p * v : 0.0);
     const double w = p - 0.5 * tau * pv * v;
-    PH(2)
     if (hf == 0) W.ws[li] = w;
     wave_sync();
-    PH(3)
     double wk[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) wk[q] = W.ws[hf + 2 * q];
@@ -317,17 +336,6 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
       double *dst = ok ? Rf + at(r1 + k, li - k) : tr;
       *dst = e[q] - v * wk[q] - w * vk[q];
     }
-#ifdef TG_BULGE_PHASES
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH(4)
-    if (FULL && lane == 0) {
-      atomicAdd(g_ph + 0, ph1 - ph0);
-      atomicAdd(g_ph + 1, ph2 - ph1);
-      atomicAdd(g_ph + 2, ph3 - ph2);
-      atomicAdd(g_ph + 3, ph4 - ph3);
-      atomicAdd(g_ph + 4, 1ull);
-    }
-#endif
   }
 }
 
@@ -361,7 +369,34 @@ __device__ inline int group_high(int n, int j0, int t) {
 }
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ void publish(unsigned *p, unsigned v) {
+#if TG_BULGE_FLAG_L2
+  __hip_atomic_store((tg::spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+  tg::ctl_store(p, v);
+#endif
+}
+
+#if TG_BULGE_STATS
+#define BSTAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime();
+#else
+#define BSTAMP(v)
+#endif
+#ifndef TG_BULGE_HB
+#define TG_BULGE_HB 0  // debug: per-wave heartbeat (group, step, phase) into host memory
+#endif
+#if TG_BULGE_HB
+#define HB(ph) \
+  if (wlane == 0) \
+    ((volatile unsigned long long *)stats)[blockIdx.x * 16 + wid] = \
+        (unsigned long long)(G + 1) << 32 | (unsigned long long)(t + 1) << 8 | (ph);
+#else
+#define HB(ph)
+#endif
+
+// ctl[0] = chosen XCD + 1, ctl[1] = group queue, ctl[2] = stall word
 __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, int n,
                                                        double *__restrict__ V2,
                                                        double *__restrict__ tau2, int smax,
@@ -369,13 +404,16 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
                                                        unsigned *__restrict__ ctl,
                                                        unsigned long long *__restrict__ stats,
                                                        unsigned long long timeout) {
-  uint64_t sw = 0, stk = 0, sbar = 0, spf = 0, swb = 0, nsteps = 0;
+#if TG_BULGE_STATS
+  uint64_t sw = 0, stk = 0, sbar = 0, nsteps = 0;
+#endif
   __shared__ double R[RING][LDB];
   __shared__ WaveScratch wsc[NCW];
   __shared__ Refl rfl[G_SW][2];
   __shared__ int sh_G;
-  const int tid = threadIdx.x, wid = tid >> 6;
-  // workers: one XCD only (ctl[0] = chosen XCD + 1, ctl[1] = group queue)
+  __shared__ int sh_dead;  // a wait of this workgroup gave up: no further waits
+  const int tid = threadIdx.x, wid = tid >> 6, wlane = tid & 63;
+  unsigned *stall = ctl + 2;
   if (tid == 0) {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
@@ -384,6 +422,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
                                          __HIP_MEMORY_SCOPE_AGENT);
     const unsigned chosen = expect == 0 ? x + 1 : expect;
     sh_G = (chosen == x + 1) ? 0 : -1;
+    sh_dead = 0;
   }
   __syncthreads();
   if (sh_G < 0) return;
@@ -391,11 +430,15 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   const int ngroups = tg::cdiv(nsw, G_SW);
   const int bytes = n * LDB * int(sizeof(double));
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(B, 0, bytes, 0x00020000);
-  constexpr int SC1 = 16;
-  const int nthr_col = LDB / 2;  // threads per column for 16-B transfers
-  constexpr int nthr_col_c = LDB / 2;
+  constexpr int SC1 = 16;                 // cache policy bit of the L1-bypassing loads
+  constexpr int NTC = LDB / 2;            // 16-B chunks per column
+  constexpr int PFN = SB_B * NTC / BT + 1;  // chunks per thread of a whole-workgroup load
+  constexpr int PW = SB_B * NTC / 64;       // chunks per lane of the loader wave
   while (true) {
-    if (tid == 0) sh_G = int(atomicAdd(ctl + 1, 1u));
+    if (tid == 0) {
+      // a stalled launch: stop taking groups (the results are poisoned anyway)
+      sh_G = tg::ctl_load(stall) ? ngroups : int(atomicAdd(ctl + 1, 1u));
+    }
     __syncthreads();
     const int G = sh_G;
     __syncthreads();
@@ -404,118 +447,55 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     const int g = min(G_SW, nsw - j0);
     const int total = group_steps(n, nsw, G);
     const int ptotal = G > 0 ? group_steps(n, nsw, G - 1) : 0;
-    int known = (G > 0) ? 0 : 1 << 30;
-    auto wait_for = [&](int need) {
-      need = min(need, ptotal + 1);  // ptotal + 1: producer finished and fully written back
-      if (known >= need) return;
-      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-      if (tid == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-               unsigned(need)) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
-            __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
+    // progress of the producer group known to this thread (the loader wave's
+    // lanes and the group-start wait keep it; ptotal + 1 = finished + written back)
+    unsigned known = (G > 0) ? 0u : ~0u;
+    // one lane: wait until the producer published `need`
+    auto wait_lane = [&](unsigned need) -> unsigned {
+      unsigned seen = 0;
+      if (!sh_dead && !tg::spin_geq(prog + G - 1, need, stall, timeout, &seen)) sh_dead = 1;
+      return seen;
+    };
+    // initial window [j0, high(0)): every thread loads, after one wait
+    {
+      const unsigned need = unsigned(min(group_need(0), ptotal + 1));
+      BSTAMP(tw)
+      if (G > 0 && tid == 0) wait_lane(need);
       __syncthreads();
-      known = need;
+      if (G > 0) known = need;
+#if TG_BULGE_STATS
       sw += __builtin_amdgcn_s_memrealtime() - tw;
-    };
-    // column loader: columns [c0, c1) (c1 - c0 <= SB_B) with 16-B sc1 loads into registers
-    double2 pf[SB_B * LDB / 2 / BT + 1];
-    constexpr int PFN = SB_B * LDB / 2 / BT + 1;
-    auto load_cols = [&](int c0, int c1) {
-#pragma unroll
-      for (int u = 0; u < PFN; ++u) {
-        const int idx = tid + u * BT;  // 16-B chunk index
-        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
-        const int cc = min(c, max(c1 - 1, 0));
-        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (cc * LDB + 2 * h) * 8, 0, SC1);
-        pf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
-                             __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
-      }
-    };
-    auto store_pf = [&](int c0, int c1) {
+#endif
+    }
+    const int h0 = group_high(n, j0, 0);
+    for (int c0 = j0; c0 < h0; c0 += SB_B) {
+      const int c1 = min(c0 + SB_B, h0);
+      double2 pf[PFN];
 #pragma unroll
       for (int u = 0; u < PFN; ++u) {
         const int idx = tid + u * BT;
-        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
-        if (c < c1 && idx < SB_B * nthr_col) {
+        const int c = min(c0 + idx / NTC, c1 - 1), h = idx % NTC;
+        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
+        pf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                             __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+      }
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) {
+        const int idx = tid + u * BT;
+        const int c = c0 + idx / NTC, h = idx % NTC;
+        if (c < c1 && idx < SB_B * NTC) {
           R[rslot(c)][2 * h] = pf[u].x;
           R[rslot(c)][2 * h + 1] = pf[u].y;
         }
       }
-    };
-    auto write_back = [&](int c0, int c1) {  // plain 16-B stores from LDS
-      for (int idx = tid; idx < (c1 - c0) * nthr_col; idx += BT) {
-        const int c = c0 + idx / nthr_col, h = idx % nthr_col;
-        const double2 v = make_double2(R[rslot(c)][2 * h], R[rslot(c)][2 * h + 1]);
-        const u32x2 lo2 = __builtin_bit_cast(u32x2, v.x), hi2 = __builtin_bit_cast(u32x2, v.y);
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                               (c * LDB + 2 * h) * 8, 0, 0);
-      }
-    };
-    // initial window: [low(0), high(0))
-    int ld = j0, wb = ld;
-    wait_for(group_need(0));
-    for (int c0 = ld; c0 < group_high(n, j0, 0); c0 += SB_B) {
-      const int c1 = min(c0 + SB_B, group_high(n, j0, 0));
-      load_cols(c0, c1);
-      store_pf(c0, c1);
     }
-    ld = group_high(n, j0, 0);
+    int ld = h0, wb = j0;  // ring holds [wb, ld); every wave tracks both
     __syncthreads();
     if (wid == 2) first_refl(R, n, j0, rfl[0][0]);
     __syncthreads();
-    const int wlane = tid & 63;
-    constexpr int PW = SB_B * nthr_col_c / 64;  // 16-B chunks per loader lane per step
-#if TG_BULGE_PF2
-    // loader prefetch: pb holds the columns [pf_lo, pf_hi) loaded one step early
-    double2 pb[PW];
-    int pf_lo = ld, pf_hi = ld;
-    auto poll = [&](int need) {
-      if (G > 0 && known < need) {
-        if (wlane == 0) {
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                 unsigned(need)) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
-              __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-        }
-        known = need;
-        __builtin_amdgcn_wave_barrier();
-      }
-    };
-    auto issue_pf = [&](int lo, int hi) {  // columns [lo, hi), hi - lo <= SB_B
-#pragma unroll
-      for (int u = 0; u < PW; ++u) {
-        const int idx = wlane + 64 * u;
-        const int c = min(lo + idx / nthr_col, hi - 1), h = idx % nthr_col;
-        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
-        pb[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
-                             __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
-      }
-      pf_lo = lo;
-      pf_hi = hi;
-    };
-    if (wid == NCW + 1 && 1 < total) {
-      const int nh = group_high(n, j0, 1);
-      if (nh > ld) {
-        poll(min(group_need(1), ptotal + 1));
-        issue_pf(ld, nh);
-      }
-    }
-#endif
     for (int t = 0; t < total; ++t) {
-      const uint64_t c0t = __builtin_amdgcn_s_memrealtime();
+      BSTAMP(c0t)
+      HB(1)
       if (wid < NCW) {
         const int pair = wid / 3, role = wid % 3;
         const int s = t - LAG * pair;
@@ -533,78 +513,43 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
         }
       } else if (wid == NCW) {
 #if TG_BULGE_WDEFER
-        // writer: step t-1's stores had a step to drain: publish t-1, then
-        // retire the columns step t-1 left behind
+        // writer: the stores of step t-1 had a step to drain; publish t-1 first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (t > 0 && wlane == 0)
-          __hip_atomic_store(prog + G, unsigned(t - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t > 0 && wlane == 0) publish(prog + G, unsigned(t - 1));
 #endif
         // writer: retire the columns step t-1 left behind, drain, publish t
         const int nl = group_low(n, nsw, j0, g, t);
-        if (nl > wb) {
-          for (int idx = wlane; idx < (nl - wb) * nthr_col; idx += 64) {
-            const int c = wb + idx / nthr_col, h = idx % nthr_col;
-            const double2 v = make_double2(R[rslot(c)][2 * h], R[rslot(c)][2 * h + 1]);
-            const u32x2 lo2 = __builtin_bit_cast(u32x2, v.x), hi2 = __builtin_bit_cast(u32x2, v.y);
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                   (c * LDB + 2 * h) * 8, 0, 0);
-          }
-          wb = nl;
+        for (int idx = wlane; idx < (nl - wb) * NTC; idx += 64) {
+          const int c = wb + idx / NTC, h = idx % NTC;
+          const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+          const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                 (c * LDB + 2 * h) * 8, 0, 0);
         }
 #if !TG_BULGE_WDEFER
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (wlane == 0)
-          __hip_atomic_store(prog + G, unsigned(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wlane == 0) publish(prog + G, unsigned(t));
 #endif
       } else {
-#if TG_BULGE_PF2
-        // loader: columns of step t+1 (loaded at step t-1) into the ring, then
-        // issue the loads of step t+2's columns
-        if (pf_hi > pf_lo) {
-#pragma unroll
-          for (int u = 0; u < PW; ++u) {
-            const int idx = wlane + 64 * u;
-            const int c = pf_lo + idx / nthr_col, h = idx % nthr_col;
-            if (c < pf_hi) {
-              R[rslot(c)][2 * h] = pb[u].x;
-              R[rslot(c)][2 * h + 1] = pb[u].y;
-            }
-          }
-          ld = max(ld, pf_hi);
-          pf_lo = pf_hi;
-        }
-        if (t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
-        const int nh2 = group_high(n, j0, t + 2);
-        if (t + 2 < total && nh2 > ld) {
-          poll(min(group_need(t + 2), ptotal + 1));
-          issue_pf(ld, nh2);
-        }
-#else
-        // loader: columns step t + 1 adds
+        // loader: the columns step t + 1 adds
         const int nh = group_high(n, j0, t + 1);
         if (t + 1 < total && nh > ld) {
-          const int need = min(group_need(t + 1), ptotal + 1);
-          if (G > 0 && known < need) {
-            if (wlane == 0) {
-              const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-              while (__hip_atomic_load(prog + G - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                     unsigned(need)) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // give up: stall
-                  __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  break;
-                }
-              }
-            }
-            known = need;
+          const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
+          if (known < need) {
+            unsigned seen = 0;
+            HB(4)
+            if (wlane == 0) seen = wait_lane(need);
+            HB(5)
+            // every lane: the poll has returned before any column load issues
+            seen = __builtin_amdgcn_readfirstlane(seen);
+            known = max(need, seen);
             __builtin_amdgcn_wave_barrier();
           }
           double2 buf[PW];
 #pragma unroll
           for (int u = 0; u < PW; ++u) {
             const int idx = wlane + 64 * u;
-            const int c = min(ld + idx / nthr_col, nh - 1), h = idx % nthr_col;
+            const int c = min(ld + idx / NTC, nh - 1), h = idx % NTC;
             const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
             buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
                                   __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
@@ -612,48 +557,48 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #pragma unroll
           for (int u = 0; u < PW; ++u) {
             const int idx = wlane + 64 * u;
-            const int c = ld + idx / nthr_col, h = idx % nthr_col;
+            const int c = ld + idx / NTC, h = idx % NTC;
             if (c < nh) {
               R[rslot(c)][2 * h] = buf[u].x;
               R[rslot(c)][2 * h + 1] = buf[u].y;
             }
           }
         }
-        if (t + 1 < total) ld = max(ld, nh);
-#endif
       }
-      const uint64_t c1t = __builtin_amdgcn_s_memrealtime();
+      BSTAMP(c1t)
+      HB(2)
       __syncthreads();
-      // every wave tracks ld / wb (only the I/O waves act on them)
-      if (wid != NCW + 1 && t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
-      if (wid != NCW) wb = max(wb, group_low(n, nsw, j0, g, t));
+      if (t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
+      wb = max(wb, group_low(n, nsw, j0, g, t));
+#if TG_BULGE_STATS
       const uint64_t c2t = __builtin_amdgcn_s_memrealtime();
       stk += c1t - c0t;
       sbar += c2t - c1t;
       ++nsteps;
-      if ((tid & 63) == 0) {
-        __shared__ unsigned long long wt[8];
-        if (t == 0 && G == sh_G) {}
-        (void)wt;
-        if (stats) atomicAdd(stats + 8 + wid, (unsigned long long)(c1t - c0t));
-      }
+      if (wlane == 0 && stats) atomicAdd(stats + 8 + wid, (unsigned long long)(c1t - c0t));
+#endif
     }
     // group end: write back what is left, drain, publish done
-    if (wb < ld) write_back(wb, ld);
+    for (int idx = tid; idx < (ld - wb) * NTC; idx += BT) {
+      const int c = wb + idx / NTC, h = idx % NTC;
+      const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+      const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                             (c * LDB + 2 * h) * 8, 0, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0)
-      __hip_atomic_store(prog + G, unsigned(total + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) publish(prog + G, unsigned(total + 1));
   }
+#if TG_BULGE_STATS
   if (stats && tid == 0) {
     atomicAdd(stats + 0, 1ull);
     atomicAdd(stats + 1, (unsigned long long)sw);
     atomicAdd(stats + 2, (unsigned long long)stk);
     atomicAdd(stats + 3, (unsigned long long)sbar);
-    atomicAdd(stats + 4, (unsigned long long)spf);
-    atomicAdd(stats + 5, (unsigned long long)swb);
     atomicAdd(stats + 6, (unsigned long long)nsteps);
   }
+#endif
 }
 
 // Bst[c][d] = A[c + d][c] for d <= b, 0 for b < d < 2b.
@@ -697,14 +642,25 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     if (err != hipSuccess) return err;
     unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] stall flag
     stall = ctl + 2;
-    const char *tt = getenv("TG_BULGE_TIMEOUT_TICKS");
-    const unsigned long long timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s
-    unsigned long long *stats = nullptr;
+    const unsigned long long timeout = spin_timeout_ticks("TG_BULGE_TIMEOUT_TICKS");
+    // TG_BULGE_STATS (environment): elapsed time of the launch; with a
+    // -DTG_BULGE_STATS=1 build also the per-step clock stamps per wave
     const bool want = getenv("TG_BULGE_STATS") != nullptr;
+    unsigned long long *stats = nullptr;
+#if TG_BULGE_HB
+    unsigned long long *hbh = nullptr;
+    (void)hipHostMalloc(&hbh, 256 * 16 * 8, hipHostMallocMapped);
+    memset(hbh, 0, 256 * 16 * 8);
+    (void)hipHostGetDevicePointer((void **)&stats, hbh, 0);
+    hipEvent_t hbe;
+    (void)hipEventCreateWithFlags(&hbe, hipEventDisableTiming);
+#endif
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (want) {
-      (void)hipMalloc(&stats, 16 * sizeof(unsigned long long));
-      (void)hipMemsetAsync(stats, 0, 16 * sizeof(unsigned long long), st);
+      if (TG_BULGE_STATS) {
+        (void)hipMalloc(&stats, 24 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(stats, 0, 24 * sizeof(unsigned long long), st);
+      }
       (void)hipEventCreate(&e0);
       (void)hipEventCreate(&e1);
       (void)hipEventRecord(e0, st);
@@ -714,35 +670,53 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     double ntask = 0.0;
     for (int j = 0; j < nsw; ++j) ntask += (n - 3 - j) / SB_B + 1;
     auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / G_SW,
-                          12.0 * SB_B * SB_B * ntask);
+                              12.0 * SB_B * SB_B * ntask);
     hipLaunchKernelGGL(bulge_lds_kernel, dim3(256), dim3(BT), 0, st, Bst, n, V2, tau2, sb_smax(n),
                        prog, ctl, stats, timeout);
     tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;
+#if TG_BULGE_HB
+    (void)hipEventRecord(hbe, st);
+    for (int it = 0; it < 300 && hipEventQuery(hbe) == hipErrorNotReady; ++it) usleep(10000);
+    if (hipEventQuery(hbe) == hipErrorNotReady) {
+      fprintf(stderr, "bulge HANG: heartbeat (block: wave=G/step/phase)\n");
+      for (int bk = 0; bk < 256; ++bk) {
+        bool any = false;
+        for (int w = 0; w < NCW + 2; ++w) any |= hbh[bk * 16 + w] != 0;
+        if (!any) continue;
+        fprintf(stderr, "  b%3d:", bk);
+        for (int w = 0; w < NCW + 2; ++w) {
+          const unsigned long long v = hbh[bk * 16 + w];
+          fprintf(stderr, " %llu/%llu/%llu", (v >> 32) - 1, ((v >> 8) & 0xffffff) - 1, v & 255);
+        }
+        fprintf(stderr, "\n");
+      }
+      fflush(stderr);
+      _exit(3);
+    }
+    stats = nullptr;
+#endif
     if (want) {
       (void)hipEventRecord(e1, st);
-      unsigned long long h[16];
-      (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
+      unsigned long long h[24] = {0};
+      if (stats) (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
       (void)hipStreamSynchronize(st);
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
-      const double W = double(h[0]), S = double(h[6]);
-      fprintf(stderr,
-              "bulge: %.2f ms, workers %.0f, steps/worker %.0f; per step (us): wait %.2f task %.2f "
-              "bar %.2f pfstore %.2f wb %.2f\n",
-              ms, W, S / W, h[1] / 100.0 / S, h[2] / 100.0 / S, h[3] / 100.0 / S, h[4] / 100.0 / S,
-              h[5] / 100.0 / S);
-      fprintf(stderr, "  per-wave busy per step (us):");
-      for (int w = 0; w < NCW + 2; ++w) fprintf(stderr, " w%d %.2f", w, h[8 + w] / 100.0 / S);
-      fprintf(stderr, "\n");
-#ifdef TG_BULGE_PHASES
-      unsigned long long ph[8];
-      (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph));
-      fprintf(stderr, "  D wave phases (us): loads+matvec %.3f reduce %.3f sync %.3f update %.3f (n %llu)\n",
-              ph[0] / 100.0 / ph[4], ph[1] / 100.0 / ph[4], ph[2] / 100.0 / ph[4], ph[3] / 100.0 / ph[4], ph[4]);
-#endif
-      (void)hipFree(stats);
+      fprintf(stderr, "bulge: %.2f ms (G_SW %d)\n", ms, G_SW);
+      if (stats) {
+        const double W = double(h[0]), S = double(h[6]);
+        fprintf(stderr,
+                "  workers %.0f, steps/worker %.0f; per step (us): wait %.2f task %.2f bar %.2f\n",
+                W, S / W, h[1] / 100.0 / S, h[2] / 100.0 / S, h[3] / 100.0 / S);
+        fprintf(stderr, "  per-wave busy per step (us):");
+        for (int w = 0; w < NCW + 2; ++w) fprintf(stderr, " w%d %.2f", w, h[8 + w] / 100.0 / S);
+        fprintf(stderr, "\n");
+        (void)hipFree(stats);
+      }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
     }
   }
   hipLaunchKernelGGL(extract_tri_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, Bst, n, stall, d,
@@ -1006,3 +980,58 @@ size_t sb2st_t2_count(int n) {
 }
 
 }  // namespace tg
+
+// ---------------------------------------------------------------------------
+// C ABI: the band -> tridiagonal stage on its own (tests and tools).
+// ---------------------------------------------------------------------------
+namespace {
+struct BandWs {
+  double *Bst, *V2, *tau2;
+  unsigned *prog;
+};
+template <class A>
+void band_ws_layout(A &ar, int n, BandWs *p) {
+  BandWs d{};
+  BandWs &b = p ? *p : d;
+  const size_t nsw = size_t(std::max(1, n - 2)), smax = size_t(tg::sb_smax(n));
+  if constexpr (std::is_same_v<A, tg::Arena>) {
+    b.Bst = ar.template take<double>(size_t(n) * LDB);
+    b.V2 = ar.template take<double>(nsw * smax * SB_B);
+    b.tau2 = ar.template take<double>(nsw * smax);
+    b.prog = ar.template take<unsigned>(nsw + 4);
+  } else {
+    ar.template take<double>(size_t(n) * LDB);
+    ar.template take<double>(nsw * smax * SB_B);
+    ar.template take<double>(nsw * smax);
+    ar.template take<unsigned>(nsw + 4);
+  }
+}
+}  // namespace
+
+extern "C" size_t tg_band_tridiag_workspace_size(int n) {
+  if (n < 1) return 0;
+  tg::Sizer s;
+  band_ws_layout(s, n, nullptr);
+  return s.off + 256;
+}
+
+extern "C" int tg_band_tridiag(void *stream, const double *A, int n, int lda, double *d, double *e,
+                               void *ws, size_t ws_bytes) {
+  TG_ARG(A != nullptr, 2, "A is null");
+  TG_ARG(n >= 1, 3, "n must be >= 1");
+  TG_ARG(lda >= n, 4, "lda < n");
+  TG_ARG(d != nullptr && e != nullptr, 5, "d / e is null");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  tg::Arena ar(ws, ws_bytes);
+  BandWs b{};
+  band_ws_layout(ar, n, &b);
+  TG_WS(ar);
+  TG_HIP(tg::sb2st(st, A, lda, n, b.Bst, b.V2, b.tau2, b.prog, d, e));
+  bool stalled = false;
+  TG_HIP(tg::sb2st_stalled(st, n, b.prog, &stalled));
+  if (stalled) {
+    tg::set_error("tg_band_tridiag: bulge-chasing pipeline stalled (a hand-off wait timed out)");
+    return int(hipErrorLaunchTimeOut);
+  }
+  return 0;
+}

@@ -1,0 +1,73 @@
+// Bounded spin-waits of the persistent kernels (bulge chasing, panel QR, the
+// few-vector back-transform, the pivot steps).
+//
+// Every persistent launch owns one STALL word in device memory (zeroed by the
+// host before the launch, read back after it).  A waiter that runs past its
+// timeout sets the word; every other wait of the launch also polls the word
+// and gives up as soon as it is set, so a stalled launch drains after ONE
+// timeout instead of one timeout per remaining wait (the caller reports the
+// stall and poisons its outputs).  A wait that gives up returns false.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+namespace tg {
+
+typedef __attribute__((address_space(1))) unsigned spin_u32;
+
+// Relaxed agent-scope (sc1, L1-bypassing) load / store of a control word.
+__device__ __forceinline__ unsigned ctl_load(const unsigned *p) {
+  return __hip_atomic_load((spin_u32 *)const_cast<unsigned *>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ctl_store(unsigned *p, unsigned v) {
+  __hip_atomic_store((spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane: wait until *word >= target.  `timeout` is in ticks of the
+// 100 MHz s_memrealtime clock.  Returns the last value seen (>= target on
+// success) through *seen when non-null.
+__device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned *stall,
+                                unsigned long long timeout, unsigned *seen = nullptr) {
+  unsigned v = ctl_load(word);
+  if (v >= target) {
+    if (seen) *seen = v;
+    return true;
+  }
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned it = 0;; ++it) {
+    __builtin_amdgcn_s_sleep(1);
+    v = ctl_load(word);
+    if (v >= target) break;
+    if ((it & 31u) == 0u) {
+      if (ctl_load(stall) != 0u) {
+        if (seen) *seen = v;
+        return false;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        ctl_store(stall, 1u);
+        if (seen) *seen = v;
+        return false;
+      }
+    }
+  }
+  if (seen) *seen = v;
+  return true;
+}
+
+// Host: spin timeout of the persistent kernels, in 100 MHz ticks.  Every wait
+// in them is one pipeline step or one grid barrier (microseconds), so the
+// default of 2 s only ever fires on a real stall; TG_SPIN_TIMEOUT_MS
+// overrides it, the per-kernel variables (TG_BULGE_TIMEOUT_TICKS, ...) too.
+inline unsigned long long spin_timeout_ticks(const char *kernel_env) {
+  if (kernel_env) {
+    const char *t = getenv(kernel_env);
+    if (t) return strtoull(t, nullptr, 10);
+  }
+  const char *ms = getenv("TG_SPIN_TIMEOUT_MS");
+  return ms ? strtoull(ms, nullptr, 10) * 100000ull : 200000000ull;
+}
+
+}  // namespace tg

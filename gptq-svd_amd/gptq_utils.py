@@ -280,14 +280,31 @@ class Quantizer:
 # A6  (gptq_utils.py:275-291)
 # ---------------------------------------------------------------------------
 def log_quantization_error(W_orig, W_quant, R_x, perm):
+    """||(W_o - W_q) R_x^T||_F / ||W_o R_x^T||_F with W_o = W_orig[:, perm],
+    logged in the reference's format (extract_log.py:20 parses it).  Both
+    products run in ONE fused FP32 MFMA pass (tg_pred_error: R_x is read as
+    float64 and rounded to float32 like the reference's R_x.to(float32), the
+    m x k products never leave the chip, their sums of squares are FP64).
+    Returns the value (the reference returns None)."""
     if R_x is None or perm is None:
         return None
-    R_mat = R_x.to(device=W_orig.device, dtype=torch.float32)
-    W_o = W_orig[:, perm]
-    W_q = W_quant[:, perm]
-    y_orig_norm = torch.linalg.norm(torch.matmul(W_o, R_mat.T))
-    y_diff_norm = torch.linalg.norm(torch.matmul(W_o - W_q, R_mat.T))
-    relative_error = (y_diff_norm / y_orig_norm).item()
+    _lib.require_cuda(W_orig, "log_quantization_error W_orig")
+    dev = W_orig.device
+    W = W_orig.to(torch.float32).contiguous()
+    Wq = W_quant.to(device=dev, dtype=torch.float32).contiguous()
+    R = R_x.to(device=dev, dtype=torch.float64).contiguous()
+    p = perm.to(device=dev, dtype=torch.int64).contiguous()
+    m, n = W.shape
+    k = R.shape[0]
+    if Wq.shape != W.shape or R.shape[1] != n or p.numel() != n:
+        raise RuntimeError("log_quantization_error: shape mismatch")
+    out = torch.empty(2, dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        ws = workspace(_lib.lib.tg_pred_error_workspace_size(m, n, k), dev)
+        call("tg_pred_error", stream(), ptr(W), ptr(Wq), m, n, n, ptr(R), k, n, ptr(p), ptr(out),
+             ptr(ws), ws.numel())
+    y_orig_sq, y_diff_sq = out.tolist()  # the reference's .item() sync (:290)
+    relative_error = (y_diff_sq ** 0.5) / (y_orig_sq ** 0.5)
     logging.info(f"   [Metric] Relative prediction error: {relative_error:.6f}")
     return relative_error
 

@@ -74,6 +74,16 @@ int tg_eigh_vectors(void *stream, int n, const double *w_asc, int k, double *Vh,
  * complement path below asks for the dropped eigenpairs k .. k+nc-1. */
 int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, int first, int count,
                           double *Vh, int ldv, void *ws, size_t ws_bytes);
+/* The band -> tridiagonal stage of tg_eigh_values on its own (tests, tools):
+ * A (n x n, full storage, ld lda) holds a symmetric band matrix of
+ * half-bandwidth 32 (only the lower band A[c + d][c], d <= 32, is read);
+ * on return d (n) / e (n - 1 used) hold a similar symmetric tridiagonal.
+ * Bulge chasing as in tg_eigh_values (part of the eigh of
+ * gptq_utils.py:93).  Synchronises the stream (reads the stall word);
+ * a stalled hand-off returns hipErrorLaunchTimeOut. */
+size_t tg_band_tridiag_workspace_size(int n);
+int tg_band_tridiag(void *stream, const double *A, int n, int lda, double *d, double *e, void *ws,
+                    size_t ws_bytes);
 
 /* ---- A3: truncation rank (gptq_utils.py:97-108) ---------------------------
  * From ascending eigenvalues: S = sqrt(max(L, 1e-12)) descending, then the
@@ -112,6 +122,18 @@ int tg_pivoted_factor_complement(void *stream, const double *H, int ldh, const d
 size_t tg_ufactor_rx_workspace_size(int n, int k);
 int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U, int ldu,
                    void *ws, size_t ws_bytes);
+
+/* ---- A6: relative prediction error (log_quantization_error,
+ * gptq_utils.py:275-291) ---------------------------------------------------
+ * out[0] = ||W[:, perm] R^T||_F^2, out[1] = ||(W - Wq)[:, perm] R^T||_F^2
+ * (device, 2 doubles) with R = R_x (k x n, ld ldr) rounded to float32, the
+ * reference's `R_x.to(float32)`.  W, Wq: m x n float32 (ld ldw), original
+ * column order; perm: n int64.  The products are FP32 MFMA (TF32 off in the
+ * reference), the sums of squares FP64; the caller takes sqrt(out[1] / out[0]). */
+size_t tg_pred_error_workspace_size(int m, int n, int k);
+int tg_pred_error(void *stream, const float *W, const float *Wq, int m, int n, int ldw,
+                  const double *Rx, int k, int ldr, const int64_t *perm, double *out, void *ws,
+                  size_t ws_bytes);
 
 /* ---- A7: Quantizer.find_params (gptq_utils.py:249-266) --------------------
  * W (m x n f32, ld ldw) -> scale, zero (m x n/g f32, ld n/g); g = group or n. */

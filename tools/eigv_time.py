@@ -32,7 +32,10 @@ for r in range(reps + 1):
     if r:
         ts.append(1e3 * (time.perf_counter() - t0))
 wc = w.cpu().numpy()
+ref = np.linalg.eigvalsh(H.cpu().numpy())
+err = float(np.abs(wc - ref).max() / np.abs(ref).max())
 if len(sys.argv) > 1:
     np.save(sys.argv[1], wc)
-print(f"{os.path.basename(lib.LIB_PATH)}: eigh_values min {min(ts):.2f} med {np.median(ts):.2f} ms",
+print(f"{os.path.basename(lib.LIB_PATH)}: eigh_values min {min(ts):.2f} med {np.median(ts):.2f} ms"
+      f" max|w - w_lapack|/|w|max = {err:.2e}",
       flush=True)
