@@ -66,6 +66,7 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
                     unsigned *tmo);
 
 int sb_smax(int n);
+size_t sb2st_prog_words(int n);
 size_t sb2st_t2_count(int n);
 
 // control words: 4 + 4 per panel, padded to a multiple of 16 bytes
@@ -101,8 +102,8 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.tau2, nsw * smax);
   take(b.T2, sb2st_t2_count(n));
   // per-group progress + 4 control words (XCD, group queue, stall flag)
-  if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(nsw + 4);
-  else ar.template take<unsigned>(nsw + 4);
+  if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(sb2st_prog_words(n));
+  else ar.template take<unsigned>(sb2st_prog_words(n));
   // partials: panel QR (2 per worker), X row blocks, M (one per 128 rows)
   const size_t npart = std::max<size_t>(std::max<size_t>(2 * PQR_NWMAX + 2, size_t(n) / SB_C + 2),
                                         size_t(n) / 128 + 2) * 1024;

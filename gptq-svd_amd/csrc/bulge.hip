@@ -117,7 +117,7 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 #define TG_BULGE_WDEFER 0
 #endif
 #ifndef TG_BULGE_STATS
-#define TG_BULGE_STATS 1  // per-step s_memrealtime stamps (TEMPORARY default: see DESIGN.md §8)
+#define TG_BULGE_STATS 0  // per-step s_memrealtime stamps (build-time: they slow every step)
 #endif
 constexpr int G_SW = TG_BULGE_GSW;   // sweeps per group (wave triples per workgroup)
 constexpr int LAG = 2;               // pipeline lag between consecutive sweeps (tasks)
@@ -371,6 +371,18 @@ __device__ inline int group_high(int n, int j0, int t) {
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// Lane-0 operations without a lane-0 branch.  A `if (tid == 0)` block next to
+// the group loop's back edge let the compiler's CFG structurizer give lane 0
+// of wave 0 a loop nest of its own (it left the inner loop through an exec
+// mask at the group end and re-entered at the group take), so that wave
+// executed the group's barriers once for lane 0 and once for lanes 1-63 and
+// the workgroup deadlocked (diagnosed with a per-wave live-lane heartbeat:
+// wave 0 ran with 63 lanes).  Every lane of the wave executes these: lane 0
+// on the real word, the others on a private dummy word of their own.
+__device__ __forceinline__ unsigned *lane0_or_dummy(unsigned *real, unsigned *dummy, int wlane) {
+  return wlane == 0 ? real : dummy + wlane;
+}
+
 __device__ __forceinline__ void publish(unsigned *p, unsigned v) {
 #if TG_BULGE_FLAG_L2
   __hip_atomic_store((tg::spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -388,10 +400,15 @@ __device__ __forceinline__ void publish(unsigned *p, unsigned v) {
 #define TG_BULGE_HB 0  // debug: per-wave heartbeat (group, step, phase) into host memory
 #endif
 #if TG_BULGE_HB
-#define HB(ph) \
-  if (wlane == 0) \
-    ((volatile unsigned long long *)stats)[blockIdx.x * 16 + wid] = \
-        (unsigned long long)(G + 1) << 32 | (unsigned long long)(t + 1) << 8 | (ph);
+// record (group, step, live lanes, phase) from the first active lane
+#define HB(ph)                                                                          \
+  {                                                                                     \
+    const unsigned long long ex_ = __builtin_amdgcn_read_exec();                        \
+    if (int(__lane_id()) == __builtin_ctzll(ex_))                                       \
+      ((volatile unsigned long long *)stats)[blockIdx.x * 16 + wid] =                   \
+          (unsigned long long)(G + 1) << 32 | (unsigned long long)(t + 1) << 16 |       \
+          (unsigned long long)__builtin_popcountll(ex_) << 8 | (ph);                    \
+  }
 #else
 #define HB(ph)
 #endif
@@ -412,8 +429,11 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   __shared__ Refl rfl[G_SW][2];
   __shared__ int sh_G;
   __shared__ int sh_dead;  // a wait of this workgroup gave up: no further waits
-  const int tid = threadIdx.x, wid = tid >> 6, wlane = tid & 63;
+  // wave index as an SGPR: every role branch below is a scalar (SCC) branch, no exec masks
+  const int tid = threadIdx.x, wlane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   unsigned *stall = ctl + 2;
+  unsigned *dummy = ctl + 4;  // 64 words: the lanes 1-63 targets of lane-0 operations
   if (tid == 0) {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
@@ -425,7 +445,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     sh_dead = 0;
   }
   __syncthreads();
-  if (sh_G < 0) return;
+  if (__builtin_amdgcn_readfirstlane(sh_G) < 0) return;  // uniform: no exec-masked kernel body
   const int nsw = n - 2;
   const int ngroups = tg::cdiv(nsw, G_SW);
   const int bytes = n * LDB * int(sizeof(double));
@@ -435,12 +455,16 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   constexpr int PFN = SB_B * NTC / BT + 1;  // chunks per thread of a whole-workgroup load
   constexpr int PW = SB_B * NTC / 64;       // chunks per lane of the loader wave
   while (true) {
-    if (tid == 0) {
+    if (wid == 0) {
       // a stalled launch: stop taking groups (the results are poisoned anyway)
-      sh_G = tg::ctl_load(stall) ? ngroups : int(atomicAdd(ctl + 1, 1u));
+      const unsigned v = atomicAdd(lane0_or_dummy(ctl + 1, dummy, wlane), 1u);
+      const int Gn = tg::ctl_load(stall) ? ngroups : int(__builtin_amdgcn_readfirstlane(v));
+      sh_G = Gn;  // every lane writes the same value
     }
     __syncthreads();
-    const int G = sh_G;
+    // scalar (SGPR) copy: every loop bound below is wave-uniform to the compiler too,
+    // so the step loop is a plain scalar loop around its barrier
+    const int G = __builtin_amdgcn_readfirstlane(sh_G);
     __syncthreads();
     if (G >= ngroups) break;
     const int j0 = G * G_SW;
@@ -449,18 +473,20 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     const int ptotal = G > 0 ? group_steps(n, nsw, G - 1) : 0;
     // progress of the producer group known to this thread (the loader wave's
     // lanes and the group-start wait keep it; ptotal + 1 = finished + written back)
-    unsigned known = (G > 0) ? 0u : ~0u;
-    // one lane: wait until the producer published `need`
-    auto wait_lane = [&](unsigned need) -> unsigned {
+    unsigned known = __builtin_amdgcn_readfirstlane((G > 0) ? 0u : ~0u);
+    // one whole wave: wait until the producer published `need` (wave-uniform)
+    auto wait_wave = [&](unsigned need) -> unsigned {
       unsigned seen = 0;
-      if (!sh_dead && !tg::spin_geq(prog + G - 1, need, stall, timeout, &seen)) sh_dead = 1;
+      if (!__builtin_amdgcn_readfirstlane(sh_dead) &&
+          !tg::spin_geq(prog + G - 1, need, stall, timeout, &seen))
+        sh_dead = 1;
       return seen;
     };
     // initial window [j0, high(0)): every thread loads, after one wait
     {
       const unsigned need = unsigned(min(group_need(0), ptotal + 1));
       BSTAMP(tw)
-      if (G > 0 && tid == 0) wait_lane(need);
+      if (G > 0 && wid == 0) wait_wave(need);
       __syncthreads();
       if (G > 0) known = need;
 #if TG_BULGE_STATS
@@ -504,10 +530,12 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           const bool nx = s + 1 < ntasks(n, jj);
           const Refl &ri = rfl[pair][t & 1];
           Refl &ro = rfl[pair][(t + 1) & 1];
+          HB(6)
           if (r1 >= SB_B && r1 + 2 * SB_B <= n)
             bulge_task_lds<true>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
           else
             bulge_task_lds<false>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
+          HB(7)
         } else if (pair < g && pair > 0 && s == -1 && role == 2) {
           first_refl(R, n, j0 + pair, rfl[pair][(t + 1) & 1]);
         }
@@ -515,35 +543,38 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #if TG_BULGE_WDEFER
         // writer: the stores of step t-1 had a step to drain; publish t-1 first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (t > 0 && wlane == 0) publish(prog + G, unsigned(t - 1));
+        if (t > 0) publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t - 1));
 #endif
         // writer: retire the columns step t-1 left behind, drain, publish t
         const int nl = group_low(n, nsw, j0, g, t);
-        for (int idx = wlane; idx < (nl - wb) * NTC; idx += 64) {
-          const int c = wb + idx / NTC, h = idx % NTC;
-          const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
-          const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                 (c * LDB + 2 * h) * 8, 0, 0);
+        // wave-uniform trip count (scalar loop), the tail masked by an if
+        const int lim = (nl - wb) * NTC;
+        for (int b0 = 0; b0 < lim; b0 += 64) {
+          const int idx = b0 + wlane;
+          if (idx < lim) {
+            const int c = wb + idx / NTC, h = idx % NTC;
+            const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+            const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                   (c * LDB + 2 * h) * 8, 0, 0);
+          }
         }
+        HB(8)
 #if !TG_BULGE_WDEFER
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (wlane == 0) publish(prog + G, unsigned(t));
+        publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
 #endif
+        HB(9)
       } else {
         // loader: the columns step t + 1 adds
         const int nh = group_high(n, j0, t + 1);
         if (t + 1 < total && nh > ld) {
           const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
           if (known < need) {
-            unsigned seen = 0;
             HB(4)
-            if (wlane == 0) seen = wait_lane(need);
+            // the column loads below issue after the poll has returned
+            known = max(need, wait_wave(need));
             HB(5)
-            // every lane: the poll has returned before any column load issues
-            seen = __builtin_amdgcn_readfirstlane(seen);
-            known = max(need, seen);
-            __builtin_amdgcn_wave_barrier();
           }
           double2 buf[PW];
 #pragma unroll
@@ -563,6 +594,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
               R[rslot(c)][2 * h + 1] = buf[u].y;
             }
           }
+          HB(10)
         }
       }
       BSTAMP(c1t)
@@ -579,16 +611,22 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #endif
     }
     // group end: write back what is left, drain, publish done
-    for (int idx = tid; idx < (ld - wb) * NTC; idx += BT) {
-      const int c = wb + idx / NTC, h = idx % NTC;
-      const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
-      const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                             (c * LDB + 2 * h) * 8, 0, 0);
+    {
+      const int lim = (ld - wb) * NTC;  // uniform trip count, masked tail
+      for (int b0 = 0; b0 < lim; b0 += BT) {
+        const int idx = b0 + tid;
+        if (idx < lim) {
+          const int c = wb + idx / NTC, h = idx % NTC;
+          const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+          const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                 (c * LDB + 2 * h) * 8, 0, 0);
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) publish(prog + G, unsigned(total + 1));
+    if (wid == 0) publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(total + 1));
   }
 #if TG_BULGE_STATS
   if (stats && tid == 0) {
@@ -628,6 +666,9 @@ namespace tg {
 
 int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 
+// progress word per sweep group + control words + 64 dummy words
+size_t sb2st_prog_words(int n) { return size_t(cdiv(std::max(1, n - 2), G_SW)) + 4 + 64; }
+
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
                  double *tau2, unsigned *prog, double *d, double *e) {
   hipLaunchKernelGGL(extract_band_kernel, dim3(cdiv(int64_t(n) * LDB, 256)), dim3(256), 0, st, A,
@@ -638,7 +679,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
   const unsigned *stall = nullptr;
   if (nsw > 0) {
     const int ngroups = cdiv(nsw, G_SW);
-    err = hipMemsetAsync(prog, 0, sizeof(unsigned) * (ngroups + 4), st);
+    err = hipMemsetAsync(prog, 0, sizeof(unsigned) * sb2st_prog_words(n), st);
     if (err != hipSuccess) return err;
     unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] stall flag
     stall = ctl + 2;
@@ -680,7 +721,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     (void)hipEventRecord(hbe, st);
     for (int it = 0; it < 300 && hipEventQuery(hbe) == hipErrorNotReady; ++it) usleep(10000);
     if (hipEventQuery(hbe) == hipErrorNotReady) {
-      fprintf(stderr, "bulge HANG: heartbeat (block: wave=G/step/phase)\n");
+      fprintf(stderr, "bulge HANG: heartbeat (block: wave=G/step/lanes/phase)\n");
       for (int bk = 0; bk < 256; ++bk) {
         bool any = false;
         for (int w = 0; w < NCW + 2; ++w) any |= hbh[bk * 16 + w] != 0;
@@ -688,7 +729,8 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
         fprintf(stderr, "  b%3d:", bk);
         for (int w = 0; w < NCW + 2; ++w) {
           const unsigned long long v = hbh[bk * 16 + w];
-          fprintf(stderr, " %llu/%llu/%llu", (v >> 32) - 1, ((v >> 8) & 0xffffff) - 1, v & 255);
+          fprintf(stderr, " %llu/%llu/%llu/%llu", (v >> 32) - 1, ((v >> 16) & 0xffff) - 1, (v >> 8) & 255,
+                  v & 255);
         }
         fprintf(stderr, "\n");
       }
@@ -998,12 +1040,12 @@ void band_ws_layout(A &ar, int n, BandWs *p) {
     b.Bst = ar.template take<double>(size_t(n) * LDB);
     b.V2 = ar.template take<double>(nsw * smax * SB_B);
     b.tau2 = ar.template take<double>(nsw * smax);
-    b.prog = ar.template take<unsigned>(nsw + 4);
+    b.prog = ar.template take<unsigned>(tg::sb2st_prog_words(n));
   } else {
     ar.template take<double>(size_t(n) * LDB);
     ar.template take<double>(nsw * smax * SB_B);
     ar.template take<double>(nsw * smax);
-    ar.template take<unsigned>(nsw + 4);
+    ar.template take<unsigned>(tg::sb2st_prog_words(n));
   }
 }
 }  // namespace

@@ -26,35 +26,37 @@ __device__ __forceinline__ void ctl_store(unsigned *p, unsigned v) {
   __hip_atomic_store((spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane: wait until *word >= target.  `timeout` is in ticks of the
-// 100 MHz s_memrealtime clock.  Returns the last value seen (>= target on
-// success) through *seen when non-null.
+// Wait until *word >= target.  Called by EVERY lane of a wave (the lanes
+// load the same word in one request and the value is made scalar), so the
+// loop and its exits are wave-uniform scalar branches: no exec-masked loop
+// with divergent exits inside the callers' barrier loops.  `timeout` is in
+// ticks of the 100 MHz s_memrealtime clock.  The last value seen goes to
+// *seen when non-null.
 __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned *stall,
                                 unsigned long long timeout, unsigned *seen = nullptr) {
-  unsigned v = ctl_load(word);
-  if (v >= target) {
-    if (seen) *seen = v;
-    return true;
-  }
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (unsigned it = 0;; ++it) {
-    __builtin_amdgcn_s_sleep(1);
-    v = ctl_load(word);
-    if (v >= target) break;
-    if ((it & 31u) == 0u) {
-      if (ctl_load(stall) != 0u) {
-        if (seen) *seen = v;
-        return false;
-      }
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-        ctl_store(stall, 1u);
-        if (seen) *seen = v;
-        return false;
+  unsigned v = __builtin_amdgcn_readfirstlane(ctl_load(word));
+  bool ok = true;
+  if (v < target) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned it = 0;; ++it) {
+      __builtin_amdgcn_s_sleep(1);
+      v = __builtin_amdgcn_readfirstlane(ctl_load(word));
+      if (v >= target) break;
+      if ((it & 31u) == 0u) {
+        if (__builtin_amdgcn_readfirstlane(ctl_load(stall)) != 0u) {
+          ok = false;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+          ctl_store(stall, 1u);
+          ok = false;
+          break;
+        }
       }
     }
   }
   if (seen) *seen = v;
-  return true;
+  return ok;
 }
 
 // Host: spin timeout of the persistent kernels, in 100 MHz ticks.  Every wait

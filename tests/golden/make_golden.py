@@ -24,6 +24,8 @@ import torch
 
 REF = "/root/reference/src/TruncGPTQ"
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from synth import make_x  # noqa: E402  (shared with the tests)
 
 
 def install_shim():
@@ -50,22 +52,6 @@ def install_shim():
     sys.path.insert(0, REF)
     import gptq_utils  # noqa: E402
     return gptq_utils
-
-
-def make_x(kind, N, n, gen):
-    """Synthetic activations following benchmarks.py:31-79 make_X recipes."""
-    if kind == "gaussian":
-        X = torch.randn(N, n, generator=gen)
-    elif kind == "ar1":  # gaussian_corr, AR(1) rho=0.9 (benchmarks.py:18-28, :50-54)
-        idx = torch.arange(n)
-        Sigma = 0.9 ** (idx[None, :] - idx[:, None]).abs().double()
-        L = torch.linalg.cholesky(Sigma + 1e-6 * torch.eye(n, dtype=torch.float64)).float()
-        X = torch.randn(N, n, generator=gen) @ L.T
-    elif kind == "lognormal":
-        X = torch.exp(0.5 * torch.randn(N, n, generator=gen))
-    else:
-        raise ValueError(kind)
-    return X.half()  # real hook inputs are fp16 (quantize.py:127-130)
 
 
 # name, n, m, N, xkind, bits, group, sym, eps, method, block_size
@@ -177,6 +163,57 @@ GPTQ = [
 ]
 
 
+# OPT-125M shapes (BASELINE config 1: q/k/v/out_proj and fc1 read d = 768,
+# fc2 reads 3072; 4-bit asym g128).  The inputs are regenerated from the seed
+# by the test (gaussian X only: pure RNG, no BLAS), so the fixture holds only
+# outputs: rank, perm, eigenvalues, U through 4 probe vectors, codes.
+# name, n, m, N, bits, group, sym, eps, method, block_size
+OPT = [
+    ("o_opt_qkv_n768_m768", 768, 768, 1536, 4, 128, False, 1e-4, "energy", 1024),
+    ("o_opt_fc1_n768_m3072", 768, 3072, 1536, 4, 128, False, 1e-4, "energy", 1024),
+    ("o_opt_fc2_n3072_m768", 3072, 768, 4608, 4, 128, False, 1e-4, "energy", 1024),
+]
+
+
+def opt_probes(n, seed):
+    return torch.randn(n, 4, generator=torch.Generator().manual_seed(seed + 99),
+                       dtype=torch.float64)
+
+
+def gen_opt(g, spec, seed):
+    import logging
+    name, n, m, N, bits, group, sym, eps, method, bs = spec
+    gen = torch.Generator().manual_seed(seed)
+    X = make_x("gaussian", N, n, gen)
+    W = torch.randn(m, n, generator=gen) * 0.05
+    acc = g.HessianAccumulator(n, "cpu")
+    acc.add_batch(X)
+    H = acc.get_hessian()
+    R, R_x, perm = g.process_hessian_alt(H, threshold=eps, threshold_method=method)
+    q = g.Quantizer(w_bits=bits, group_size=group, sym=sym)
+    lines = []
+    h = logging.Handler()
+    h.emit = lambda r: lines.append(r.getMessage())
+    logging.getLogger().addHandler(h)
+    logging.getLogger().setLevel(logging.INFO)
+    final_W, k = g.gptq_fwrd(W.clone(), R, q, perm, block_size=bs, use_triton=True, R_x=R_x)
+    logging.getLogger().removeHandler(h)
+    L, _ = torch.linalg.eigh(H.double())
+    S = torch.sqrt(L.clamp(min=1e-12)).flip(0)
+    s_, z_ = q.get_expanded_params(m, n)
+    codes = torch.round(final_W / s_ + z_)       # exact: final_W = (q - z) s
+    assert torch.equal((codes - z_) * s_, final_W)
+    metric = [ln for ln in lines if "Relative prediction error" in ln][-1]
+    return name, dict(
+        seed=np.int64(seed), N=np.int64(N), n=np.int64(n), m=np.int64(m), k=np.int64(k),
+        perm=perm.numpy().astype(np.int32), S=S.numpy(),
+        Uprobe=(R @ opt_probes(n, seed)).numpy(), Unorm=np.float64(torch.linalg.norm(R)),
+        codes=codes.numpy().astype(np.uint8), scale=q.scale.squeeze(-1).numpy(),
+        zero=q.zero.squeeze(-1).numpy(), bits=np.int64(bits), group=np.int64(group),
+        sym=np.bool_(sym), eps=np.float64(eps), method=np.str_(method), block_size=np.int64(bs),
+        metric_line=np.str_(metric))
+
+
 def gen_gptq(g, spec, seed):
     name, n, m, N, xkind, bits, group, sym, actorder, bs, hov = spec
     gen = torch.Generator().manual_seed(seed)
@@ -242,6 +279,12 @@ def main():
         name, d = gen_gptq(g, spec, 3000 + i)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name)
+    for i, spec in enumerate(OPT):
+        if only and spec[0] not in only:
+            continue
+        name, d = gen_opt(g, spec, 5000 + i)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+        print("wrote", name, "k =", int(d["k"]), str(d["metric_line"]))
     for i, spec in enumerate(SPECTRA):
         if only and spec[0] not in only:
             continue

@@ -9,7 +9,8 @@ seeded inputs (numpy/LAPACK eigh + dgeqp3 + QR: ~5 s on the box's host cores).
   codes end to end   mismatch rate <= 6e-4    (the reference's own
                                                Triton-vs-loop disagreement)
 
-n = 8192 / 12288 / 14336 (Llama-3-70B q/o, Qwen3-8B down, Llama-3-8B down):
+n = 8192 / 12288 / 14336 / 28672 (Llama-3-70B q/o, Qwen3-8B down, Llama-3-8B
+down, Llama-3-70B down -- BASELINE configs 3-5):
 size-independent identities (the oracle would take minutes there):
   ||P^T H P - R_x^T R_x||_F = sqrt(sum_{i>k} S_i^4)   rel. <= 1e-8
       (H - H_k = V_r L_r V_r^T for the discarded eigenpairs)
@@ -104,11 +105,17 @@ def test_fullsize_end_to_end(g, bench_layer, oracle_mod):
 
 
 @pytest.mark.parametrize("n,path", [(8192, "kept"), (8192, "complement"), (12288, "complement"),
-                                    (14336, "complement"), (14336, "kept")])
+                                    (14336, "complement"), (14336, "kept"),
+                                    (28672, "complement"), (28672, "kept")])
 def test_large_n_identities(g, oracle_mod, n, path, monkeypatch):
+    import time
     monkeypatch.setenv("TG_SPECTRAL_PATH", path)
     _, H = wishart(g, n, 3 * n // 4, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     U, R_x, perm, S, k = g.truncated_spectral_factor(H, 1e-4, "energy")
+    torch.cuda.synchronize()
+    print(f"n={n} {path}: k={k}, process_hessian_alt {time.perf_counter() - t0:.3f} s")
     assert g.truncated_spectral_factor.last_path[0] == path
     assert 0 < k <= 3 * n // 4 + 1
     assert torch.equal(torch.sort(perm).values, torch.arange(n, device=DEV))
