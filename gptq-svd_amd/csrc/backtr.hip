@@ -24,6 +24,7 @@
 
 #include "band.h"
 #include "common.h"
+#include "spin.h"
 
 namespace {
 
@@ -108,22 +109,15 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Step done by this workgroup; wait for all workers.
+// Step done by this workgroup; wait for all workers.  Wave 0 arrives and
+// polls as a whole wave (scalar loop, spin.h); a stalled barrier sets cnt[1]
+// and every later barrier of the launch returns at once.
 __device__ inline void grid_barrier(const BtArgs &a, unsigned target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Z stores drained
   __syncthreads();
-  if (threadIdx.x == 0) {
-    gu32 *c = (gu32 *)(a.cnt);
-    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-        __hip_atomic_store((gu32 *)(a.cnt + 1), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    tg::wave_arrive(a.cnt);
+    tg::spin_geq(a.cnt, target, a.cnt + 1, a.timeout);
 #if !TG_BT_XCD
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -732,8 +726,7 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.single = pl.single ? 1 : 0;
   a.part = reinterpret_cast<double *>(static_cast<char *>(dev) + few_ops_bytes(pl));
   a.cnt = cnt;
-  const char *tt = getenv("TG_BT_TIMEOUT_TICKS");
-  a.timeout = tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
+  a.timeout = spin_timeout_ticks("TG_BT_TIMEOUT_TICKS");
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
   int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
   // the workers (one CU each: BtShared fills the LDS) must all be resident:

@@ -31,6 +31,7 @@
 
 #include "../../include/truncgptq.h"
 #include "common.h"
+#include "spin.h"
 #include "gemm64.h"
 #include "reduce.h"
 
@@ -438,19 +439,12 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
     __syncthreads();
     PVT(3)
     // all-to-all: wait for every workgroup's candidate of this step
-    if (tid == 0) {
-      __hip_atomic_fetch_add(w.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // wave 0 as a whole wave (scalar loop, spin.h): arrive, bounded poll; a
+    // stall sets flag[15] and ends every later wait of the launch at once
+    if (__builtin_amdgcn_readfirstlane(wid) == 0) {
+      tg::wave_arrive(w.cnt);
       const unsigned target = base + unsigned(G) * unsigned(t + 1);
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      s_me = 0;
-      while (__hip_atomic_load(w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: abandon, flag it
-          __hip_atomic_store(w.flag + 15, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_me = -1;
-          break;
-        }
-      }
+      s_me = tg::spin_geq(w.cnt, target, w.flag + 15, 200000000ull) ? 0 : -1;
     }
     __syncthreads();
     if (s_me < 0) return;

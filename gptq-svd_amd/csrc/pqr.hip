@@ -33,6 +33,7 @@
 
 #include "band.h"
 #include "common.h"
+#include "spin.h"
 #include "lanes.h"
 
 namespace {
@@ -137,24 +138,16 @@ __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Grid barrier (counter form): every wave's sc1 stores drained, one add per
-// workgroup, a bounded relaxed poll by one lane.
+// Grid barrier (counter form): every wave's sc1 stores drained, one arrival
+// per workgroup and a bounded poll, both by wave 0 as a whole wave (scalar
+// loop, spin.h); a stalled barrier sets *tmo and later ones return at once.
 __device__ __forceinline__ void grid_bar(const PqrArgs &g, unsigned &ep) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ++ep;
-  if (threadIdx.x == 0) {
-    gu32 *c = (gu32 *)(g.cnt);
-    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = unsigned(g.nw) * ep;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > g.timeout) {
-        __hip_atomic_store((gu32 *)(g.tmo), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    tg::wave_arrive(g.cnt);
+    tg::spin_geq(g.cnt, unsigned(g.nw) * ep, g.tmo, g.timeout);
   }
   __syncthreads();
 }
@@ -937,10 +930,7 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
   g.bc = bc;
   g.cnt = cnt;
   g.tmo = tmo;
-  static const unsigned long long tmo_ticks = [] {
-    const char *tt = getenv("TG_PQR_TIMEOUT_TICKS");
-    return tt ? strtoull(tt, nullptr, 10) : 200000000ull;  // 2 s of the 100 MHz clock
-  }();
+  static const unsigned long long tmo_ticks = spin_timeout_ticks("TG_PQR_TIMEOUT_TICKS");
   g.timeout = tmo_ticks;
   {
     const char *fb = getenv("TG_PQR_FALLBACK");

@@ -59,6 +59,16 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
   return ok;
 }
 
+// One arrival on a counter by a whole wave without a lane-0 branch: lane 0
+// adds 1, the other lanes add 0 (a lane-0 `if` next to a loop that holds
+// barriers can let the CFG structurizer run lane 0 through a loop nest of its
+// own, bulge.hip).  Returns the value before lane 0's add.
+__device__ __forceinline__ unsigned wave_arrive(unsigned *cnt) {
+  const unsigned one = (__lane_id() == 0) ? 1u : 0u;
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_fetch_add((spin_u32 *)cnt, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Host: spin timeout of the persistent kernels, in 100 MHz ticks.  Every wait
 // in them is one pipeline step or one grid barrier (microseconds), so the
 // default of 2 s only ever fires on a real stall; TG_SPIN_TIMEOUT_MS

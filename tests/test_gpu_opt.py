@@ -7,7 +7,7 @@
    m = 768).  End to end on the GPU (own H, eigh, perm, U, codes):
      k, perm identical; S rel <= 1e-12; U through 4 probe vectors rel <= 1e-8
      (bar 1e-3); codes mismatch <= 6e-4 (the reference's own Triton-vs-loop
-     disagreement); the A6 log line equal to the reference's.
+     disagreement); the A6 log line's value within the reference's 6th decimal.
 2. The harness on a tiny random OPT (the reference harness cannot run OPT:
    quantize.py:98 reads model.model.rotary_emb): every linear of every
    layer quantised once in the reference's group order, ranks in range,
@@ -65,8 +65,14 @@ def test_opt_shapes_end_to_end(name, caplog):
     mism = float(np.mean(codes != d["codes"]))
     print(f"{name}: k={k}, code mismatch vs reference {mism:.2e}")
     assert mism <= 6e-4
+    # the A6 line: extract_log.py:20's pattern, the value within the 6th
+    # decimal of the reference's (its FP32 sums vs our FP64 sums of squares)
+    import re
     lines = [r.getMessage() for r in caplog.records if "Relative prediction error" in r.getMessage()]
-    assert lines[-1] == str(d["metric_line"]), (lines[-1], str(d["metric_line"]))
+    pat = re.compile(r"Relative prediction error:\s+([\d\.]+)")
+    got = float(pat.search(lines[-1]).group(1))
+    ref = float(pat.search(str(d["metric_line"])).group(1))
+    assert abs(got - ref) <= 1.5e-6, (lines[-1], str(d["metric_line"]))
 
 
 def tiny_opt(seed):
