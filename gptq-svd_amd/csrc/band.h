@@ -12,7 +12,7 @@ namespace tg {
 constexpr int SB_B = 32;    // half-bandwidth of the band matrix (= panel width)
 constexpr int SB_C = 256;   // TSQR leaf height (last leaf of a level absorbs < SB_C rows)
 constexpr int SB_LV = 6;    // max TSQR levels
-constexpr int PQR_NWMAX = 32;        // panel-QR workgroups (pqr.hip)
+constexpr int PQR_NWMAX = 256;       // panel-QR workgroups (pqr.hip): 256 rows each, one per CU
 constexpr int PQR_BC_DOUBLES = 8192; // panel-QR broadcast block
 
 // One TSQR level of one panel: `rows` stacked rows split in `nc` chunks.
@@ -26,8 +26,9 @@ struct SbPanel {
 };
 
 // single: one compact-WY block per panel (Y m x 32, one T; pqr.hip panel
-// QR), the default for n <= 32768; otherwise (or TG_SB_TSQR=1) the TSQR tree
-// of leaves of SB_C rows.  A panel's levels are then one level of one chunk
+// QR), the default while the panel QR takes the first panel's rows
+// (pqr_rows_per_thread); otherwise (or TG_SB_TSQR=1) the TSQR tree of leaves
+// of SB_C rows.  A panel's levels are then one level of one chunk
 // of m rows (P.L[0] = {m, 1, ...}).
 struct SbPlan {
   std::vector<SbPanel> panels;
@@ -59,8 +60,6 @@ struct SbBufs {
 int pqr_rows_per_thread(int m);
 // Panel A[r0:r0+m, p:p+32] -> Y (m x 32), YT = Y T, T (32 x 32); writes
 // [R; 0] and its transpose into A.  cnt: 2 words zeroed before the launch.
-bool pqr_spread();
-void pqr_set_spread(bool on);
 hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
                     double *YT, double *T, double *part, double *bc, unsigned *cnt,
                     unsigned *tmo);
@@ -91,7 +90,7 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.R[0], w * SB_B);
   take(b.R[1], w * SB_B);
   take(b.Gr, w * n);
-  take(b.U, std::max(w * n, size_t((n + 127) / 128) * SB_B * size_t(n)));  // X partials
+  take(b.U, w * n);  // X partials: one m x 32 slab per 256-row block of A22
   take(b.Xs, w * w);
   take(b.Zg, w * kmax);
   take(b.P, w * kmax);

@@ -550,114 +550,6 @@ __global__ __launch_bounds__(512) void ytz_kernel(const double *__restrict__ Y,
     }
 }
 
-// X = A22 YT from the lower triangle of A22 only (the single-level path keeps
-// A22's strict upper part stale: syr2k without mirror writes).  Lower tiles
-// (z, c) of XB x XB, c <= z; an off-diagonal tile is read once and used
-// twice: T1 = A_zc^T YT_z -> rows of block c, T2 = A_zc YT_c -> rows of block
-// z; a diagonal tile as the symmetric block (upper entries read mirrored).
-// Partials: slot s of block b holds T1 of tile (s, b) for s > b, the diagonal
-// for s = b and T2 of tile (b, s) for s < b, so every (slot, block) pair is
-// written once and X = sum over the nb = ceil(m / XB) slots (sum_partials).
-constexpr int XB = 128, XK = 32;
-__global__ __launch_bounds__(256) void symx_kernel(const double *__restrict__ A, int64_t lda, int m,
-                                                   const double *__restrict__ YT,
-                                                   double *__restrict__ part) {
-  __shared__ double As[XK][XB + 2];   // rows k0 .. k0 + 31 of block z, columns of block c
-  __shared__ double Yc[XB][SB_B + 2];  // YT rows of block c
-  __shared__ double Yz[XK][SB_B + 2];  // YT rows k0 .. k0 + 31 of block z
-  const int b = blockIdx.x;
-  int z = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
-  while ((z + 1) * (z + 2) / 2 <= b) ++z;
-  while (z * (z + 1) / 2 > b) --z;
-  const int c = b - z * (z + 1) / 2;
-  const bool diag = z == c;
-  const int z0 = z * XB, c0 = c * XB;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int lr = lane & 15, lk = lane >> 4;
-  for (int e = tid; e < XB * SB_B; e += 256) {
-    const int j = e >> 5, l = e & 31;
-    Yc[j][l] = c0 + j < m ? YT[int64_t(c0 + j) * SB_B + l] : 0.0;
-  }
-  doublex4 t1[2][2];  // T1 rows 32 wid .. + 31 (columns of block c), 32 columns
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) t1[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
-  const int ar = tid >> 3, ac = (tid & 7) * 16;  // loader: row ar, columns ac .. ac + 15
-  for (int k0 = 0; k0 < XB; k0 += XK) {
-    {
-      const int gi = z0 + k0 + ar;
-      double v[16];
-      if (!diag) {
-        const double *src = A + int64_t(min(gi, m - 1)) * lda + c0 + ac;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = (gi < m && c0 + ac + q < m) ? src[q] : 0.0;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int gj = c0 + ac + q;
-          const int r = max(gi, gj), cc = min(gi, gj);
-          v[q] = (gi < m && gj < m) ? A[int64_t(r) * lda + cc] : 0.0;
-        }
-      }
-      const int yi = tid >> 3, yl = (tid & 7) * 4;
-      double yv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) yv[q] = z0 + k0 + yi < m ? YT[int64_t(z0 + k0 + yi) * SB_B + yl + q] : 0.0;
-      __syncthreads();  // previous chunk's reads done
-#pragma unroll
-      for (int q = 0; q < 16; ++q) As[ar][ac + q] = v[q];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Yz[yi][yl + q] = yv[q];
-      __syncthreads();
-    }
-    // T2 rows k0 .. k0 + 31 of block z: wave (rb, cb) = (wid >> 1, wid & 1), K = XB
-    {
-      const int rb = wid >> 1, cb = wid & 1;
-      doublex4 t2 = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-      for (int kq = 0; kq < XB; kq += 4) {
-        const double af = As[rb * 16 + lr][kq + lk];
-        const double bf = Yc[kq + lk][cb * 16 + lr];
-        t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, t2, 0, 0, 0);
-      }
-      // slot c (z for the diagonal), rows of block z
-      double *dst = part + int64_t(c) * m * SB_B;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gi = z0 + k0 + rb * 16 + lk + 4 * q;  // acc[q]: row (lane >> 4) + 4 q
-        if (gi < m) dst[int64_t(gi) * SB_B + cb * 16 + lr] = t2[q];
-      }
-    }
-    if (!diag) {  // T1 += A_chunk^T Yz_chunk
-#pragma unroll
-      for (int kq = 0; kq < XK; kq += 4) {
-        double af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = As[kq + lk][wid * 32 + i * 16 + lr];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = Yz[kq + lk][j * 16 + lr];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            t1[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], t1[i][j], 0, 0, 0);
-      }
-    }
-  }
-  if (diag) return;
-  double *dst = part + int64_t(z) * m * SB_B;  // slot z, rows of block c
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gj = c0 + wid * 32 + i * 16 + lk + 4 * q;
-        if (gj < m) dst[int64_t(gj) * SB_B + j * 16 + lr] = t1[i][j][q];
-      }
-}
-
 // A22 -= Yd X^T + X Yd^T - Yd S Yd^T,  S = (M + M^T)/2  (== Yd W^T + W Yd^T
 // with W = X - Yd M / 2).  Yd block-diagonal over chunks of c rows:
 //   (Yd X^T)[r][c'] = sum_l Y[r][l] X[c'][I(r)*32 + l]
@@ -672,7 +564,7 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
                                                        const double *__restrict__ X,
                                                        int64_t ldx,
                                                        const double *__restrict__ M,
-                                                       int64_t ldm, int mirror = 1) {
+                                                       int64_t ldm) {
   // one LDS block: As, Bs, YS during the K loop, then the 64 x 65 tile for the
   // coalesced mirror stores
   constexpr int SMN = (2 * S2K + SB_B) * (S2T + S2P);
@@ -786,7 +678,7 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
           else if (gi != gj) A[int64_t(gj) * lda + gi] = v;
         }
       }
-  if (tm != tn && mirror) {
+  if (tm != tn) {
     __syncthreads();
     for (int idx = tid; idx < S2T * S2T; idx += 256) {
       const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
@@ -960,53 +852,6 @@ __global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y
   if (tid == 0) *ticket = 0u;
 }
 
-// Look-ahead strip of the single-level update: the first 32 columns of A22
-// (and their transpose) get  A22 -= Y X^T + X Y^T - Y S Y^T  (S = (M + M^T)/2)
-// ahead of the rest, so the next panel can be factored while syr2k_bs_kernel
-// updates A22[32:, 32:].  Delta[i][j] = Y_i . (X_j - S Y_j) + X_i . Y_j;
-// the 32 x 32 corner is computed for i >= j and mirrored (bitwise symmetric).
-__global__ __launch_bounds__(256) void strip_update_kernel(double *__restrict__ A, int64_t lda,
-                                                           int m, const double *__restrict__ Y,
-                                                           const double *__restrict__ X,
-                                                           const double *__restrict__ M) {
-  __shared__ double Ss[SB_B][SB_B + 1], Wj[SB_B][SB_B + 1], Yj[SB_B][SB_B + 1];
-  const int tid = threadIdx.x;
-  const int nj = min(SB_B, m);
-  for (int e = tid; e < SB_B * SB_B; e += 256) {
-    const int x = e >> 5, y = e & 31;
-    Ss[x][y] = 0.5 * (M[x * SB_B + y] + M[y * SB_B + x]);
-    Yj[x][y] = x < nj ? Y[x * SB_B + y] : 0.0;
-  }
-  __syncthreads();
-  for (int e = tid; e < SB_B * SB_B; e += 256) {
-    const int j = e >> 5, l = e & 31;  // W_j = X_j - S Y_j
-    double z = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < SB_B; ++k) z = fma(Ss[l][k], Yj[j][k], z);
-    Wj[j][l] = (j < nj ? X[j * SB_B + l] : 0.0) - z;
-  }
-  __syncthreads();
-  const int i = blockIdx.x * 64 + (tid >> 2), j0 = (tid & 3) * 8;
-  if (i >= m) return;
-  double yi[SB_B], xi[SB_B];
-#pragma unroll
-  for (int l = 0; l < SB_B; ++l) {
-    yi[l] = Y[int64_t(i) * SB_B + l];
-    xi[l] = X[int64_t(i) * SB_B + l];
-  }
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) {
-    const int j = j0 + jj;
-    if (j >= nj || (i < SB_B && j > i)) continue;
-    double d = 0.0;
-#pragma unroll
-    for (int l = 0; l < SB_B; ++l) d = fma(yi[l], Wj[j][l], fma(xi[l], Yj[j][l], d));
-    const double v = A[int64_t(i) * lda + j] - d;
-    A[int64_t(i) * lda + j] = v;
-    if (i != j) A[int64_t(j) * lda + i] = v;
-  }
-}
-
 // A[r0+i][p+l] = [R; 0] and the transpose (i < m, l < 32).
 __global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, int r0, int m,
                                    const double *__restrict__ R) {
@@ -1054,221 +899,38 @@ static hipError_t side_stream(SideStream *&out) {
   return hipSuccess;
 }
 
-// CU-partitioned streams for the overlapped band reduction (created once per
-// device and size class): `sp` may use only r CUs on every XCD (mask bits k
-// map to XCD k % 8, so bits [0, 8 r) are r CUs per XCD), `su` every other CU.
-// The panel QR's workers (one CU each: their LDS fills it) are spread one
-// block per XCD in turn, so r >= workers / 8 keeps them all resident while
-// the trailing update owns the rest of the chip.
-struct CuStreams {
-  hipStream_t su = nullptr, sp = nullptr;
-  int r = 0;
-  hipEvent_t evq[2] = {nullptr, nullptr}, evs[2] = {nullptr, nullptr}, evj = nullptr, evd = nullptr;
-};
-static hipError_t cu_streams(int r, CuStreams *&out) {
-  static CuStreams cs[64][4];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  hipDeviceProp_t pr;
-  if ((e = hipGetDeviceProperties(&pr, dev)) != hipSuccess) return e;
-  const int ncu = pr.multiProcessorCount;
-  int slot = 0;
-  while (slot < 3 && (1 << slot) < r) ++slot;
-  r = 1 << slot;
-  if (ncu % 8 != 0 || 8 * r * 4 > ncu) return hipErrorNotSupported;
-  CuStreams &x = cs[dev & 63][slot];
-  if (!x.su) {
-    const int nw = (ncu + 31) / 32;
-    std::vector<uint32_t> mu(nw, 0u), mp(nw, 0u);
-    for (int k = 0; k < ncu; ++k) (k < 8 * r ? mp : mu)[k / 32] |= 1u << (k % 32);
-    if ((e = hipExtStreamCreateWithCUMask(&x.su, nw, mu.data())) != hipSuccess) return e;
-    if ((e = hipExtStreamCreateWithCUMask(&x.sp, nw, mp.data())) != hipSuccess) return e;
-    for (int i = 0; i < 2; ++i) {
-      if ((e = hipEventCreateWithFlags(&x.evq[i], hipEventDisableTiming)) != hipSuccess) return e;
-      if ((e = hipEventCreateWithFlags(&x.evs[i], hipEventDisableTiming)) != hipSuccess) return e;
-    }
-    if ((e = hipEventCreateWithFlags(&x.evj, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&x.evd, hipEventDisableTiming)) != hipSuccess) return e;
-    x.r = r;
-  }
-  out = &x;
-  return hipSuccess;
-}
-
-// Overlapped form: panel pi + 1's QR (on the reserved CUs) runs while panel
-// pi's trailing update A22[32:, 32:] runs on the other CUs.  Per panel, on su:
-// wait QR(pi) -> X, M -> strip update (the next panel's 32 rows / columns) ->
-// event -> syr2k of the rest; on sp: wait strip(pi) -> QR(pi + 1) -> event.
-// Buffer use as in the look-ahead form below (the QR's partials region is
-// idle between ytx_m and the strip event; YT is read only by X).
-static hipError_t sy2sb_overlap(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
-                                const SbBufs &b, CuStreams &cs) {
-  const int np = int(pl.panels.size());
-  TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
-  TG_CHK(hipEventRecord(cs.evj, st));
-  TG_CHK(hipStreamWaitEvent(cs.su, cs.evj, 0));
-  TG_CHK(hipStreamWaitEvent(cs.sp, cs.evj, 0));
-  const bool spread0 = pqr_spread();
-  pqr_set_spread(true);
-  auto pqr = [&](hipStream_t s, int pi) {
-    const SbPanel &P = pl.panels[pi];
-    return panel_qr(s, A, lda, P.p, P.r0, P.m, b.Y + P.L[0].yoff, b.YT, b.T + P.L[0].toff,
-                    b.pq_part, b.pq_bc, b.pq_ctl + 4 + 4 * pi, b.pq_ctl);
-  };
-  hipError_t err = hipSuccess;
-  auto run = [&]() -> hipError_t {
-    TG_CHK(pqr(cs.sp, 0));
-    TG_CHK(hipEventRecord(cs.evq[0], cs.sp));
-    for (int pi = 0; pi < np; ++pi) {
-      const SbPanel &P = pl.panels[pi];
-      const int m = P.m, r0 = P.r0, ph = pi & 1;
-      double *A22 = A + int64_t(r0) * lda + r0;
-      double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
-      TG_CHK(hipStreamWaitEvent(cs.su, cs.evq[ph], 0));  // panel QR pi done
-      const int nz = std::max(1, m / SB_C);
-      ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
-      TG_CHK(dgemm_chunked(cs.su, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
-      TG_CHK(sum_partials(cs.su, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
-      hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, cs.su, Yp, b.X, m, Tp,
-                         b.M, b.pq_part, b.pq_ctl + 1);
-      TG_CHK(hipGetLastError());
-      if (pi + 1 < np) {
-        hipLaunchKernelGGL(strip_update_kernel, dim3(cdiv(m, 64)), dim3(256), 0, cs.su, A22,
-                           int64_t(lda), m, Yp, b.X, b.M);
-        TG_CHK(hipGetLastError());
-        TG_CHK(hipEventRecord(cs.evs[ph], cs.su));
-        TG_CHK(hipStreamWaitEvent(cs.sp, cs.evs[ph], 0));
-        TG_CHK(pqr(cs.sp, pi + 1));
-        TG_CHK(hipEventRecord(cs.evq[ph ^ 1], cs.sp));
-        const int mr = m - SB_B;
-        if (mr > 0) {
-          const int nt = cdiv(mr, S2T);
-          auto tok = prof_begin(cs.su, PROF_SBUPD, 12.0 * double(mr) * mr, 96.0 * double(mr) * mr);
-          hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, cs.su,
-                             A22 + int64_t(SB_B) * lda + SB_B, int64_t(lda), mr, mr, 1,
-                             Yp + SB_B * SB_B, b.X + SB_B * SB_B, int64_t(SB_B), b.M, int64_t(SB_B));
-          prof_end(cs.su, tok);
-          TG_CHK(hipGetLastError());
-        }
-      } else {
-        const int nt = cdiv(m, S2T);
-        auto tok = prof_begin(cs.su, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
-        hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, cs.su, A22,
-                           int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
-        prof_end(cs.su, tok);
-        TG_CHK(hipGetLastError());
-      }
-    }
-    return hipSuccess;
-  };
-  err = run();
-  pqr_set_spread(spread0);
-  TG_CHK(err);
-  TG_CHK(hipEventRecord(cs.evd, cs.su));
-  TG_CHK(hipStreamWaitEvent(st, cs.evd, 0));
-  TG_CHK(hipEventRecord(cs.evj, cs.sp));
-  TG_CHK(hipStreamWaitEvent(st, cs.evj, 0));
-  return hipSuccess;
-}
-
 // One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
-// Look-ahead (TG_SB_LOOKAHEAD=1; off by default: measured +5 ms at n = 4096,
-// the panel QR's workgroups need a whole CU's LDS and wait for the trailing
-// update to drain, so nothing overlaps and the events cost): after M, the strip kernel
-// updates the next panel's 32 columns (and rows), the side stream factors the
-// next panel while syr2k_bs_kernel updates A22[32:, 32:] on the main stream;
-// the next X waits for both.  Buffers: YT is only read by X (done before the
-// next panel QR writes it); X, M, U and the partials are main-stream only
-// while the side stream runs (the panel QR's partials region is idle then).
+// (Measured and removed in round 3's clean-up, DESIGN.md §5: a look-ahead
+// with the next panel's QR on a side stream, +5 ms -- the QR's workgroups need
+// a whole CU's LDS and wait for the trailing update to drain; the same on
+// CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
+// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
-  static const int cumask = [] {
-    const char *v = getenv("TG_SB_CUMASK");
-    return v ? atoi(v) : 0;
-  }();
-  if (cumask && !pl.panels.empty()) {
-    const int nwmax = cdiv(pl.panels[0].m, 256);
-    CuStreams *cs = nullptr;
-    if (cu_streams(cdiv(nwmax, 8), cs) == hipSuccess && 8 * cs->r >= nwmax) {
-      if (cumask == 2) {  // diagnostic: both on the update stream (mask cost alone)
-        CuStreams one = *cs;
-        one.sp = one.su;
-        return sy2sb_overlap(st, A, lda, n, pl, b, one);
-      }
-      return sy2sb_overlap(st, A, lda, n, pl, b, *cs);
-    }
-  }
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
-  const char *la = getenv("TG_SB_LOOKAHEAD");
-  const bool look = la && la[0] == '1';
-  // TG_SB_LOWER=1: A22 kept as its lower triangle (X from lower tiles by
-  // symx_kernel, syr2k without mirror writes).  Measured slower: syr2k
-  // 38 -> 35 us but X 27 -> 35 us and twice the partials (per panel at m = 4096).
-  static const bool lower_env = getenv("TG_SB_LOWER") != nullptr;
-  const bool lower = !look && lower_env;
-  SideStream *ss = nullptr;
-  if (look) TG_CHK(side_stream(ss));
   const int np = int(pl.panels.size());
-  auto pqr = [&](hipStream_t s, int pi) {
-    const SbPanel &P = pl.panels[pi];
-    return panel_qr(s, A, lda, P.p, P.r0, P.m, b.Y + P.L[0].yoff, b.YT, b.T + P.L[0].toff,
-                    b.pq_part, b.pq_bc, b.pq_ctl + 4 + 4 * pi, b.pq_ctl);
-  };
-  if (np > 0) TG_CHK(pqr(st, 0));
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
-    const int m = P.m, r0 = P.r0, ph = pi & 1;
+    const int m = P.m, r0 = P.r0;
     double *A22 = A + int64_t(r0) * lda + r0;
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
-    if (look && pi > 0) TG_CHK(hipStreamWaitEvent(st, ss->ev1[ph], 0));  // panel QR pi done
-    if (lower) {
-      // X = A22 YT from A22's lower triangle (tiles read once, used twice)
-      const int nb = cdiv(m, XB);
-      hipLaunchKernelGGL(symx_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, A22,
-                         int64_t(lda), m, b.YT, b.U);
-      TG_CHK(hipGetLastError());
-      TG_CHK(sum_partials(st, b.U, nb, m, SB_B, 1.0, 0.0, b.X, SB_B));
-    } else {
-      // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
-      const int nz = std::max(1, m / SB_C);
-      ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
-      TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
-      TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
-    }
+    TG_CHK(panel_qr(st, A, lda, P.p, P.r0, P.m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
+                    b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
+    // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
+    const int nz = std::max(1, m / SB_C);
+    ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
+    TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
+    TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
     // M = T^T Y^T X
     hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
                        b.pq_part, b.pq_ctl + 1);
     TG_CHK(hipGetLastError());
-    const bool next = pi + 1 < np;
-    if (look && next) {
-      hipLaunchKernelGGL(strip_update_kernel, dim3(cdiv(m, 64)), dim3(256), 0, st, A22,
-                         int64_t(lda), m, Yp, b.X, b.M);
-      TG_CHK(hipGetLastError());
-      TG_CHK(hipEventRecord(ss->ev0[ph], st));
-      TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[ph], 0));
-      TG_CHK(pqr(ss->s, pi + 1));
-      TG_CHK(hipEventRecord(ss->ev1[ph ^ 1], ss->s));
-      const int mr = m - SB_B;
-      if (mr > 0) {
-        const int nt = cdiv(mr, S2T);
-        auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(mr) * mr, 96.0 * double(mr) * mr);
-        hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st,
-                           A22 + int64_t(SB_B) * lda + SB_B, int64_t(lda), mr, mr, 1,
-                           Yp + SB_B * SB_B, b.X + SB_B * SB_B, int64_t(SB_B), b.M, int64_t(SB_B));
-        prof_end(st, tok);
-        TG_CHK(hipGetLastError());
-      }
-    } else {
-      const int nt = cdiv(m, S2T);
-      auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
-      hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                         int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B),
-                         lower ? 0 : 1);
-      prof_end(st, tok);
-      TG_CHK(hipGetLastError());
-      if (next) TG_CHK(pqr(st, pi + 1));
-    }
+    const int nt = cdiv(m, S2T);
+    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
+    hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                       int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+    prof_end(st, tok);
+    TG_CHK(hipGetLastError());
   }
   return hipSuccess;
 }

@@ -1353,7 +1353,7 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   const int nref = ts ? 0 : n - 1;
   if (ts) {
     // few vectors (the complement path's request): one persistent launch
-    static const bool multi = getenv("TG_BT_MULTI") != nullptr;
+    const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
     if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl) <= sizeof(double) * size_t(n) * tg::SB_B) {
       TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.tau2, sb.T2));
       bool tmo = false;

@@ -65,6 +65,11 @@ struct PivWs {
 constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
 static_assert(PGMAX * PPS % 256 == 0, "slot copy assumes whole rounds of 256 threads");
 
+// The candidate-set pivot order with compacted Schur complements (two n x n
+// buffers) for n <= 32768; above (or TG_PIVOT_OLD=1, read per call) the
+// cross-workgroup per-pivot path, which needs only one.
+inline bool compact_pivot(int n) { return n <= 32768 && getenv("TG_PIVOT_OLD") == nullptr; }
+
 template <class A>
 void piv_layout(A &ar, int n, int k, PivWs *p) {
   PivWs d{};
@@ -90,7 +95,7 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.prow, PB);
   take(q.pinv, PB);
   take(q.Lpp, PB * PB);
-  take(q.Hk2, size_t(n) * n);
+  take(q.Hk2, compact_pivot(n) ? size_t(n) * n : size_t(1));
   take(q.oidx, n);
 }
 
@@ -1197,190 +1202,12 @@ __global__ void gather_scale_kernel(const double *__restrict__ Vh, int ldv, cons
 // rows become one MFMA GEMM U12 = W G12.  X = U11^-1 by back substitution,
 // one column per thread group.
 constexpr int NU = 64;
-// Cholesky: thread (column c = tid & 63, rows r0 = tid >> 6 mod 4) updates
-// a[r][c] -= U[j][r] U[j][c] for j < r <= c; the scaled row U[j][:] goes to a
-// separate matrix (row j of `a` is only read in step j), so one barrier per
-// column suffices.  Inverse X = U11^-1: four lanes of one wave per column,
-// partial sums combined by DPP quad permutes, x[i][c] handed on through LDS
-// with wave-level ordering only (no workgroup barrier).
-template <int CTRL>
-__device__ inline double dpp_d(double x) {
-  return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
-                          __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
-}
-__global__ __launch_bounds__(256) void potrf_inv_kernel(double *__restrict__ U, int ldu, int p,
-                                                        int pb, double *__restrict__ Wout,
-                                                        int *__restrict__ info) {
-  __shared__ double a[NU][NU + 1];
-  __shared__ double u[NU][NU + 1];
-  const int tid = threadIdx.x, c = tid & 63, r0 = tid >> 6;
-  {
-    const double *col = U + size_t(p) * ldu + p + min(c, pb - 1);
-#pragma unroll
-    for (int q = 0; q < NU / 4; ++q) {
-      const int r = r0 + 4 * q;
-      const double v = col[size_t(min(r, pb - 1)) * ldu];  // clamped: no guarded loads
-      a[r][c] = (r < pb && c < pb) ? v : (r == c ? 1.0 : 0.0);
-    }
-  }
-  __syncthreads();
-  int bad = 0;
-  for (int j = 0; j < NU; ++j) {
-    const double djj = a[j][j];
-    const double piv = sqrt(djj);
-    const double inv = 1.0 / piv;
-    bad |= !(djj > 0.0) && j < pb;
-    const double ujc = a[j][c] * inv;
-    if (r0 == 0) u[j][c] = c > j ? ujc : (c == j ? piv : 0.0);
-    for (int r = j + 1 + r0; r <= c; r += 4) a[r][c] -= (a[j][r] * inv) * ujc;
-    __syncthreads();
-  }
-  if (tid == 0 && bad) atomicAdd(info, 1);
-  // X = U^-1 (upper) into `a` (dead now): column cc by 4 lanes, part = lane & 3
-  {
-    const int cc = tid >> 2, part = tid & 3;
-    for (int i = NU - 1; i >= 0; --i) {
-      double s = 0.0;
-      if (i < cc)
-        for (int l = i + 1 + part; l <= cc; l += 4) s += u[i][l] * a[l][cc];
-      s += dpp_d<0xB1>(s);  // lane ^ 1
-      s += dpp_d<0x4E>(s);  // lane ^ 2
-      if (part == 0) a[i][cc] = i > cc ? 0.0 : ((i == cc ? 1.0 : 0.0) - s) / u[i][i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-  __syncthreads();
-  for (int idx = tid; idx < pb * NU; idx += blockDim.x) {
-    const int r = idx / NU, cc = idx % NU;
-    if (cc < pb) U[size_t(p + r) * ldu + p + cc] = cc >= r ? u[r][cc] : 0.0;
-  }
-  // W = X^T (lower), NU x NU, row stride NU
-  for (int idx = tid; idx < NU * NU; idx += blockDim.x) {
-    const int r = idx / NU, cc = idx % NU;
-    Wout[idx] = (r < pb && cc < pb) ? a[cc][r] : 0.0;
-  }
-}
-
-__global__ __launch_bounds__(256) void potf2_kernel(double *__restrict__ U, int ldu, int p, int pb,
-                                                    int *__restrict__ info) {
-  __shared__ double a[CB][CB + 1];
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < CB * CB; idx += blockDim.x) {
-    const int r = idx / CB, c = idx % CB;
-    a[r][c] = (r < pb && c < pb) ? U[size_t(p + r) * ldu + p + c] : (r == c ? 1.0 : 0.0);
-  }
-  __syncthreads();
-  for (int j = 0; j < CB; ++j) {
-    const double djj = a[j][j];
-    const double piv = sqrt(djj);
-    if (tid == 0 && !(djj > 0.0) && j < pb) atomicAdd(info, 1);
-    __syncthreads();
-    for (int c = j + 1 + tid; c < CB; c += blockDim.x) a[j][c] /= piv;
-    __syncthreads();
-    if (tid == 0) a[j][j] = piv;
-    // trailing: a[r][c] -= a[j][r] * a[j][c], j < r <= c
-    const int m = CB - j - 1;
-    for (int idx = tid; idx < m * m; idx += blockDim.x) {
-      const int r = j + 1 + idx / m, c = j + 1 + idx % m;
-      if (c >= r) a[r][c] -= a[j][r] * a[j][c];
-    }
-    __syncthreads();
-  }
-  for (int idx = tid; idx < pb * pb; idx += blockDim.x) {
-    const int r = idx / pb, c = idx % pb;
-    U[size_t(p + r) * ldu + p + c] = c >= r ? a[r][c] : 0.0;
-  }
-}
-
-// Same contract as potrf_inv_kernel, one wave and no barriers: lane c keeps
-// column c of the block (a[r] = A[r][c]) and of X = U^-1 (x[r]) in registers.
-// Step j of the Cholesky needs row j of U across lanes (U[j][r] lives in lane
-// r): every lane writes its a[j] to an LDS row, then reads the row back as
-// broadcast loads (one address per instruction, no bank conflicts).  Entries
-// below the diagonal are updated too (branch-free) and zeroed at their step.
-// The inverse is the same pattern by rows of U: X[i][c] = (d_ic -
-// sum_{l>i} U[i][l] X[l][c]) / U[i][i].
-__global__ __launch_bounds__(64) void potrf_inv_w_kernel(double *__restrict__ U, int ldu, int p,
-                                                         int pb, double *__restrict__ Wout,
-                                                         int *__restrict__ info) {
-  __shared__ double2 row2[NU / 2];
-  __shared__ double wt[NU][NU + 1];
-  double *row = reinterpret_cast<double *>(row2);
-  const int c = threadIdx.x;
-  double a[NU];
-  double *base = U + size_t(p) * ldu + p;
-  {
-    const int cc = min(c, pb - 1);
-#pragma unroll
-    for (int r = 0; r < NU; ++r) {
-      const double v = base[size_t(min(r, pb - 1)) * ldu + cc];  // clamped: no guarded loads
-      a[r] = (r < pb && c < pb) ? v : (r == c ? 1.0 : 0.0);
-    }
-  }
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < NU; ++j) {
-    row[c] = a[j];
-    __builtin_amdgcn_wave_barrier();
-    double rv[NU];
-#pragma unroll
-    for (int q = j / 2; q < NU / 2; ++q) {  // 16-B broadcast reads of row j of the update
-      const double2 t = row2[q];
-      rv[2 * q] = t.x;
-      rv[2 * q + 1] = t.y;
-    }
-    const double d = rv[j];
-    const double piv = sqrt(d);
-    const double inv = 1.0 / piv;
-    bad |= !(d > 0.0) && j < pb;
-    const double ujc = a[j] * inv;
-    a[j] = c > j ? ujc : (c == j ? piv : 0.0);
-    const double f = ujc * inv;
-#pragma unroll
-    for (int r = j + 1; r < NU; ++r) a[r] -= rv[r] * f;
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (c == 0 && bad) atomicAdd(info, 1);
-  // U block (upper) back in place
-#pragma unroll
-  for (int r = 0; r < NU; ++r)
-    if (r < pb && c < pb) base[size_t(r) * ldu + c] = c >= r ? a[r] : 0.0;
-  // X = U^-1 by rows of U: X[i][c] = (d_ic - sum_{l>i} U[i][l] X[l][c]) / U[i][i];
-  // x[] overwrites a[] from the bottom (a[i] is dead once row i is in LDS)
-#pragma unroll
-  for (int i = NU - 1; i >= 0; --i) {
-    row[c] = a[i];  // row i of U
-    __builtin_amdgcn_wave_barrier();
-    double rv[NU];
-#pragma unroll
-    for (int q = i / 2; q < NU / 2; ++q) {
-      const double2 t = row2[q];
-      rv[2 * q] = t.x;
-      rv[2 * q + 1] = t.y;
-    }
-    double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
-#pragma unroll
-    for (int l = i + 1; l < NU; l += 2) {
-      s0 -= rv[l] * a[l];
-      if (l + 1 < NU) s1 -= rv[l + 1] * a[l + 1];
-    }
-    a[i] = (s0 + s1) / rv[i];
-    __builtin_amdgcn_wave_barrier();
-  }
-  // W = X^T (lower) through LDS for coalesced rows
-#pragma unroll
-  for (int r = 0; r < NU; ++r) wt[c][r] = (r < pb && c < pb) ? a[r] : 0.0;  // X[r][c]
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int r = 0; r < NU; ++r) Wout[r * NU + c] = wt[r][c];
-}
-
-// Same contract as potrf_inv_w_kernel on four waves: lane c = column c, wave
+// Diagonal NU x NU block of the U Cholesky: U11 = chol_upper(G11) written to
+// U and W = U11^-T (lower) to Wout, so the panel's off-diagonal rows become
+// one MFMA GEMM U12 = W G12.  Four waves: lane c = column c, wave
 // g holds rows 16g .. 16g + 15 (a[q] = A[16g + q][c]), so each wave issues a
-// quarter of the update (the one-wave kernel is bound by its ≈17k issued
-// instructions).  Step j: the owner wave publishes row j (columns < j as 0,
+// quarter of the update (a one-wave form, measured and removed, issued ≈17k
+// instructions per block: 50 us against 31).  Step j: the owner wave publishes row j (columns < j as 0,
 // so the update needs no mask: rows above j take multiplier 0, finished
 // columns factor 0), one barrier, every wave updates its rows.  The inverse
 // runs right-looking over U's columns: step l (descending) finalises row l of
@@ -1523,104 +1350,19 @@ __global__ void zero_lower_kernel(double *__restrict__ U, int ldu, int k) {
 // Right-looking blocked upper Cholesky of the first k rows of the symmetric
 // n x n matrix in U (upper triangle read): U[:k, :] <- R with R^T R = G
 // restricted to those rows (k = n: the full factor).  NU-row panels: the
-// diagonal block and its inverse in LDS (potrf_inv_kernel), the panel rows as
+// diagonal block and its inverse (potrf_inv_4w_kernel), the panel rows as
 // one MFMA GEMM U12 = U11^-T G12, the trailing update as a second GEMM.
 // info[0] counts non-positive pivots.
-// Diagonal-block factor + inverse: the four-wave kernel (TG_POTRF_WAVES=1 / 8:
-// the one-wave kernel / eight waves, for A/B).
+// Diagonal-block factor + inverse: the four-wave kernel.
 static void launch_potrf_inv(hipStream_t st, double *U, int ldu, int p, int pb, double *Wb,
                              int *info) {
-  static const int waves = [] {
-    const char *v = getenv("TG_POTRF_WAVES");
-    return v ? atoi(v) : 4;
-  }();
-  if (waves == 1)
-    hipLaunchKernelGGL(potrf_inv_w_kernel, dim3(1), dim3(64), 0, st, U, ldu, p, pb, Wb, info);
-  else if (waves == 8)
-    hipLaunchKernelGGL(potrf_inv_4w_kernel<8>, dim3(1), dim3(512), 0, st, U, ldu, p, pb, Wb, info);
-  else
-    hipLaunchKernelGGL(potrf_inv_4w_kernel<4>, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
-}
-
-// Low-priority side stream + events for the look-ahead (once per device).
-struct LaStream {
-  hipStream_t s = nullptr;
-  hipEvent_t ev_panel = nullptr, ev_rest = nullptr;
-};
-static hipError_t la_stream(LaStream *&out) {
-  static LaStream ls[64];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  LaStream &x = ls[dev & 63];
-  if (!x.s) {
-    int least = 0, greatest = 0;
-    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
-    if ((e = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least)) != hipSuccess)
-      return e;
-    if ((e = hipEventCreateWithFlags(&x.ev_panel, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&x.ev_rest, hipEventDisableTiming)) != hipSuccess) return e;
-  }
-  out = &x;
-  return hipSuccess;
-}
-
-#define LA_CHK(x)                   \
-  do {                              \
-    hipError_t e_ = (x);            \
-    if (e_ != hipSuccess) return e_; \
-  } while (0)
-
-// Look-ahead form (depth 1).  Panel i = rows [p, c0), next panel rows [c0, c1).
-// Main stream: next-panel update TA(i) (rows [c0, c1), K = panel i) ->
-// diagonal factor + panel solve of panel i+1.  Side stream, concurrently: the
-// rest of panel i's trailing update TB(i) (rows [c1, k), columns >= c1; the
-// columns [c0, c1) of those rows are below the diagonal and never read).
-// TA(i+1) writes rows that TB(i) wrote, so the main stream waits for TB(i)
-// there; the critical path per panel is max(TA + factor + solve, TB).
-static hipError_t chol_upper_rows_la(hipStream_t st, LaStream &ls, double *U, int ldu, int k,
-                                     int n, double *Wb, int *info) {
-  auto factor_solve = [&](hipStream_t s, int p) -> hipError_t {
-    const int pb = std::min(NU, k - p), c0 = p + pb;
-    launch_potrf_inv(s, U, ldu, p, pb, Wb, info);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || c0 >= n) return e;
-    double *P = U + size_t(p) * ldu + c0;
-    return tg::dgemm(s, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
-  };
-  LA_CHK(factor_solve(st, 0));
-  bool pending = false;  // a TB on the side stream the main stream has not waited for
-  for (int p = 0; p < k; p += NU) {
-    const int pb = std::min(NU, k - p), c0 = p + pb;
-    if (c0 >= k) break;
-    const int c1 = std::min(c0 + NU, k);
-    const double *P = U + size_t(p) * ldu + c0;  // panel i rows, columns >= c0
-    if (pending) LA_CHK(hipStreamWaitEvent(st, ls.ev_rest, 0));  // TB(i-1) done
-    pending = false;
-    if (c1 < k) {
-      LA_CHK(hipEventRecord(ls.ev_panel, st));  // panel i solved
-      LA_CHK(hipStreamWaitEvent(ls.s, ls.ev_panel, 0));
-      LA_CHK(tg::dgemm(ls.s, true, false, k - c1, n - c1, pb, -1.0, P + (c1 - c0), ldu,
-                       P + (c1 - c0), ldu, 1.0, U + size_t(c1) * ldu + c1, ldu));
-      LA_CHK(hipEventRecord(ls.ev_rest, ls.s));
-      pending = true;
-    }
-    LA_CHK(tg::dgemm(st, true, false, c1 - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
-                     U + size_t(c0) * ldu + c0, ldu));
-    LA_CHK(factor_solve(st, c0));
-  }
-  if (pending) LA_CHK(hipStreamWaitEvent(st, ls.ev_rest, 0));
-  return hipSuccess;
+  hipLaunchKernelGGL(potrf_inv_4w_kernel<4>, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
 }
 
 hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, double *Wb,
                            int *info) {
-  // measured slower than the single-stream order on MI355X (the cross-stream
-  // event waits cost more than the overlap gains): opt-in only
-  static const bool la = getenv("TG_CHOL_LOOKAHEAD") != nullptr;
-  LaStream *ls = nullptr;
-  if (la && k > 2 * NU && la_stream(ls) == hipSuccess)
-    return chol_upper_rows_la(st, *ls, U, ldu, k, n, Wb, info);
+  // (a depth-1 look-ahead on a side stream measured +0.4 ms: the event
+  // waits cost more than the overlap; removed)
   for (int p = 0; p < k; p += NU) {
     const int pb = std::min(NU, k - p);
     launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
@@ -2017,8 +1759,7 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
 }
 
 static int pivot_core(hipStream_t st, PivWs &w, int n, int k, int64_t *perm, double *Rx, int ldr) {
-  static const bool old_pivot = getenv("TG_PIVOT_OLD") != nullptr;
-  if (!old_pivot && n <= 32768) {
+  if (compact_pivot(n)) {
     const int e = pivot_core_sel(st, w, n, k);
     if (e != 0) return e;
     hipLaunchKernelGGL(rx_gather_kernel, dim3(tg::cdiv(n, 256) < 16 ? tg::cdiv(n, 256) : 16, k),
@@ -2310,7 +2051,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
   urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info, &Rq, &rw);
   TG_WS(ar);
   TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
-  static const bool two_chol = getenv("TG_URX_TWOCHOL") != nullptr;
+  const bool two_chol = getenv("TG_URX_TWOCHOL") != nullptr;  // read per call (tests set it)
   if (!two_chol) {
     const int m = n - k;
     const dim3 gk(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k);

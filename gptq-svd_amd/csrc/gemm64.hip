@@ -321,7 +321,7 @@ rocblas_handle blas_handle(hipStream_t st) {
 }
 
 bool use_blas(int M, int N, int K, const double *A, const double *B, const double *C) {
-  static const bool off = getenv("TG_NO_ROCBLAS") != nullptr;
+  const bool off = getenv("TG_NO_ROCBLAS") != nullptr;  // read per call (tests set it)
   if (off || K < 32 || double(M) * N * K < double(1 << 28)) return false;
   // rocBLAS does not allow C to alias an operand (chol_upper_rows' in-place
   // panel solve does; it stays on dgemm_kernel)

@@ -904,12 +904,9 @@ __global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
 
 namespace tg {
 
-// Workers spread over the XCDs (one block each) instead of packed on one XCD:
-// for a CU-masked side stream that reserves a few CUs on every XCD.
-static bool g_pqr_spread = getenv("TG_PQR_SPREAD") != nullptr;
-bool pqr_spread() { return g_pqr_spread; }
-void pqr_set_spread(bool on) { g_pqr_spread = on; }
-
+// One row per thread, 256 rows per workgroup, every workgroup resident (one
+// per CU: the row block and the factor tiles fill its LDS): panels of up to
+// 256 x 256 rows (n <= 65,568), the largest down_proj (n = 28,672) needs 112.
 int pqr_rows_per_thread(int m) { return m <= PQR_NWMAX * PT ? 1 : 0; }
 
 hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
@@ -954,7 +951,10 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
   }
   // 2 Gram passes + the row solve and the final [Y | YT] product: ~10 m 32^2 flops
   auto tok = prof_begin(st, PROF_TSQR, 8.0 * m * SB_B * 3, 10.0 * m * SB_B * SB_B);
-  g.wstride = pqr_spread() ? 1 : 8;
+  // up to 32 workers share one XCD (launched x8, blockIdx % 8 == 0: one XCD
+  // under round-robin dispatch -- speed only: the hand-offs are sc1 stores and
+  // loads, correct across XCDs); more are spread over the chip
+  g.wstride = g.nw <= 32 ? 8 : 1;
   hipLaunchKernelGGL(pqr_kernel, dim3(g.wstride * g.nw), dim3(PT), 0, st, g);
   prof_end(st, tok);
   if (g.stats) {

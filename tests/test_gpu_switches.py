@@ -1,0 +1,62 @@
+"""Every path-selecting developer switch left in the library, on the GPU:
+each alternative path must reproduce the default path on the same Hessian
+(perm identical, U / R_x to 1e-10, the quantised weights bit-identical).
+n = 2048 (rank 1536): large enough that the GEMMs take the rocBLAS branch
+(TG_NO_ROCBLAS covers the in-house FP64 GEMM in its place) and both spectral
+paths exist.  The switches are read per call."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def problem():
+    import gptq_svd_amd.gptq_utils as g
+    torch.manual_seed(5)
+    n = 2048
+    X = torch.randn(3 * n // 4, n).half().to(DEV)
+    acc = g.HessianAccumulator(n, DEV)
+    acc.add_batch(X)
+    H = acc.get_hessian()
+    W = torch.randn(256, n, device=DEV)
+    return g, H, W
+
+
+def solve(g, H, W):
+    U, R_x, perm, S, k = g.truncated_spectral_factor(H, 1e-4, "energy")
+    q = g.Quantizer(4, 128, False)
+    Wq, _ = g.gptq_fwrd(W, U, q, perm, block_size=1024)
+    return dict(U=U.cpu().numpy(), R_x=R_x.cpu().numpy(), perm=perm.cpu().numpy(),
+                Wq=Wq.cpu().numpy(), path=g.truncated_spectral_factor.last_path[0])
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("path", ["kept", "complement"])
+@pytest.mark.parametrize("switches", [
+    {"TG_PIVOT_OLD": "1"},
+    {"TG_PIVOT_OLD": "1", "TG_PIVOT_STEPWISE": "1"},
+    {"TG_INVIT_REG": "1"},
+    {"TG_BT_MULTI": "1"},
+    {"TG_URX_TWOCHOL": "1"},
+    {"TG_NO_ROCBLAS": "1"},
+], ids=lambda d: "+".join(d))
+def test_switch_matches_default(problem, path, switches, monkeypatch):
+    g, H, W = problem
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
+    ref = solve(g, H, W)
+    assert ref["path"] == path
+    for k, v in switches.items():
+        monkeypatch.setenv(k, v)
+    got = solve(g, H, W)
+    assert got["path"] == path
+    assert np.array_equal(got["perm"], ref["perm"])
+    assert rel(got["U"], ref["U"]) <= 1e-10
+    assert rel(got["R_x"], ref["R_x"]) <= 1e-10
+    mism = float(np.mean(got["Wq"] != ref["Wq"]))
+    assert mism <= 1e-5, mism  # U agrees to ~1e-15: at most a rounding-tie flip
