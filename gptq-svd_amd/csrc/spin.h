@@ -42,7 +42,7 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
       __builtin_amdgcn_s_sleep(1);
       v = __builtin_amdgcn_readfirstlane(ctl_load(word));
       if (v >= target) break;
-      if ((it & 31u) == 0u) {
+      if ((it & 31u) == 31u) {  // short waits never pay for these reads
         if (__builtin_amdgcn_readfirstlane(ctl_load(stall)) != 0u) {
           ok = false;
           break;
@@ -59,14 +59,16 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
   return ok;
 }
 
-// One arrival on a counter by a whole wave without a lane-0 branch: lane 0
-// adds 1, the other lanes add 0 (a lane-0 `if` next to a loop that holds
-// barriers can let the CFG structurizer run lane 0 through a loop nest of its
-// own, bulge.hip).  Returns the value before lane 0's add.
-__device__ __forceinline__ unsigned wave_arrive(unsigned *cnt) {
-  const unsigned one = (__lane_id() == 0) ? 1u : 0u;
-  return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_fetch_add((spin_u32 *)cnt, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+// One arrival on a counter, called by a whole wave: lane 0 adds 1 (a plain
+// lane-0 `if` around the one atomic: with a per-lane 1 / 0 value the atomic
+// optimizer would scan the wave lane by lane).  No return value: the add is
+// fire-and-forget and the caller's poll of the same word starts at once.
+// Keep such lane-0 blocks away from loop headers and latches: a pair of them
+// there let the CFG structurizer run lane 0 through a loop nest of its own
+// (bulge.hip); the waits themselves are whole-wave loops (spin_geq).
+__device__ __forceinline__ void wave_arrive(unsigned *cnt) {
+  if (__lane_id() == 0)
+    (void)__hip_atomic_fetch_add((spin_u32 *)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Host: spin timeout of the persistent kernels, in 100 MHz ticks.  Every wait
