@@ -48,7 +48,7 @@ BOUND = {
     "bisect": ("hbm", "bytes"),
     "inverse_iteration": ("hbm", "bytes"),
     "back_transform": ("fp64_mfma", "flops"),
-    "bulge_chase": ("fp64", "flops"),     # latency-bound pipeline (3n dependent tasks)
+    "bulge_chase": ("fp64", "flops"),     # latency-bound pipeline (see bulge_chain)
     "tsqr_leaf": ("fp64", "flops"),       # latency-bound (32 dependent columns)
     "band_update": ("hbm", "bytes"),
     "q1_apply": ("hbm", "bytes"),
@@ -209,8 +209,21 @@ def cpu_baseline(H, W, args):
                         f"factorisation {t1 - t0:.2f}s + quantize/pack {t2 - t1:.2f}s"))
 
 
-PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02",
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03",
                         "pmc_traffic.json")
+LATENCY_BOUND = {"bulge_chase", "tsqr_leaf"}
+BULGE_GSW, BULGE_LAG = 2, 2  # csrc/bulge.hip G_SW, LAG
+
+
+def bulge_chain(n, avg_ms):
+    """The bulge pipeline's critical path: a group of G_SW
+    sweeps starts 4 + LAG (G_SW - 1) steps behind its predecessor (the
+    loader of step t - 1 waits for the producer's step t + 2 + LAG (G_SW - 1)
+    + 1), so one launch is about groups x that many dependent steps."""
+    groups = -(-(n - 2) // BULGE_GSW)
+    steps = groups * (4 + BULGE_LAG * (BULGE_GSW - 1))
+    return dict(dependent_steps=steps, us_per_step=round(avg_ms * 1e3 / steps, 3),
+                model="groups x (4 + LAG (G_SW - 1)) pipeline steps, G_SW = 2, LAG = 2")
 
 
 def pmc_traffic(cls, args):
@@ -228,6 +241,21 @@ def pmc_traffic(cls, args):
         return {}
     return dict(traffic=ent["traffic_bytes"], traffic_unit="bytes/launch",
                 traffic_source=os.path.relpath(PMC_FILE, os.path.dirname(PMC_FILE) + "/../.."))
+
+
+def pmc_summary(args):
+    """Time-weighted HBM bandwidth of every class with PMC passes (the same
+    committed profile as `pmc_traffic`; default workload only)."""
+    default = (args.n, args.m, args.tokens, args.bits, args.group, args.sym) == (
+        4096, 4096, 3072, 4, 128, False)
+    if not default or not os.path.exists(PMC_FILE):
+        return None
+    out = {}
+    for cls, ent in json.load(open(PMC_FILE)).items():
+        if "bandwidth_GBs" in ent:
+            out[cls] = dict(bytes_per_launch=ent["traffic_bytes"], GBs=ent["bandwidth_GBs"],
+                            hbm_frac=ent["hbm_frac"])
+    return out or None
 
 
 def launch_plan(gpus: int, env=None):
@@ -351,12 +379,15 @@ def run(args):
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
         else:
             achieved = per_launch / (avg_ms * 1e-3) / 1e12
-        roof = dict(kernel=name, bound="hbm" if kind == "hbm" else "mfma",
+        bound = "hbm" if kind == "hbm" else ("latency" if name in LATENCY_BOUND else "mfma")
+        roof = dict(kernel=name, bound=bound,
                     peak_kind=kind,
                     achieved=round(achieved, 3), peak=peak, unit=unit,
                     frac=round(achieved / peak, 4), traffic=None,
                     avg_launch_ms=round(avg_ms, 5), launches_per_step=p["launches"] // args.steps)
         roof.update(pmc_traffic(name, args))
+        if name == "bulge_chase":
+            roof["chain"] = bulge_chain(args.n, avg_ms)
 
     extra = {}
     if rank == 0:
@@ -364,6 +395,9 @@ def run(args):
         extra["phases_ms"] = ph
         extra["spectral_path"] = phases.path
         extra["kernel_ms_per_step"] = shares
+        pm = pmc_summary(args)
+        if pm:
+            extra["pmc_hbm"] = pm
         if not args.no_syrk:
             extra["syrk"] = syrk_bench(g, args, device)
     cpu = None

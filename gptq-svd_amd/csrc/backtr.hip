@@ -55,6 +55,7 @@ struct BtArgs {
   double *part;           // single: per-sub-chunk P partials (32 x 32 each)
   unsigned *cnt;          // [0] step counter, [1] timeout flag (zeroed per call)
   unsigned long long timeout;
+  int wexp;               // XCD form: workers wanted (= workgroups per XCD)
 };
 
 struct SmQ2 {
@@ -138,7 +139,7 @@ __device__ inline void q2_fetch(const BtArgs &a, int G2, int s, Q2Pre &p) {
   for (int q = 0; q < 16; ++q) {
     const int idx = lane + 64 * q, r = idx >> 5, d = idx & 31;
     const int jj = refl_valid(a.n, j0 + r, s) ? j0 + r : j0;
-    p.vv[q] = a.V2[(int64_t(jj) * a.smax + s) * SB_B + d];
+    p.vv[q] = d == 0 ? 1.0 : a.V2[(int64_t(jj) * a.smax + s) * SB_B + d];  // [0] holds tau
     p.tt[q] = Tb[idx];
   }
 }
@@ -541,8 +542,13 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
   const __amdgpu_buffer_rsrc_t rz =
       __builtin_amdgcn_make_buffer_rsrc(a.Z, 0, int(int64_t(a.n) * a.k * 8), 0x00020000);
 #if TG_BT_XCD
-  // workers: the workgroups on the first XCD to arrive; cnt[2] = XCD + 1,
-  // cnt[3] = worker tickets, cnt[4] = workgroups checked in (all of them)
+  // workers: the first a.wexp workgroups to arrive on the first XCD to
+  // arrive; cnt[2] = XCD + 1, cnt[3] = worker tickets, cnt[4] = workgroups
+  // checked in.  The workers start as soon as a.wexp tickets are out (the
+  // usual case: the dispatcher deals the grid of a.wexp x XCDs workgroups
+  // round-robin), or, when fewer land there, once every workgroup of the
+  // grid has checked in (then the ticket count is final): both ways every
+  // worker reads the same count.
   if (threadIdx.x == 0) {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
@@ -550,22 +556,29 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
     __hip_atomic_compare_exchange_strong((gu32 *)(a.cnt + 2), &expect, x + 1, __ATOMIC_RELAXED,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool mine = (expect == 0 ? x + 1 : expect) == x + 1;
-    sh_w[0] = mine ? int(__hip_atomic_fetch_add((gu32 *)(a.cnt + 3), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT))
-                   : -1;
+    int ticket = -1;
+    if (mine)
+      ticket = int(__hip_atomic_fetch_add((gu32 *)(a.cnt + 3), 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT));
+    // the ticket is taken (returned) before this workgroup counts as checked in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add((gu32 *)(a.cnt + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (mine) {  // worker count is known once every workgroup has checked in
+    sh_w[0] = ticket < a.wexp ? ticket : -1;
+    if (sh_w[0] >= 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load((gu32 *)(a.cnt + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-             gridDim.x) {
+      unsigned tk;
+      while ((tk = __hip_atomic_load((gu32 *)(a.cnt + 3), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT)) < unsigned(a.wexp) &&
+             __hip_atomic_load((gu32 *)(a.cnt + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 gridDim.x) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
           __hip_atomic_store((gu32 *)(a.cnt + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
-      sh_w[1] = int(__hip_atomic_load((gu32 *)(a.cnt + 3), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT));
+      tk = __hip_atomic_load((gu32 *)(a.cnt + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sh_w[1] = int(min(tk, unsigned(a.wexp)));
     }
   }
   __syncthreads();
@@ -730,18 +743,13 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
   int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
   // the workers (one CU each: BtShared fills the LDS) must all be resident:
-  // in the XCD form they are the workgroups of one XCD, so at most its CUs
+  // in the XCD form they are workgroups of one XCD, so at most its CUs
   // (sub-chunks beyond W are taken in turn by the loops)
-  static const int cu_xcd = [] {
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 32;
-    return std::max(1, ncu / 8);
-  }();
-  if (TG_BT_XCD) W = std::min(W, cu_xcd);
+  const XcdInfo xi = xcd_info();
+  if (TG_BT_XCD) W = std::min(W, xi.cus_per_xcd);
+  a.wexp = W;
   auto tok = prof_begin(st, PROF_Q2, 0.0, 0.0);
-  const int grid = TG_BT_XCD ? 8 * W : W;  // XCD form: ~W land on each XCD
+  const int grid = TG_BT_XCD ? xi.xcds * W : W;  // XCD form: W land on each XCD
   if (k <= 16)
     hipLaunchKernelGGL(bt_few_kernel<1>, dim3(grid), dim3(64 * BW), 0, st, a);
   else

@@ -49,7 +49,7 @@ struct SbBufs {
   double *Zg, *P, *Mz;    // back-transformation temporaries (ncmax*32 x k)
   // stage 2 (bulge.hip)
   double *Bst;            // band storage n x 2b
-  double *V2, *tau2;      // bulge-chasing reflectors ((n-2) x smax x b, (n-2) x smax)
+  double *V2;             // bulge-chasing reflector records (tau, v_1..v_{b-1}), (n-2) x smax x b
   double *T2;             // Q2 block T factors
   unsigned *prog;         // pipeline progress per sweep group
   // panel QR (pqr.hip): partials, broadcast block, per-panel control words
@@ -98,7 +98,6 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   const size_t nsw = size_t(std::max(1, n - 2)), smax = size_t(sb_smax(n));
   take(b.Bst, size_t(n) * 2 * SB_B);
   take(b.V2, nsw * smax * SB_B);
-  take(b.tau2, nsw * smax);
   take(b.T2, sb2st_t2_count(n));
   // per-group progress + 4 control words (XCD, group queue, stall flag)
   if constexpr (std::is_same_v<A, Arena>) b.prog = ar.template take<unsigned>(sb2st_prog_words(n));
@@ -122,13 +121,13 @@ hipError_t sy2sb_timed_out(hipStream_t st, const SbPlan &pl, const SbBufs &b, bo
 // 100 MHz clock, default 2 s) poisons d and e with NaN; the stall flag stays
 // in prog and is read back by sb2st_stalled (one D2H copy + stream sync).
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
-                 double *tau2, unsigned *prog, double *d, double *e);
+                 unsigned *prog, double *d, double *e);
 hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled);
 // Z (n x k row-major) <- Q2 Z.
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
-                       const double *tau2, double *T2);
+                       double *T2);
 // Q2 block T factors only (T2), for sb_apply_few.
-hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, const double *tau2, double *T2);
+hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, double *T2);
 // Z (n x k row-major, k <= 32) <- Q1 Q2 Z in one persistent launch (backtr.hip);
 // T2 must hold the Q2 T factors; dev: sb_apply_few_scratch bytes of device
 // scratch.  Syncs the stream (reads the barrier timeout flag).

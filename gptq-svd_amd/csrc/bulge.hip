@@ -19,7 +19,9 @@
 // Workgroups hand over through a per-group step counter.
 //
 // Band storage (lower, with bulge room): Bst[c * LDB + d] = B[c + d][c],
-// d < 2b.  Reflectors of (j, s): V2[(j * smax + s) * b + i], tau2[j * smax + s].
+// d < 2b.  Reflector of (j, s): the b-double record V2[(j * smax + s) * b ..]
+// holds tau in element 0 (v_0 = 1 is implicit) and v_1 .. v_{b-1} after it,
+// written as one 256-B line pair of 16-B stores.
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
@@ -191,10 +193,21 @@ __device__ __forceinline__ void first_refl(double (*R)[LDB], int n, int j, Refl 
 }
 
 
+// The reflector record (tau, v_1, .., v_{b-1}) by 16 lanes, 16 B each, as
+// non-temporal stores: the 68 MB record stream (n = 4096) is read back only
+// by the back-transform, and in the default policy it pushed the L2-resident
+// band's dirty lines out to memory (WRITE_SIZE 2x the record bytes).
+__device__ __forceinline__ void store_refl(double *rec, const Refl &r, int lane) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  if (lane < SB_B / 2) {
+    const double x0 = lane == 0 ? r.tau : r.v[2 * lane];
+    __builtin_nontemporal_store(d2{x0, r.v[2 * lane + 1]}, reinterpret_cast<d2 *>(rec) + lane);
+  }
+}
+
 template <bool FULL>
 __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, int s, int role,
-                                               bool has_next, double *__restrict__ V2,
-                                               double *__restrict__ tau2, int smax,
+                                               bool has_next, double *__restrict__ V2, int smax,
                                                WaveScratch &W, const Refl &rin, Refl &rout) {
   const int lane = threadIdx.x & 63, li = lane & 31, hf = lane >> 5;
   const int r1 = j + 1 + s * SB_B;
@@ -208,8 +221,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
   if (role == 0 && s == 0) {
     // the left block of (j, 0) is column j (written by first_refl) next to
     // columns that are already tridiagonal (zero in rows R): nothing to apply
-    if (hf == 0) V2[(int64_t(j) * smax) * SB_B + li] = rin.v[li];
-    if (lane == 0) tau2[int64_t(j) * smax] = rin.tau;
+    store_refl(V2 + int64_t(j) * smax * SB_B, rin, lane);
     return;
   }
   // block loads (issued before the reflector is needed)
@@ -306,8 +318,7 @@ __device__ __forceinline__ void bulge_task_lds(double (*R)[LDB], int n, int j, i
         if (FULL || i < L) Ac[i] = e[q] - twc * vk[q];
       }
     }
-    if (hf == 0) V2[(int64_t(j) * smax + s) * SB_B + li] = v;
-    if (lane == 0) tau2[int64_t(j) * smax + s] = tau;
+    store_refl(V2 + (int64_t(j) * smax + s) * SB_B, rin, lane);
   } else {
     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
@@ -415,8 +426,7 @@ __device__ __forceinline__ void publish(unsigned *p, unsigned v) {
 
 // ctl[0] = chosen XCD + 1, ctl[1] = group queue, ctl[2] = stall word
 __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, int n,
-                                                       double *__restrict__ V2,
-                                                       double *__restrict__ tau2, int smax,
+                                                       double *__restrict__ V2, int smax,
                                                        unsigned *__restrict__ prog,
                                                        unsigned *__restrict__ ctl,
                                                        unsigned long long *__restrict__ stats,
@@ -532,9 +542,9 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           Refl &ro = rfl[pair][(t + 1) & 1];
           HB(6)
           if (r1 >= SB_B && r1 + 2 * SB_B <= n)
-            bulge_task_lds<true>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
+            bulge_task_lds<true>(R, n, jj, s, role, nx, V2, smax, wsc[wid], ri, ro);
           else
-            bulge_task_lds<false>(R, n, jj, s, role, nx, V2, tau2, smax, wsc[wid], ri, ro);
+            bulge_task_lds<false>(R, n, jj, s, role, nx, V2, smax, wsc[wid], ri, ro);
           HB(7)
         } else if (pair < g && pair > 0 && s == -1 && role == 2) {
           first_refl(R, n, j0 + pair, rfl[pair][(t + 1) & 1]);
@@ -670,7 +680,7 @@ int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 size_t sb2st_prog_words(int n) { return size_t(cdiv(std::max(1, n - 2), G_SW)) + 4 + 64; }
 
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
-                 double *tau2, unsigned *prog, double *d, double *e) {
+                 unsigned *prog, double *d, double *e) {
   hipLaunchKernelGGL(extract_band_kernel, dim3(cdiv(int64_t(n) * LDB, 256)), dim3(256), 0, st, A,
                      int64_t(lda), n, Bst);
   hipError_t err = hipGetLastError();
@@ -712,7 +722,11 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     for (int j = 0; j < nsw; ++j) ntask += (n - 3 - j) / SB_B + 1;
     auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / G_SW,
                               12.0 * SB_B * SB_B * ntask);
-    hipLaunchKernelGGL(bulge_lds_kernel, dim3(256), dim3(BT), 0, st, Bst, n, V2, tau2, sb_smax(n),
+    // one workgroup per CU (the ring fills the LDS): the elected XCD's share
+    // of the grid is its CUs, the other XCDs' workgroups exit at once
+    const XcdInfo xi = xcd_info();
+    hipLaunchKernelGGL(bulge_lds_kernel, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st, Bst, n,
+                       V2, sb_smax(n),
                        prog, ctl, stats, timeout);
     tg::prof_end(st, tok);
     err = hipGetLastError();
@@ -798,8 +812,7 @@ constexpr int QR = QB + SB_B - 1;  // rows per block (63)
 
 __device__ inline bool refl_valid(int n, int j, int s) { return j <= n - 3 && s < ntasks(n, j); }
 
-__global__ __launch_bounds__(256) void q2_tfactor_kernel(const double *__restrict__ V2,
-                                                         const double *__restrict__ tau2, int n,
+__global__ __launch_bounds__(256) void q2_tfactor_kernel(const double *__restrict__ V2, int n,
                                                          int smax, double *__restrict__ T2) {
   __shared__ double Vs[QB][SB_B];
   __shared__ double Gs[QB][QB + 1];
@@ -811,9 +824,11 @@ __global__ __launch_bounds__(256) void q2_tfactor_kernel(const double *__restric
   if (!refl_valid(n, j0, s)) return;
   for (int idx = tid; idx < QB * SB_B; idx += 256) {
     const int a = idx / SB_B, i = idx % SB_B;
-    Vs[a][i] = refl_valid(n, j0 + a, s) ? V2[(int64_t(j0 + a) * smax + s) * SB_B + i] : 0.0;
+    const bool ok = refl_valid(n, j0 + a, s);
+    const double x = ok ? V2[(int64_t(j0 + a) * smax + s) * SB_B + i] : 0.0;
+    Vs[a][i] = i == 0 ? (ok ? 1.0 : 0.0) : x;
+    if (i == 0) taus[a] = x;  // element 0 of the record is tau
   }
-  if (tid < QB) taus[tid] = refl_valid(n, j0 + tid, s) ? tau2[int64_t(j0 + tid) * smax + s] : 0.0;
   __syncthreads();
   for (int q = 0; q < 4; ++q) {
     const int idx = tid + 256 * q, a = idx >> 5, c = idx & 31;
@@ -875,7 +890,7 @@ __global__ __launch_bounds__(256) void q2_apply_kernel(double *__restrict__ Z, i
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = threadIdx.x + 256 * q, a = idx >> 5, d = idx & 31;
-      Vs[a][d] = refl_valid(n, j0 + a, s) ? vv[q] : 0.0;
+      Vs[a][d] = refl_valid(n, j0 + a, s) ? (d == 0 ? 1.0 : vv[q]) : 0.0;
       Ts[a][d] = tt[q];
     }
   }
@@ -983,22 +998,22 @@ __global__ __launch_bounds__(256) void q2_apply_kernel(double *__restrict__ Z, i
 
 namespace tg {
 
-hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, const double *tau2,
+hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2,
                           double *T2) {
   const int nsw = n - 2;
   if (nsw <= 0) return hipSuccess;
   hipLaunchKernelGGL(q2_tfactor_kernel, dim3(sb_smax(n), cdiv(nsw, QB)), dim3(256), 0, st, V2,
-                     tau2, n, sb_smax(n), T2);
+                     n, sb_smax(n), T2);
   return hipGetLastError();
 }
 
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
-                       const double *tau2, double *T2) {
+                       double *T2) {
   const int nsw = n - 2;
   if (nsw <= 0) return hipSuccess;
   const int smax = sb_smax(n);
   const int ng2 = cdiv(nsw, QB);
-  hipLaunchKernelGGL(q2_tfactor_kernel, dim3(smax, ng2), dim3(256), 0, st, V2, tau2, n, smax, T2);
+  hipLaunchKernelGGL(q2_tfactor_kernel, dim3(smax, ng2), dim3(256), 0, st, V2, n, smax, T2);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   const int nlev = smax + ng2 - 1;
@@ -1028,7 +1043,7 @@ size_t sb2st_t2_count(int n) {
 // ---------------------------------------------------------------------------
 namespace {
 struct BandWs {
-  double *Bst, *V2, *tau2;
+  double *Bst, *V2;
   unsigned *prog;
 };
 template <class A>
@@ -1039,7 +1054,6 @@ void band_ws_layout(A &ar, int n, BandWs *p) {
   if constexpr (std::is_same_v<A, tg::Arena>) {
     b.Bst = ar.template take<double>(size_t(n) * LDB);
     b.V2 = ar.template take<double>(nsw * smax * SB_B);
-    b.tau2 = ar.template take<double>(nsw * smax);
     b.prog = ar.template take<unsigned>(tg::sb2st_prog_words(n));
   } else {
     ar.template take<double>(size_t(n) * LDB);
@@ -1068,7 +1082,7 @@ extern "C" int tg_band_tridiag(void *stream, const double *A, int n, int lda, do
   BandWs b{};
   band_ws_layout(ar, n, &b);
   TG_WS(ar);
-  TG_HIP(tg::sb2st(st, A, lda, n, b.Bst, b.V2, b.tau2, b.prog, d, e));
+  TG_HIP(tg::sb2st(st, A, lda, n, b.Bst, b.V2, b.prog, d, e));
   bool stalled = false;
   TG_HIP(tg::sb2st_stalled(st, n, b.prog, &stalled));
   if (stalled) {

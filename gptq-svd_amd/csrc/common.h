@@ -36,6 +36,14 @@ struct Sizer {
 
 __host__ __device__ inline int cdiv(int64_t a, int64_t b) { return int((a + b - 1) / b); }
 
+// Geometry of the current device (device.hip): XCD count (largest
+// HW_REG_XCC_ID seen by a probe launch, + 1) and CUs per XCD; measured once
+// per device and cached.
+struct XcdInfo {
+  int xcds = 0, cus_per_xcd = 0;
+};
+XcdInfo xcd_info();
+
 // Sampled HIP-event timing of tagged kernel classes (tg_profile_* in the C ABI).
 // A launch site calls prof_begin/prof_end around the launch on its stream; when
 // profiling is on, every `every`-th launch of the class is bracketed by events

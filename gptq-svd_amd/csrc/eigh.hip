@@ -1154,7 +1154,7 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   const bool ts = two_stage(n);
   if (ts) {
     TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
-    TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.tau2, sb.prog, w.d, w.e));
+    TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.prog, w.d, w.e));
     bool stalled = false;
     TG_HIP(tg::sb2st_stalled(st, n, sb.prog, &stalled));
     bool ptmo = false;
@@ -1355,7 +1355,7 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
     // few vectors (the complement path's request): one persistent launch
     const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
     if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl) <= sizeof(double) * size_t(n) * tg::SB_B) {
-      TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.tau2, sb.T2));
+      TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.T2));
       bool tmo = false;
       TG_HIP(tg::sb_apply_few(st, n, w.Z, k, pl, sb, sb.X, &tmo));
       if (tmo) {
@@ -1363,7 +1363,7 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
         return int(hipErrorLaunchTimeOut);
       }
     } else {
-      TG_HIP(tg::sb_apply_q2(st, n, w.Z, k, sb.V2, sb.tau2, sb.T2));
+      TG_HIP(tg::sb_apply_q2(st, n, w.Z, k, sb.V2, sb.T2));
       TG_HIP(tg::sb_apply_q1(st, n, w.Z, k, pl, sb));
     }
   }

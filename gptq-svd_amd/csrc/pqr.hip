@@ -67,7 +67,7 @@ struct PqrArgs {
   unsigned long long timeout;
   unsigned long long *stats;  // TG_PQR_STATS: per-phase clock stamps of workgroup 0 (or null)
   int force_fb;               // TG_PQR_FALLBACK=1: every panel through the Householder path (tests)
-  int wstride;                // blocks per worker: 8 (workers on one XCD) or 1 (spread over XCDs)
+  int wstride;                // blocks per worker: the XCD count (workers on one XCD) or 1
 };
 
 struct PqrSm {
@@ -478,7 +478,7 @@ __device__ __forceinline__ void lu_hr() {
 __device__ __forceinline__ void hr_top_ool() {
   PqrSm &sm = s_pq;
   const PqrArgs &g = sm.ga;
-  const int tid = otid(), lane = tid & 63, wid = tid >> 6;
+  const int tid = otid(), wid = tid >> 6;
   double(*UI)[33] = sm.Gs;
   double(*Tmp)[33] = reinterpret_cast<double(*)[33]>(&sm.MB[0][0]);  // MB is written last
   DBG_STAMP(16)
@@ -717,7 +717,7 @@ __device__ __forceinline__ int ph_decide(int npass) {
   PqrSm &sm = s_pq;
   const PqrArgs &g = sm.ga;
   const int tid = otid(), lane = tid & 63, wid = tid >> 6;
-  const int dk = npass == 1 ? 0 : 8;
+  [[maybe_unused]] const int dk = npass == 1 ? 0 : 8;
   DBG_STAMP(dk + 0)
   gram_reduce(g, sm);
   __syncthreads();
@@ -860,7 +860,7 @@ __device__ __noinline__ void ph_householder(int w, unsigned ep) {
 
 __global__ __launch_bounds__(PT) void pqr_kernel(PqrArgs ga) {
   PqrSm &sm = s_pq;
-  if (blockIdx.x % ga.wstride != 0) return;  // workers: one per 8 (one XCD under round-robin)
+  if (blockIdx.x % ga.wstride != 0) return;  // workers: one per XCD count (one XCD under round-robin)
   const int w = blockIdx.x / ga.wstride;
   const int tid = otid();
   if (tid == 0) sm.ga = ga;
@@ -954,7 +954,8 @@ hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, do
   // up to 32 workers share one XCD (launched x8, blockIdx % 8 == 0: one XCD
   // under round-robin dispatch -- speed only: the hand-offs are sc1 stores and
   // loads, correct across XCDs); more are spread over the chip
-  g.wstride = g.nw <= 32 ? 8 : 1;
+  const XcdInfo xi = xcd_info();
+  g.wstride = g.nw <= xi.cus_per_xcd ? xi.xcds : 1;
   hipLaunchKernelGGL(pqr_kernel, dim3(g.wstride * g.nw), dim3(PT), 0, st, g);
   prof_end(st, tok);
   if (g.stats) {
