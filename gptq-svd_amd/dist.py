@@ -32,6 +32,25 @@ def shard_rows(m: int, world: int, rank: int) -> tuple[int, int]:
     return r0, r0 + base + (1 if rank < extra else 0)
 
 
+def _gloo(pg) -> bool:
+    return dist.get_backend(pg) == "gloo"
+
+
+def all_reduce_sum(t: torch.Tensor, pg=None) -> torch.Tensor:
+    """SUM all-reduce; returns the result (device tensors go through the host
+    under gloo, which has no device-side reduction here)."""
+    world, _ = _world(pg)
+    if world == 1:
+        return t
+    if t.is_cuda and _gloo(pg):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=pg)
+        return h.to(t.device)
+    t = t.contiguous()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg)
+    return t
+
+
 def gather_packed(t: torch.Tensor, pg=None) -> torch.Tensor:
     """all_gather of one equally-shaped tensor per rank -> (world, *shape)."""
     world, _ = _world(pg)
@@ -49,6 +68,9 @@ def all_gather_rows(t: torch.Tensor, m: int, pg=None) -> torch.Tensor:
     if world == 1:
         return t
     rows_max = max(shard_rows(m, world, r)[1] - shard_rows(m, world, r)[0] for r in range(world))
+    dev = t.device
+    if t.is_cuda and _gloo(pg):
+        t = t.cpu()
     pad = torch.zeros((rows_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     pad[: t.shape[0]] = t
     bufs = [torch.empty_like(pad) for _ in range(world)]
@@ -57,7 +79,7 @@ def all_gather_rows(t: torch.Tensor, m: int, pg=None) -> torch.Tensor:
     for r in range(world):
         r0, r1 = shard_rows(m, world, r)
         parts.append(bufs[r][: r1 - r0])
-    return torch.cat(parts, dim=0)
+    return torch.cat(parts, dim=0).to(dev)
 
 
 def quantize_rows_sharded(W: torch.Tensor, U: torch.Tensor, perm: torch.Tensor, w_bits: int,

@@ -18,12 +18,26 @@ What differs, deliberately:
   calibration set several times over;
 * the re-forward stores each batch's actual size (the reference indexes with
   the accumulation loop's last ``curr_batch_size``, quantize.py:233-234,
-  which drops rows when n_samples % batch_size != 0);
+  which drops rows when n_samples % batch_size != 0), and a short last batch
+  gets the captured keyword tensors (attention mask ...) cut to its size;
 * OPT works: its sublayer names (``self_attn.out_proj``, ``fc1``, ``fc2``)
   are sequenced, and no ``model.model.rotary_emb`` is required
   (quantize.py:98 reads it and never uses it);
 * optional packing: with ``pack=True`` every quantised linear's AutoGPTQ
-  tensors are kept (``export.save_quantized`` writes them).
+  tensors are kept (``export.save_quantized`` writes them);
+* multi-GPU (one process per GPU, ``torch.distributed`` initialised): the
+  calibration sequences are sharded over the ranks (rank r takes sequences
+  r, r + world, ...) and stay sharded through the whole model; each group's H
+  is the all-reduce (SUM) of the ranks' FP64 sums x^T x and sample counts,
+  divided by the total count -- the single-process H up to the order of the
+  FP64 additions; every rank factorises that H (the solver is
+  deterministic, so every rank holds the same U, perm); each linear's rows
+  are quantised by their owning rank (``dist.shard_rows``; rows are
+  independent given U and perm) and all-gathered, so every rank writes the
+  same dequantised weight.  The reference places a 70B model's layers
+  across 8 GPUs and runs them one after another (quantize.py:238-249); here
+  each GPU holds the whole model (288 GB) and the ranks split the
+  calibration forward passes, the H accumulation and the quantisation.
 """
 from __future__ import annotations
 
@@ -34,8 +48,9 @@ from typing import Any, Dict, List, Optional, Sequence
 import torch
 from torch import nn
 
-from .gptq_utils import (HessianAccumulator, Quantizer, gptq_fwrd, pack_quantized,
-                         process_hessian, process_hessian_alt)
+from . import dist as tgdist
+from .gptq_utils import (HessianAccumulator, Quantizer, gptq_fwrd, log_quantization_error,
+                         pack_quantized, process_hessian, process_hessian_alt)
 
 __all__ = ["get_layers", "get_sequenced_groups", "capture_initial_inputs", "quantize_model",
            "adaptive_eps"]
@@ -89,6 +104,16 @@ def _to(v, device):
         return v.to(device)
     if isinstance(v, (list, tuple)):
         return type(v)(_to(x, device) for x in v)
+    return v
+
+
+def _batch_slice(v, cap: int, b: int):
+    """Keyword tensors captured with a batch of `cap` sequences (attention
+    masks, position embeddings of some models), cut to a batch of b < cap."""
+    if isinstance(v, torch.Tensor):
+        return v[:b] if v.dim() > 0 and v.shape[0] == cap else v
+    if isinstance(v, (list, tuple)):
+        return type(v)(_batch_slice(x, cap, b) for x in v)
     return v
 
 
@@ -146,13 +171,60 @@ def capture_initial_inputs(model: nn.Module, input_ids_list: Sequence[torch.Tens
     return inps, kw
 
 
+def _world(pg):
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(pg), dist.get_rank(pg)
+
+
+def allreduce_hessian(acc, pg=None) -> None:
+    """Sum the ranks' unnormalised H (FP64) and sample counts in place, so
+    ``acc.get_hessian()`` is the H of all ranks' rows together."""
+    world, _ = _world(pg)
+    if world == 1:
+        return
+    acc.H.copy_(tgdist.all_reduce_sum(acc.H, pg))
+    cnt = torch.tensor([float(acc.n_samples)], dtype=torch.float64, device=acc.H.device)
+    acc.n_samples = int(tgdist.all_reduce_sum(cnt, pg).item())
+
+
+def quantize_linear_sharded(W: torch.Tensor, R: torch.Tensor, perm: torch.Tensor,
+                            w_bits: int, group_size: int, sym: bool, block_size: int,
+                            use_triton: bool, pg=None):
+    """gptq_fwrd over this rank's rows of W, gathered: returns (dequantised W,
+    rank, Quantizer holding the gathered codes / scale / zero) on every rank."""
+    world, rank = _world(pg)
+    m, n = W.shape
+    r0, r1 = tgdist.shard_rows(m, world, rank)
+    q = Quantizer(w_bits=w_bits, group_size=group_size, sym=sym)
+    G = n // (group_size if group_size > 0 else n)
+    if r1 > r0:
+        Wq, k = gptq_fwrd(W[r0:r1], R, q, perm, block_size=block_size, use_triton=use_triton)
+        Wq = Wq.to(W.dtype)
+        codes = q.codes.to(torch.uint8)
+        scale, zero = q.scale.squeeze(-1).float(), q.zero.squeeze(-1).float()
+    else:
+        # no rows here (m < world): still join every gather
+        k = R.shape[0]
+        Wq = torch.empty((0, n), dtype=W.dtype, device=W.device)
+        codes = torch.empty((0, n), dtype=torch.uint8, device=W.device)
+        scale = torch.empty((0, G), dtype=torch.float32, device=W.device)
+        zero = torch.empty((0, G), dtype=torch.float32, device=W.device)
+    Wq = tgdist.all_gather_rows(Wq, m, pg)
+    q.codes = tgdist.all_gather_rows(codes, m, pg)
+    q.scale = tgdist.all_gather_rows(scale, m, pg).unsqueeze(-1)
+    q.zero = tgdist.all_gather_rows(zero, m, pg).unsqueeze(-1)
+    return Wq, k, q
+
+
 @torch.no_grad()
 def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mode: str = "eigh",
                    w_bits: int = 4, group_size: int = -1, sym: bool = False, eps: float = 1e-2,
                    threshold_method: str = "mean_trimmed", actorder: bool = False,
                    damp_percent: float = 0.01, use_adaptive_eps: bool = False,
                    batch_size: int = 8, device="cuda", block_size: int = 1024,
-                   pack: bool = False, offload: bool = False) -> Dict[str, Any]:
+                   pack: bool = False, offload: bool = False, pg=None) -> Dict[str, Any]:
     """Quantise every sequenced linear of `model` in place (layer by layer).
 
     mode "eigh" = TruncGPTQ (process_hessian_alt + gptq_fwrd(use_triton=True));
@@ -160,11 +232,18 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     `offload`: move each layer to `device` for its turn and back to the CPU
     afterwards (the reference's policy, quantize.py:101, :239); by default
     the model stays where it is (a whole 8B/70B model fits in 288 GB).
+    `pg`: process group of the multi-GPU mode (module docstring); it is on
+    whenever torch.distributed is initialised with more than one rank.
     Returns {"layer_stats": [...], "total_time": s, "packed": {name: tensors}}.
     """
     if mode not in ("eigh", "gptq"):
         raise ValueError(f"mode must be 'eigh' or 'gptq', got {mode!r}")
     t_start = time.time()
+    world, rank = _world(pg)
+    if world > 1:
+        input_ids_list = list(input_ids_list)[rank::world]
+        if not input_ids_list:
+            raise ValueError(f"rank {rank}: fewer calibration sequences than ranks ({world})")
     inps, layer_kwargs = capture_initial_inputs(model, input_ids_list, device=device,
                                                 batch_size=batch_size)
     kw = {k: _to(v, device) for k, v in layer_kwargs.items()}
@@ -176,9 +255,14 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     stats: List[Dict[str, Any]] = []
     packed: Dict[str, Dict[str, torch.Tensor]] = {}
 
+    cap = min(batch_size, n_samples)  # batch the keyword tensors were captured with
+
     def run_layer(layer, dst: Optional[torch.Tensor]):
         for j in range(0, n_samples, batch_size):
-            out = layer(inps[j: j + batch_size], **kw)
+            x = inps[j: j + batch_size]
+            kwb = kw if x.shape[0] == cap else {k: _batch_slice(v, cap, x.shape[0])
+                                                 for k, v in kw.items()}
+            out = layer(x, **kwb)
             if dst is not None:
                 out = out[0] if isinstance(out, (tuple, list)) else out
                 dst[j: j + out.shape[0]] = out
@@ -197,6 +281,7 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
                 run_layer(layer, None)
             finally:
                 hook.remove()
+            allreduce_hessian(acc, pg)
             H = acc.get_hessian()
             del acc
             if mode == "eigh":
@@ -210,15 +295,22 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
                 sub = _submodule(layer, name)
                 q = Quantizer(w_bits=w_bits, group_size=group_size, sym=sym)
                 t0 = time.time()
-                Wq, rank = gptq_fwrd(sub.weight.data.float(), R, q, perm, block_size=block_size,
-                                     use_triton=(mode == "eigh"), R_x=R_x)
+                if world > 1:
+                    W = sub.weight.data.float()
+                    Wq, k, q = quantize_linear_sharded(W, R, perm, w_bits, group_size, sym,
+                                                       block_size, mode == "eigh", pg)
+                    if R_x is not None and rank == 0:
+                        log_quantization_error(W, Wq, R_x, perm)
+                else:
+                    Wq, k = gptq_fwrd(sub.weight.data.float(), R, q, perm,
+                                      block_size=block_size, use_triton=(mode == "eigh"), R_x=R_x)
                 sub.weight.copy_(Wq)
                 full = f"layer_{i}.{name}"
                 if pack:
                     qw, qz, sc = pack_quantized(q)
                     packed[qual.get(id(sub), full)] = dict(qweight=qw, qzeros=qz, scales=sc)
                 dt = time.time() - t0
-                used = rank if mode == "eigh" else "N/A"
+                used = k if mode == "eigh" else "N/A"
                 logging.info(f"   {name: <15} | Rank: {str(used): <4} | Time: {dt:.2f}s")
                 stats.append({"name": full, "rank": used, "time": dt})
             del R, R_x, perm
@@ -227,5 +319,6 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
         if offload:
             layers[i] = layer.to("cpu")
         logging.info(f"[*] Layer {i + 1}/{len(layers)} completed in {time.time() - t_layer:.2f}s")
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     return {"layer_stats": stats, "total_time": time.time() - t_start, "packed": packed}

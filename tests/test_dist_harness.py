@@ -1,0 +1,145 @@
+"""CPU multi-process (gloo, world_size 2) coverage of the harness's multi-GPU
+mode (harness.py module docstring): calibration sequences sharded over the
+ranks, each group's H all-reduced (FP64 sums + counts), rows of every linear
+quantised by their owning rank and all-gathered.
+
+The solver calls are replaced by the CPU oracle (tests only: the HIP library
+needs a GPU), so this checks the distributed plumbing: against the
+single-process run with the same stand-ins every H agrees to FP64 rounding
+(only the order of the additions differs), every rank ends with the same
+weights bit for bit, and the weights equal the single-process ones.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def tiny_opt(seed):
+    from transformers import OPTConfig, OPTForCausalLM
+    cfg = OPTConfig(vocab_size=256, hidden_size=64, ffn_dim=256, num_hidden_layers=2,
+                    num_attention_heads=4, max_position_embeddings=64, word_embed_proj_dim=64,
+                    do_layer_norm_before=True, dropout=0.0, attention_dropout=0.0)
+    cfg._attn_implementation = "eager"
+    torch.manual_seed(seed)
+    return OPTForCausalLM(cfg).float().eval()
+
+
+def _patch(harness, hs):
+    """CPU stand-ins for the HIP solver calls; `hs` collects every group's H."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as o
+
+    class CpuAcc:
+        def __init__(self, n, device=None):
+            self.H = torch.zeros((n, n), dtype=torch.float64)
+            self.n_samples = 0
+
+        def add_batch(self, x):
+            x = x.reshape(-1, x.shape[-1]).double()
+            self.H += x.T @ x
+            self.n_samples += x.shape[0]
+
+        def get_hessian(self):
+            H = self.H / self.n_samples
+            hs.append(H.clone())
+            return H
+
+    def solve(H, threshold=1e-4, threshold_method="energy"):
+        f = o.process_hessian_alt(H.numpy(), threshold, threshold_method)
+        return (torch.from_numpy(np.ascontiguousarray(f.U)),
+                torch.from_numpy(np.ascontiguousarray(f.R_x)), torch.from_numpy(f.perm))
+
+    def fwrd(W, R, q, perm, block_size=1024, use_triton=True, R_x=None):
+        Wn = W.float().numpy()
+        Wq, k, codes = o.gptq_fwrd(Wn, R.numpy(), perm.numpy(), q.w_bits, q.group_size, q.sym,
+                                   block_size, gemm="fma", impl="c", return_codes=True)
+        s, z = o.find_params(Wn, q.w_bits, q.group_size, q.sym)
+        q.codes = torch.from_numpy(codes)
+        q.scale = torch.from_numpy(np.asarray(s, np.float32)).reshape(W.shape[0], -1, 1)
+        q.zero = torch.from_numpy(np.asarray(z, np.float32)).reshape(W.shape[0], -1, 1)
+        return torch.from_numpy(Wq), k
+
+    harness.HessianAccumulator = CpuAcc
+    harness.process_hessian_alt = solve
+    harness.gptq_fwrd = fwrd
+    harness.log_quantization_error = lambda *a, **k: None
+
+
+def _run(ids):
+    import gptq_svd_amd.harness as harness
+    hs = []
+    _patch(harness, hs)
+    model = tiny_opt(5)
+    res = harness.quantize_model(model, ids, mode="eigh", w_bits=4, group_size=64, sym=False,
+                                 eps=1e-3, threshold_method="energy", batch_size=2, device="cpu")
+    W = {n: p.detach().clone().numpy() for n, p in model.named_parameters()
+         if n.endswith("weight") and "layers" in n and p.dim() == 2}
+    return hs, res, W
+
+
+def _worker(rank, world, port, ids, out):
+    torch.set_num_threads(1)
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hs, res, W = _run(ids)
+        out[rank] = dict(H=[h.numpy() for h in hs], W=W,
+                         ranks=[s["rank"] for s in res["layer_stats"]])
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_token_sharded_harness_matches_single():
+    torch.set_num_threads(2)
+    gen = torch.Generator().manual_seed(9)
+    ids = [torch.randint(0, 256, (1, 16), generator=gen) for _ in range(6)]
+    hs1, res1, W1 = _run(ids)
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_worker, args=(2, _free_port(), ids, out), nprocs=2, join=True)
+    r0, r1 = out[0], out[1]
+    assert len(r0["H"]) == len(hs1) == 8  # 2 layers x 4 groups
+    for a, b, c in zip(r0["H"], r1["H"], hs1):
+        assert np.array_equal(a, b)  # every rank factorises the same H
+        c = c.numpy()
+        assert np.abs(a - c).max() <= 1e-12 * np.abs(c).max()
+    assert r0["ranks"] == r1["ranks"] == [s["rank"] for s in res1["layer_stats"]]
+    assert W1.keys() == r0["W"].keys() == r1["W"].keys()
+    for name in W1:
+        assert np.array_equal(r0["W"][name], r1["W"][name]), name
+        assert np.array_equal(r0["W"][name], W1[name]), name
+
+
+def test_allreduce_hessian_single_process_is_noop():
+    from gptq_svd_amd.harness import allreduce_hessian
+
+    class A:
+        H = torch.ones(3, 3, dtype=torch.float64)
+        n_samples = 4
+    a = A()
+    allreduce_hessian(a)
+    assert a.n_samples == 4 and float(a.H.sum()) == 9.0
+
+
+if __name__ == "__main__":
+    pytest.main([__file__, "-q"])
