@@ -583,6 +583,19 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
   const int ci = min(tm / c, nc - 1), cj = min(tn / c, nc - 1);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
+  // the tile's old values first (clamped addresses): their HBM latency
+  // overlaps the S / YS set-up and the K loop instead of following it
+  double old[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = min(tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r, m - 1);
+        const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
+        old[i][j][r] = A[int64_t(gi) * lda + gj];
+      }
   // S_IJ and YS = -(Y_rows S_IJ)
   for (int idx = tid; idx < SB_B * SB_B; idx += 256) {
     const int x = idx >> 5, y = idx & 31;
@@ -649,19 +662,8 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
     }
     __syncthreads();
   }
-  // old values loaded together (clamped), then the lower tile written and,
-  // for an off-diagonal tile, its transpose written row-contiguous from LDS
-  double old[2][2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = min(tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r, m - 1);
-        const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
-        old[i][j][r] = A[int64_t(gi) * lda + gj];
-      }
+  // the lower tile written and, for an off-diagonal tile, its transpose
+  // written row-contiguous from LDS
   double(*Tt)[S2T + 1] = reinterpret_cast<double(*)[S2T + 1]>(sm);  // K loop done (barrier)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -681,6 +683,142 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
   if (tm != tn) {
     __syncthreads();
     for (int idx = tid; idx < S2T * S2T; idx += 256) {
+      const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
+      if (tn + lc < m && tm + lr < m) A[int64_t(tn + lc) * lda + tm + lr] = Tt[lr][lc];
+    }
+  }
+}
+
+// Single-level panels: W = X - 1/2 Y M in place over X (m x 32 each, M 32 x
+// 32), so the trailing update is the rank-64 A22 -= Y W^T + W Y^T (K = 64
+// instead of the K = 96 form above, which folds Y S Y^T into the tiles).
+// One workgroup per 16 rows (m / 16 workgroups: the latency of one row's
+// loads, not a queue of rows, sets the time): M in LDS, the thread's Y row
+// and X pair straight from L2, two outputs per thread.
+constexpr int WU_R = 16;
+__global__ __launch_bounds__(256) void w_update_kernel(const double *__restrict__ Y,
+                                                       double *__restrict__ X, int m,
+                                                       const double *__restrict__ M) {
+  __shared__ double2 Ms[SB_B][SB_B / 2];
+  const int tid = threadIdx.x;
+  const int r = blockIdx.x * WU_R + (tid >> 4), c2 = tid & 15;  // row r, columns 2c2, 2c2 + 1
+  const int rc = min(r, m - 1);
+  double2 y[SB_B / 2];
+#pragma unroll
+  for (int h = 0; h < SB_B / 2; ++h) y[h] = reinterpret_cast<const double2 *>(Y + int64_t(rc) * SB_B)[h];
+  const double2 x = reinterpret_cast<const double2 *>(X + int64_t(rc) * SB_B)[c2];
+  for (int e = tid; e < SB_B * SB_B / 2; e += 256)
+    Ms[e >> 4][e & 15] = reinterpret_cast<const double2 *>(M)[e];
+  __syncthreads();
+  double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+  for (int h = 0; h < SB_B / 2; ++h) {
+    const double2 a = Ms[2 * h][c2], b = Ms[2 * h + 1][c2];
+    v0 = fma(y[h].x, a.x, v0);
+    v1 = fma(y[h].x, a.y, v1);
+    v0 = fma(y[h].y, b.x, v0);
+    v1 = fma(y[h].y, b.y, v1);
+  }
+  if (r < m)
+    reinterpret_cast<double2 *>(X + int64_t(r) * SB_B)[c2] = make_double2(x.x - 0.5 * v0, x.y - 0.5 * v1);
+}
+
+// A22 -= Y W^T + W Y^T on 64 x 64 lower tiles, mirrored (A22 stays bitwise
+// symmetric).  The whole K = 64 of both operands is staged at once -- A side
+// [Y_rows | W_rows], B side [W_cols | Y_cols], k-major -- behind ONE barrier,
+// with the tile's old values already in flight: the K = 96 kernel above
+// waits out an L2 round trip per 16-deep slab.  Two workgroups per CU.
+constexpr int WT = 64, WK = 2 * SB_B, WP = 4;
+__global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A, int64_t lda, int m,
+                                                         const double *__restrict__ Y,
+                                                         const double *__restrict__ W) {
+  __shared__ double Aop[WK][WT + WP];
+  __shared__ double Bop[WK][WT + WP];
+  const int b = blockIdx.x;
+  int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= b) ++I;
+  while (I * (I + 1) / 2 > b) --I;
+  const int J = b - I * (I + 1) / 2;
+  const int tm = I * WT, tn = J * WT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  double old[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = min(tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r, m - 1);
+        const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
+        old[i][j][r] = A[int64_t(gi) * lda + gj];
+      }
+  {
+    // thread: row tid / 4 of the tile, 8 consecutive k (two 16-B loads) of
+    // each of Y_r, W_r, W_c, Y_c
+    const int rl = tid >> 2, k0 = (tid & 3) * 8;
+    const int gr = min(tm + rl, m - 1), gc = min(tn + rl, m - 1);
+    const bool okr = tm + rl < m, okc = tn + rl < m;
+    double2 v[4][4];
+    const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
+                            W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int k = k0 + 2 * h;
+      Aop[k][rl] = okr ? v[0][h].x : 0.0;
+      Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
+      Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
+      Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
+      Bop[k][rl] = okc ? v[2][h].x : 0.0;
+      Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
+      Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
+      Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
+    }
+  }
+  __syncthreads();
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kq = 0; kq < WK; kq += 4) {
+    double af[2], bf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();  // operand images dead: Aop becomes the mirror tile
+  double(*Tt)[WT + 1] = reinterpret_cast<double(*)[WT + 1]>(&Aop[0][0]);
+  static_assert(WK * (WT + WP) >= WT * (WT + 1), "mirror tile must fit");
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int li = wm * 32 + i * 16 + (lane >> 4) + 4 * r, lj = wn * 32 + j * 16 + (lane & 15);
+        const int gi = tm + li, gj = tn + lj;
+        if (gi < m && gj < m && gi >= gj) {
+          const double v = old[i][j][r] - acc[i][j][r];
+          A[int64_t(gi) * lda + gj] = v;
+          if (tm != tn) Tt[li][lj] = v;
+          else if (gi != gj) A[int64_t(gj) * lda + gi] = v;
+        }
+      }
+  if (tm != tn) {
+    __syncthreads();
+    for (int idx = tid; idx < WT * WT; idx += 256) {
       const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
       if (tn + lc < m && tm + lr < m) A[int64_t(tn + lc) * lda + tm + lr] = Tt[lr][lc];
     }
@@ -925,10 +1063,13 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
                        b.pq_part, b.pq_ctl + 1);
     TG_CHK(hipGetLastError());
-    const int nt = cdiv(m, S2T);
-    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 96.0 * double(m) * m);
-    hipLaunchKernelGGL(syr2k_bs_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                       int64_t(lda), m, m, 1, Yp, b.X, int64_t(SB_B), b.M, int64_t(SB_B));
+    // W = X - Y M / 2 in place, then A22 -= Y W^T + W Y^T
+    hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, b.X, m, b.M);
+    TG_CHK(hipGetLastError());
+    const int nt = cdiv(m, WT);
+    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
+    hipLaunchKernelGGL(syr2k_w_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                       int64_t(lda), m, Yp, b.X);
     prof_end(st, tok);
     TG_CHK(hipGetLastError());
   }

@@ -140,8 +140,11 @@ __device__ inline void mainloop(const TA_ *__restrict__ A, int64_t lda,
   }
 }
 
-// C = alpha acc + beta C for the 4-wave tile; the beta != 0 reads are issued
-// together (clamped addresses) so they overlap instead of serialising.
+// C = alpha acc + beta C for the 4-wave tile, one 16-row fragment row at a
+// time: its FN x 4 beta != 0 reads are issued together (clamped addresses)
+// so they overlap, and at most FN x 4 of them are live -- the whole tile's
+// worth (FM x FN x 4 doubles on top of the accumulators) set the kernel's
+// register count to one wave per SIMD.
 template <int BM, int BN, bool SYRK, bool MIRROR = true>
 __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double alpha, double beta,
                                 double *__restrict__ C, int64_t ldc, int M, int N, int tm,
@@ -150,21 +153,19 @@ __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double 
   constexpr int FM = WM / 16, FN = WN / 16;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  double cv[FM][FN][4];
-  if (beta != 0.0) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < FM; ++i) {
+    double cv[FN][4];
+    if (beta != 0.0) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int gi = min(tm + wm * WM + i * 16 + (lane >> 4) + 4 * r, M - 1);
           const int gj = min(tn + wn * WN + j * 16 + (lane & 15), N - 1);
-          cv[i][j][r] = C[int64_t(gi) * ldc + gj];
+          cv[j][r] = C[int64_t(gi) * ldc + gj];
         }
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -172,15 +173,18 @@ __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double 
         const int gi = tm + wm * WM + i * 16 + (lane >> 4) + 4 * r;
         const int gj = tn + wn * WN + j * 16 + (lane & 15);
         if (gi < M && gj < N) {
-          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * cv[i][j][r];
+          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * cv[j][r];
           C[int64_t(gi) * ldc + gj] = v;
           if (SYRK && MIRROR && tm != tn) C[int64_t(gj) * ldc + gi] = v;
         }
       }
+  }
 }
 
+// 128 x 128 tiles: two workgroups per CU (LDS 2 x 74 KB) need <= 256
+// registers per lane (128 accumulators + the loop's operands and staging)
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK, bool MIRROR = true>
-__global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha,
+__global__ __launch_bounds__(256, BM >= 128 ? 2 : 3) void dgemm_kernel(int M, int N, int K, double alpha,
                                                     const TA_ *__restrict__ A, int64_t lda,
                                                     const TB_ *__restrict__ B, int64_t ldb,
                                                     double beta, double *__restrict__ C,
@@ -330,6 +334,27 @@ bool use_blas(int M, int N, int K, const double *A, const double *B, const doubl
 }  // namespace
 
 namespace tg {
+// Tile of the own DGEMM: TG_GEMM_TILE=128|12864|64 forces one (development
+// switch, read per call).  Otherwise 128 x 128 (two workgroups per CU, the
+// most MFMA work per staged byte) when its tiles fill at least 85% of their
+// last round on the chip, else 64 x 64 (three per CU): at M = N = 3058 the
+// 576 big tiles run as 512 + 64 (40 TF/s) where 2304 small ones make three
+// full rounds (51 TF/s); at 4096^2 the big tiles make two (57 vs 53 TF/s).
+static int gemm_tile(int M, int N) {
+  if (const char *t = getenv("TG_GEMM_TILE")) return atoi(t);
+  static const int slots128 = 2 * [] {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+    return std::max(1, ncu);
+  }();
+  const int64_t t = int64_t(cdiv(M, 128)) * cdiv(N, 128);
+  if (t < slots128 / 2) return 64;
+  const int64_t rounds = (t + slots128 - 1) / slots128;
+  return double(t) >= 0.85 * double(rounds * slots128) ? 128 : 64;
+}
+
 hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
                  const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                  double *C, int64_t ldc) {
@@ -347,10 +372,13 @@ hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double a
   if (K <= 0) {
     // C = beta * C (alpha * 0): run with K = 0 -> the kernel writes beta*C
   }
-  const int64_t tiles128 = int64_t(cdiv(M, 128)) * cdiv(N, 128);
-  if (tiles128 >= 256)
+  const int tile = gemm_tile(M, N);
+  if (tile == 128)
     return dispatch_t<double, double, 128, 128>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
                                                 C, ldc);
+  if (tile == 12864)
+    return dispatch_t<double, double, 128, 64>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
+                                               C, ldc);
   return dispatch_t<double, double, 64, 64>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C,
                                             ldc);
 }
@@ -371,11 +399,14 @@ hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, 
   hipLaunchKernelGGL((dgemm_chunked_kernel<BM_, BM_, TA_, TB_>),                              \
                      dim3(cdiv(N, BM_), cdiv(M, BM_), cs.nc), dim3(256), 0, st, cs, alpha, A, \
                      lda, B, ldb, beta, C, ldc)
+#ifndef TG_XG_BM
+#define TG_XG_BM 64
+#endif
   if (narrow) {
-    if (!ta && !tb) TG_CH2(64, 32, false, false);
-    else if (!ta && tb) TG_CH2(64, 32, false, true);
-    else if (ta && !tb) TG_CH2(64, 32, true, false);
-    else TG_CH2(64, 32, true, true);
+    if (!ta && !tb) TG_CH2(TG_XG_BM, 32, false, false);
+    else if (!ta && tb) TG_CH2(TG_XG_BM, 32, false, true);
+    else if (ta && !tb) TG_CH2(TG_XG_BM, 32, true, false);
+    else TG_CH2(TG_XG_BM, 32, true, true);
   } else if (big) {
     if (!ta && !tb) TG_CH(128, false, false);
     else if (!ta && tb) TG_CH(128, false, true);

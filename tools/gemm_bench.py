@@ -15,6 +15,10 @@ cases = [  # (name, ta, tb, M, N, K, beta)
     ("TN trail K32", 1, 0, 2994, 4032, 32, 1.0),
     ("TN syrk-like K32", 1, 0, 4096, 4096, 32, 1.0),
     ("NN U12 64", 0, 0, 64, 4032, 64, 0.0),
+    ("NN k k k", 0, 0, 3058, 3058, 3058, 0.0),
+    ("TN k n k", 1, 0, 3058, 4096, 3058, 0.0),
+    ("NN k n k", 0, 0, 3058, 4096, 3058, 0.0),
+    ("NT k k m", 0, 1, 3058, 3058, 1038, 1.0),
 ]
 for name, ta, tb, M, N, K, beta in cases:
     A = torch.randn((K, M) if ta else (M, K), dtype=torch.float64, device=dev)
