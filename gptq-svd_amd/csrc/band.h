@@ -55,6 +55,7 @@ struct SbBufs {
   // panel QR (pqr.hip): partials, broadcast block, per-panel control words
   double *pq_part, *pq_bc;
   unsigned *pq_ctl;       // [0] timeout flag, [1] M-kernel ticket, [4 + 4 i] panel i counters
+  unsigned *xm_tick;      // X / M kernel tickets (band.hip xm_kernel), xm_tick_words(n)
 };
 
 int pqr_rows_per_thread(int m);
@@ -70,6 +71,8 @@ size_t sb2st_t2_count(int n);
 
 // control words: 4 + 4 per panel, padded to a multiple of 16 bytes
 inline size_t pq_ctl_words(int n) { return 4 + 4 * size_t(std::max(1, n / SB_B + 1)); }
+// X / M kernel: one ticket per group of 16 row blocks of 16 rows, + 1
+inline size_t xm_tick_words(int n) { return size_t(n) / 256 + 8; }
 
 template <class A>
 void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
@@ -90,7 +93,9 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.R[0], w * SB_B);
   take(b.R[1], w * SB_B);
   take(b.Gr, w * n);
-  take(b.U, w * n);  // X partials: one m x 32 slab per 256-row block of A22
+  // X partials: one m x 32 slab per 256-row block of A22 (TSQR path); the
+  // single path's X / M partials (n / 16 + n / 256 blocks of 1024) fit too
+  take(b.U, std::max(w * n, (size_t(n) / 16 + size_t(n) / 256 + 2) * 1024));
   take(b.Xs, w * w);
   take(b.Zg, w * kmax);
   take(b.P, w * kmax);
@@ -109,6 +114,8 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.pq_bc, PQR_BC_DOUBLES);
   if constexpr (std::is_same_v<A, Arena>) b.pq_ctl = ar.template take<unsigned>(pq_ctl_words(n));
   else ar.template take<unsigned>(pq_ctl_words(n));
+  if constexpr (std::is_same_v<A, Arena>) b.xm_tick = ar.template take<unsigned>(xm_tick_words(n));
+  else ar.template take<unsigned>(xm_tick_words(n));
 }
 
 // A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth

@@ -689,6 +689,160 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
   }
 }
 
+// Single-level panels: X = A22 YT (m x 32, K = m) by row blocks, with the
+// 32 x 32 products Y_zᵀ X_z of the blocks reduced on the way to
+// M = Tᵀ (Yᵀ X) -- replaces the split-K GEMM over 256-row blocks of A22ᵀ,
+// its partial sum and the separate M reduction (three launches).
+// One workgroup per XR rows, XW waves splitting K: wave w streams its
+// K / XW columns of the XR rows (lane (r, kq) reads 4 consecutive k of row r,
+// so every row's 128 B come in one instruction) two iterations ahead and
+// accumulates a 16 x 32 tile on FP64 MFMA; the XW tiles are summed in wave
+// order.  Yᵀ X partials: per workgroup, then per group of XG workgroups by
+// its last arriver, then over the groups by the last group (fixed orders:
+// bit-reproducible); the very last workgroup forms M.  Tickets: tick[0 ..
+// groups) and tick[groups], zero before the launch, reset by their last
+// arrivers.
+constexpr int XR = 16, XW = 8, XG = 16;
+struct XmArgs {
+  const double *A;  // A22, lda
+  int64_t lda;
+  int m;
+  const double *YT, *Y, *T;
+  double *X, *part, *gpart, *M;
+  unsigned *tick;
+};
+struct XmFrag {
+  double a[4], b[4][2];
+};
+template <bool VEC>
+__device__ __forceinline__ void xm_load(const XmArgs &g, int row, int k0, int ke, XmFrag &f) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int kk = k0 + 4 * kq;
+  const bool rok = row < g.m;
+  const double *ar = g.A + int64_t(min(row, g.m - 1)) * g.lda;
+  if (VEC && kk + 3 < ke) {
+    const double2 lo = *reinterpret_cast<const double2 *>(ar + kk);
+    const double2 hi = *reinterpret_cast<const double2 *>(ar + kk + 2);
+    f.a[0] = rok ? lo.x : 0.0;
+    f.a[1] = rok ? lo.y : 0.0;
+    f.a[2] = rok ? hi.x : 0.0;
+    f.a[3] = rok ? hi.y : 0.0;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double v = ar[min(kk + s, g.m - 1)];
+      f.a[s] = (rok && kk + s < ke) ? v : 0.0;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const double v = g.YT[int64_t(min(kk + s, g.m - 1)) * SB_B + 16 * j + r];
+      f.b[s][j] = kk + s < ke ? v : 0.0;
+    }
+}
+__device__ __forceinline__ void xm_mma(const XmFrag &f, doublex4 (&acc)[2]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[s], f.b[s][j], acc[j], 0, 0, 0);
+}
+template <bool VEC>
+__global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
+  __shared__ double red[XW][XR][SB_B + 1];  // the last workgroup reuses it for C, T
+  __shared__ double xs[XR][SB_B + 1], ys[XR][SB_B + 1];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r0 = blockIdx.x * XR;
+  const int G = int(gridDim.x), NG = (G + XG - 1) / XG;
+  {
+    const int rr = tid >> 5, c = tid & 31;  // XR x 32 = 512 = blockDim
+    const int row = r0 + rr;
+    ys[rr][c] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
+  }
+  const int KQ = ((g.m + XW - 1) / XW + 15) / 16 * 16;
+  const int kb = wid * KQ, ke = min(g.m, kb + KQ);
+  const int row = r0 + (lane & 15);
+  doublex4 acc[2] = {doublex4{0.0, 0.0, 0.0, 0.0}, doublex4{0.0, 0.0, 0.0, 0.0}};
+  if (kb < ke) {
+    XmFrag f0, f1, f2;
+    xm_load<VEC>(g, row, kb, ke, f0);
+    xm_load<VEC>(g, row, kb + 16, ke, f1);
+    for (int k0 = kb; k0 < ke; k0 += 48) {
+      xm_load<VEC>(g, row, k0 + 32, ke, f2);
+      xm_mma(f0, acc);
+      xm_load<VEC>(g, row, k0 + 48, ke, f0);
+      xm_mma(f1, acc);
+      xm_load<VEC>(g, row, k0 + 64, ke, f1);
+      xm_mma(f2, acc);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wid][(lane >> 4) + 4 * q][16 * j + (lane & 15)] = acc[j][q];
+  __syncthreads();
+  {
+    const int rr = tid >> 5, c = tid & 31;
+    double x = 0.0;
+#pragma unroll
+    for (int w = 0; w < XW; ++w) x += red[w][rr][c];
+    if (r0 + rr < g.m) g.X[int64_t(r0 + rr) * SB_B + c] = x;
+    xs[rr][c] = r0 + rr < g.m ? x : 0.0;
+  }
+  __syncthreads();
+  // this block's Y_zᵀ X_z, write-through, then the group ticket
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+    const int a = e >> 5, c = e & 31;
+    double p = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < XR; ++rr) p = fma(ys[rr][a], xs[rr][c], p);
+    __hip_atomic_store(&g.part[size_t(blockIdx.x) * 1024 + e], p, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int grp = blockIdx.x / XG, z0 = grp * XG, z1 = min(G, z0 + XG);
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(&g.tick[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             unsigned(z1 - z0 - 1);
+  __syncthreads();
+  if (!s_last) return;
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+    double s = 0.0;
+    for (int z = z0; z < z1; ++z) s += tg::load_partial(&g.part[size_t(z) * 1024 + e]);
+    __hip_atomic_store(&g.gpart[size_t(grp) * 1024 + e], s, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    g.tick[grp] = 0u;
+    s_last = __hip_atomic_fetch_add(&g.tick[NG], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             unsigned(NG - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double *Cs = &red[0][0][0], *Ts = Cs + SB_B * SB_B;
+  static_assert(XW * XR * (SB_B + 1) >= 2 * SB_B * SB_B, "C and T fit in red");
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+    double s = 0.0;
+    for (int q = 0; q < NG; ++q) s += tg::load_partial(&g.gpart[size_t(q) * 1024 + e]);
+    Cs[e] = s;
+    Ts[e] = g.T[e];
+  }
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+    const int a = e >> 5, c = e & 31;
+    double v = 0.0;
+    for (int k = 0; k <= a; ++k) v = fma(Ts[k * SB_B + a], Cs[k * SB_B + c], v);
+    g.M[e] = v;
+  }
+  if (tid == 0) g.tick[NG] = 0u;
+}
+
 // Single-level panels: W = X - 1/2 Y M in place over X (m x 32 each, M 32 x
 // 32), so the trailing update is the rank-64 A22 -= Y W^T + W Y^T (K = 64
 // instead of the K = 96 form above, which folds Y S Y^T into the tiles).
@@ -905,91 +1059,6 @@ __global__ void sym_scatter_kernel(double *__restrict__ A, int64_t lda, int m, i
   }
 }
 
-// Single-level panels: M = T^T (Y^T X)  (32 x 32, K = m rows).  One
-// workgroup per 256 rows (wave w: rows 64w..64w+63 on FP64 MFMA), partials
-// summed in workgroup order by the last arriver (reduce.h hand-off).
-// rows per wave of ytx_m_kernel (a workgroup covers 4 YTX_RW rows); 32 rows
-// (m / 128 workgroups) measured 17.5 -> 23.2 us: the last arriver's partial
-// sum grows faster than the first phase shrinks
-constexpr int YTX_RW = 64;
-__global__ __launch_bounds__(256) void ytx_m_kernel(const double *__restrict__ Y,
-                                                    const double *__restrict__ X, int m,
-                                                    const double *__restrict__ T,
-                                                    double *__restrict__ M, double *part,
-                                                    unsigned *ticket) {
-  __shared__ double red[4][SB_B][SB_B + 1];
-  __shared__ double Ps[SB_B * SB_B];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, lr = lane >> 4, lc = lane & 15;
-  const int base = blockIdx.x * (4 * YTX_RW) + wid * YTX_RW;
-  doublex4 acc[2][2];
-#pragma unroll
-  for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) acc[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int g4 = 0; g4 < YTX_RW / 16; ++g4) {
-    double ya[4][2], xb[4][2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = base + 16 * g4 + 4 * q + lr, rc = min(r, m - 1);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        ya[q][h] = r < m ? Y[int64_t(rc) * SB_B + h * 16 + lc] : 0.0;
-        xb[q][h] = r < m ? X[int64_t(rc) * SB_B + h * 16 + lc] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          acc[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[q][ia], xb[q][cb], acc[ia][cb], 0, 0, 0);
-  }
-#pragma unroll
-  for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) red[wid][ia * 16 + lr + 4 * q][cb * 16 + lc] = acc[ia][cb][q];
-  __syncthreads();
-  for (int e = tid; e < SB_B * SB_B; e += 256) {
-    const int x = e >> 5, y = e & 31;
-    Ps[e] = (red[0][x][y] + red[1][x][y]) + (red[2][x][y] + red[3][x][y]);
-  }
-  __syncthreads();
-  if (!tg::publish_partials(Ps, SB_B * SB_B, part, ticket)) return;
-  const int G = int(gridDim.x);
-  {
-    // all of this thread's partials in flight at once (G <= 16 per batch)
-    double v[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int g0 = 0; g0 < G; g0 += 16) {
-      double t[4][16];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int b = 0; b < 16; ++b)
-          t[u][b] = tg::load_partial(&part[size_t(tid + 256 * u) * G + min(g0 + b, G - 1)]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int b = 0; b < 16; ++b) v[u] += (g0 + b < G) ? t[u][b] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) red[0][(tid + 256 * u) >> 5][(tid + 256 * u) & 31] = v[u];
-  }
-  __syncthreads();
-  for (int e = tid; e < SB_B * SB_B; e += 256) Ps[e] = T[e];  // T staged in LDS
-  __syncthreads();
-  for (int e = tid; e < SB_B * SB_B; e += 256) {
-    const int a = e >> 5, c = e & 31;
-    double v = 0.0;
-    for (int k = 0; k <= a; ++k) v = fma(Ps[k * SB_B + a], red[0][k][c], v);
-    M[e] = v;
-  }
-  if (tid == 0) *ticket = 0u;
-}
-
 // A[r0+i][p+l] = [R; 0] and the transpose (i < m, l < 32).
 __global__ void write_panel_kernel(double *__restrict__ A, int64_t lda, int p, int r0, int m,
                                    const double *__restrict__ R) {
@@ -1046,6 +1115,7 @@ static hipError_t side_stream(SideStream *&out) {
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
+  TG_CHK(hipMemsetAsync(b.xm_tick, 0, sizeof(unsigned) * xm_tick_words(n), st));
   const int np = int(pl.panels.size());
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
@@ -1054,15 +1124,15 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
     TG_CHK(panel_qr(st, A, lda, P.p, P.r0, P.m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    // X = A22 YT = sum over 256-row blocks z of A22[z, :]^T YT[z, :] (A22 symmetric)
-    const int nz = std::max(1, m / SB_C);
-    ChunkSpec cz{SB_C, nz, m, int64_t(lda), 0, SB_B, 0, 0, int64_t(m) * SB_B, m, SB_B, -1};
-    TG_CHK(dgemm_chunked(st, true, false, cz, 1.0, A22, lda, b.YT, SB_B, 0.0, b.U, SB_B));
-    TG_CHK(sum_partials(st, b.U, nz, m, SB_B, 1.0, 0.0, b.X, SB_B));
-    // M = T^T Y^T X
-    hipLaunchKernelGGL(ytx_m_kernel, dim3(cdiv(m, 4 * YTX_RW)), dim3(256), 0, st, Yp, b.X, m, Tp, b.M,
-                       b.pq_part, b.pq_ctl + 1);
-    TG_CHK(hipGetLastError());
+    // X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
+    {
+      const int G = cdiv(m, XR);
+      XmArgs xa{A22, int64_t(lda), m, b.YT, Yp, Tp, b.X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
+      const bool vec = (reinterpret_cast<uintptr_t>(A22) & 15) == 0 && (lda & 1) == 0;
+      if (vec) hipLaunchKernelGGL(xm_kernel<true>, dim3(G), dim3(64 * XW), 0, st, xa);
+      else hipLaunchKernelGGL(xm_kernel<false>, dim3(G), dim3(64 * XW), 0, st, xa);
+      TG_CHK(hipGetLastError());
+    }
     // W = X - Y M / 2 in place, then A22 -= Y W^T + W Y^T
     hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, b.X, m, b.M);
     TG_CHK(hipGetLastError());
