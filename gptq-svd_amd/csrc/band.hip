@@ -702,7 +702,10 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
 // bit-reproducible); the very last workgroup forms M.  Tickets: tick[0 ..
 // groups) and tick[groups], zero before the launch, reset by their last
 // arrivers.
-constexpr int XR = 16, XW = 8, XG = 16;
+#ifndef TG_XM_XW
+#define TG_XM_XW 8
+#endif
+constexpr int XR = 16, XW = TG_XM_XW, XG = 16;
 struct XmArgs {
   const double *A;  // A22, lda
   int64_t lda;
@@ -711,50 +714,61 @@ struct XmArgs {
   double *X, *part, *gpart, *M;
   unsigned *tick;
 };
-struct XmFrag {
-  double a[4], b[4][2];
-};
+constexpr int XDA = 6;  // A prefetch distance (K steps of 16); B (L2-resident YT) goes 2 ahead
+// Raw loads, no selects (a select right after a load waits for it): buffer
+// loads through a resource over the workgroup's rows, ending at their last
+// element (loads past it return 0), so the 16-B loads need no clamp; A values
+// outside the row block / K range are zeroed at use (xm_mma), which also
+// cancels whatever B holds there.  `rl` = row within the block (clamped).
 template <bool VEC>
-__device__ __forceinline__ void xm_load(const XmArgs &g, int row, int k0, int ke, XmFrag &f) {
-  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int kk = k0 + 4 * kq;
-  const bool rok = row < g.m;
-  const double *ar = g.A + int64_t(min(row, g.m - 1)) * g.lda;
-  if (VEC && kk + 3 < ke) {
-    const double2 lo = *reinterpret_cast<const double2 *>(ar + kk);
-    const double2 hi = *reinterpret_cast<const double2 *>(ar + kk + 2);
-    f.a[0] = rok ? lo.x : 0.0;
-    f.a[1] = rok ? lo.y : 0.0;
-    f.a[2] = rok ? hi.x : 0.0;
-    f.a[3] = rok ? hi.y : 0.0;
+__device__ __forceinline__ void xm_load_a(const XmArgs &g, __amdgpu_buffer_rsrc_t ra, int rl,
+                                          int k0, double (&fa)[4]) {
+  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  const int kk = k0 + 4 * ((threadIdx.x & 63) >> 4);
+  const int off = int((int64_t(rl) * g.lda + kk) * 8);
+  double v[4];
+  if (VEC) {
+    const u32x4v lo = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+    const u32x4v hi = __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0);
+    v[0] = __builtin_bit_cast(double, u32x2v{lo[0], lo[1]});
+    v[1] = __builtin_bit_cast(double, u32x2v{lo[2], lo[3]});
+    v[2] = __builtin_bit_cast(double, u32x2v{hi[0], hi[1]});
+    v[3] = __builtin_bit_cast(double, u32x2v{hi[2], hi[3]});
   } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const double v = ar[min(kk + s, g.m - 1)];
-      f.a[s] = (rok && kk + s < ke) ? v : 0.0;
-    }
+    for (int s = 0; s < 4; ++s)
+      v[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, off + 8 * s, 0, 0));
   }
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const double v = g.YT[int64_t(min(kk + s, g.m - 1)) * SB_B + 16 * j + r];
-      f.b[s][j] = kk + s < ke ? v : 0.0;
-    }
+  for (int s = 0; s < 4; ++s) fa[s] = v[s];
 }
-__device__ __forceinline__ void xm_mma(const XmFrag &f, doublex4 (&acc)[2]) {
+__device__ __forceinline__ void xm_load_b(const XmArgs &g, int k0, double (&fb)[4][2]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kk = k0 + 4 * (lane >> 4);
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[s], f.b[s][j], acc[j], 0, 0, 0);
+      fb[s][j] = g.YT[int64_t(min(kk + s, g.m - 1)) * SB_B + 16 * j + r];
+}
+__device__ __forceinline__ void xm_mma(const double (&fa)[4], const double (&fb)[4][2], bool rok,
+                                       int k0, int ke, doublex4 (&acc)[2]) {
+  const int kk = k0 + 4 * ((threadIdx.x & 63) >> 4);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const double a = (rok && kk + s < ke) ? fa[s] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[s][j], acc[j], 0, 0, 0);
+  }
 }
 template <bool VEC>
 __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
   __shared__ double red[XW][XR][SB_B + 1];  // the last workgroup reuses it for C, T
   __shared__ double xs[XR][SB_B + 1], ys[XR][SB_B + 1];
   __shared__ int s_last;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform K loop
   const int r0 = blockIdx.x * XR;
   const int G = int(gridDim.x), NG = (G + XG - 1) / XG;
   {
@@ -762,21 +776,44 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
     const int row = r0 + rr;
     ys[rr][c] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
   }
-  const int KQ = ((g.m + XW - 1) / XW + 15) / 16 * 16;
-  const int kb = wid * KQ, ke = min(g.m, kb + KQ);
+  // wave w takes the K steps w, w + XW, w + 2 XW, ... (16 columns each): at
+  // every moment the workgroup's waves read XW adjacent 128-B pieces of each
+  // of its rows, so every row streams in 1-KB runs (DRAM pages), where
+  // contiguous K ranges per wave made 8 x 16 scattered 128-B streams
+  const int kb = 16 * wid, KS = 16 * XW, ke = g.m;
   const int row = r0 + (lane & 15);
   doublex4 acc[2] = {doublex4{0.0, 0.0, 0.0, 0.0}, doublex4{0.0, 0.0, 0.0, 0.0}};
   if (kb < ke) {
-    XmFrag f0, f1, f2;
-    xm_load<VEC>(g, row, kb, ke, f0);
-    xm_load<VEC>(g, row, kb + 16, ke, f1);
-    for (int k0 = kb; k0 < ke; k0 += 48) {
-      xm_load<VEC>(g, row, k0 + 32, ke, f2);
-      xm_mma(f0, acc);
-      xm_load<VEC>(g, row, k0 + 48, ke, f0);
-      xm_mma(f1, acc);
-      xm_load<VEC>(g, row, k0 + 64, ke, f1);
-      xm_mma(f2, acc);
+    // K steps in a scalar loop of whole XDA-step rounds (steps past ke are
+    // zeroed at use); A fragments XDA steps ahead in a register ring, B
+    // fragments 2 ahead
+    const int nit = (ke - kb + KS - 1) / KS;
+    // the block's rows only: 32-bit offsets at any n (the whole A22 is 6.6 GB
+    // at n = 28,672)
+    const int nrow = min(XR, g.m - r0), rl = min(row, g.m - 1) - r0;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double *>(g.A + int64_t(r0) * g.lda), 0,
+        int((int64_t(nrow - 1) * g.lda + g.m) * 8), 0x00020000);
+    const bool rok = row < g.m;
+    double fa[XDA][4], fb[3][4][2];
+#pragma unroll
+    for (int u = 0; u < XDA; ++u) xm_load_a<VEC>(g, ra, rl, kb + KS * u, fa[u]);
+    xm_load_b(g, kb, fb[0]);
+    xm_load_b(g, kb + KS, fb[1]);
+    for (int it = 0; it < nit; it += XDA) {
+#pragma unroll
+      for (int u = 0; u < XDA; ++u) {
+        // scheduling barriers keep the issue order (B ahead, MFMAs, A
+        // ahead): the machine scheduler otherwise sinks the prefetches next
+        // to their uses and the in-order vmcnt then drains to 0 every step
+        const int k0 = kb + KS * (it + u);
+        xm_load_b(g, k0 + 2 * KS, fb[(u + 2) % 3]);
+        __builtin_amdgcn_sched_barrier(0);
+        xm_mma(fa[u], fb[u % 3], rok, k0, ke, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        xm_load_a<VEC>(g, ra, rl, k0 + KS * XDA, fa[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 #pragma unroll
