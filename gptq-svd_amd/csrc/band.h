@@ -71,7 +71,7 @@ size_t sb2st_t2_count(int n);
 
 // control words: 4 + 4 per panel, padded to a multiple of 16 bytes
 inline size_t pq_ctl_words(int n) { return 4 + 4 * size_t(std::max(1, n / SB_B + 1)); }
-// X / M kernel: one ticket per group of 16 row blocks of 16 rows, + 1
+// X / M kernel: one ticket per group of 32 row blocks of 16 rows, + 1
 inline size_t xm_tick_words(int n) { return size_t(n) / 256 + 8; }
 
 template <class A>

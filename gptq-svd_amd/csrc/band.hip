@@ -693,19 +693,15 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
 // 32 x 32 products Y_zᵀ X_z of the blocks reduced on the way to
 // M = Tᵀ (Yᵀ X) -- replaces the split-K GEMM over 256-row blocks of A22ᵀ,
 // its partial sum and the separate M reduction (three launches).
-// One workgroup per XR rows, XW waves splitting K: wave w streams its
-// K / XW columns of the XR rows (lane (r, kq) reads 4 consecutive k of row r,
-// so every row's 128 B come in one instruction) two iterations ahead and
-// accumulates a 16 x 32 tile on FP64 MFMA; the XW tiles are summed in wave
-// order.  Yᵀ X partials: per workgroup, then per group of XG workgroups by
-// its last arriver, then over the groups by the last group (fixed orders:
-// bit-reproducible); the very last workgroup forms M.  Tickets: tick[0 ..
+// One workgroup per XR rows of X, XW waves splitting K (interleaved steps),
+// each accumulating a 16 x 32 tile on FP64 MFMA with XDA steps of loads in
+// flight; the XW tiles are summed in wave order.  Yᵀ X partials: per
+// workgroup, then per group of XG workgroups by its last arriver, then (more
+// than one group) over the groups by the last group -- fixed orders, so the
+// sums are bit-reproducible; the last arriver forms M.  Tickets: tick[0 ..
 // groups) and tick[groups], zero before the launch, reset by their last
 // arrivers.
-#ifndef TG_XM_XW
-#define TG_XM_XW 8
-#endif
-constexpr int XR = 16, XW = TG_XM_XW, XG = 16;
+constexpr int XR = 16, XW = 8, XG = 32;
 struct XmArgs {
   const double *A;  // A22, lda
   int64_t lda;
@@ -714,55 +710,53 @@ struct XmArgs {
   double *X, *part, *gpart, *M;
   unsigned *tick;
 };
-constexpr int XDA = 6;  // A prefetch distance (K steps of 16); B (L2-resident YT) goes 2 ahead
-// Raw loads, no selects (a select right after a load waits for it): buffer
-// loads through a resource over the workgroup's rows, ending at their last
-// element (loads past it return 0), so the 16-B loads need no clamp; A values
-// outside the row block / K range are zeroed at use (xm_mma), which also
-// cancels whatever B holds there.  `rl` = row within the block (clamped).
-template <bool VEC>
-__device__ __forceinline__ void xm_load_a(const XmArgs &g, __amdgpu_buffer_rsrc_t ra, int rl,
-                                          int k0, double (&fa)[4]) {
-  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-  const int kk = k0 + 4 * ((threadIdx.x & 63) >> 4);
-  const int off = int((int64_t(rl) * g.lda + kk) * 8);
-  double v[4];
-  if (VEC) {
-    const u32x4v lo = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
-    const u32x4v hi = __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0);
-    v[0] = __builtin_bit_cast(double, u32x2v{lo[0], lo[1]});
-    v[1] = __builtin_bit_cast(double, u32x2v{lo[2], lo[3]});
-    v[2] = __builtin_bit_cast(double, u32x2v{hi[0], hi[1]});
-    v[3] = __builtin_bit_cast(double, u32x2v{hi[2], hi[3]});
-  } else {
+// The product is formed transposed, Xᵀ[:, j-block] = YTᵀ · A22[:, j-block]
+// (A22 symmetric): the MFMA B operand is then 4 rows x 16 consecutive
+// columns of A22, so lane l reads A22[k + l/16][j0 + l%16] and every load
+// instruction covers four whole 128-B lines (the row-block form, A operand =
+// 16 rows x 4 k, touched sixteen half-used lines per instruction and
+// streamed at ~8 GB/s per CU).  The A operand is YTᵀ: lane l reads
+// YT[k + l/16][16 i + l%16], 128 B of an L2-resident row.  All workgroups
+// sweep K in the same order, so at any moment they read neighbouring strips
+// of the same rows of A22.
+#ifndef TG_XM_XDA
+#define TG_XM_XDA 8
+#endif
+constexpr int XDA = TG_XM_XDA;  // K steps (4 rows of A22 each) loaded per round per wave
+struct XmStep {
+  double b, a[2];
+};
+__device__ __forceinline__ void xm_load(const XmArgs &g, int col, int k0, XmStep &f) {
+  const int lane = threadIdx.x & 63;
+  const int k = min(k0 + (lane >> 4), g.m - 1);
+  f.b = g.A[int64_t(k) * g.lda + col];
+  f.a[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
+  f.a[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
+}
+__device__ __forceinline__ void xm_mma(const XmStep &f, bool cok, int k0, doublex4 (&acc)[2],
+                                       int m) {
+  const double b = (cok && k0 + ((threadIdx.x & 63) >> 4) < m) ? f.b : 0.0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      v[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ra, off + 8 * s, 0, 0));
+  for (int i = 0; i < 2; ++i)
+    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i], b, acc[i], 0, 0, 0);
+}
+// sum over z in [z0, z1) of p[z * 1024 + e], in z order, with the L1-
+// bypassing loads of a batch all in flight before the first add
+__device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e) {
+  constexpr int NB = 8;
+  double s = 0.0;
+  for (int zb = z0; zb < z1; zb += NB) {
+    double v[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      v[u] = tg::load_partial(&p[size_t(min(zb + u, z1 - 1)) * 1024 + e]);
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (zb + u < z1) s += v[u];
   }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) fa[s] = v[s];
+  return s;
 }
-__device__ __forceinline__ void xm_load_b(const XmArgs &g, int k0, double (&fb)[4][2]) {
-  const int lane = threadIdx.x & 63, r = lane & 15, kk = k0 + 4 * (lane >> 4);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      fb[s][j] = g.YT[int64_t(min(kk + s, g.m - 1)) * SB_B + 16 * j + r];
-}
-__device__ __forceinline__ void xm_mma(const double (&fa)[4], const double (&fb)[4][2], bool rok,
-                                       int k0, int ke, doublex4 (&acc)[2]) {
-  const int kk = k0 + 4 * ((threadIdx.x & 63) >> 4);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const double a = (rok && kk + s < ke) ? fa[s] : 0.0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[s][j], acc[j], 0, 0, 0);
-  }
-}
-template <bool VEC>
+
 __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
   __shared__ double red[XW][XR][SB_B + 1];  // the last workgroup reuses it for C, T
   __shared__ double xs[XR][SB_B + 1], ys[XR][SB_B + 1];
@@ -776,50 +770,37 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
     const int row = r0 + rr;
     ys[rr][c] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
   }
-  // wave w takes the K steps w, w + XW, w + 2 XW, ... (16 columns each): at
-  // every moment the workgroup's waves read XW adjacent 128-B pieces of each
-  // of its rows, so every row streams in 1-KB runs (DRAM pages), where
-  // contiguous K ranges per wave made 8 x 16 scattered 128-B streams
-  const int kb = 16 * wid, KS = 16 * XW, ke = g.m;
-  const int row = r0 + (lane & 15);
+  // wave w takes the K steps w, w + XW, ... (4 rows of A22 each)
+  const int KS = 4 * XW, kb = 4 * wid;
+  const int col = r0 + (lane & 15);
+  const bool cok = col < g.m;
+  const int colc = min(col, g.m - 1);
   doublex4 acc[2] = {doublex4{0.0, 0.0, 0.0, 0.0}, doublex4{0.0, 0.0, 0.0, 0.0}};
-  if (kb < ke) {
-    // K steps in a scalar loop of whole XDA-step rounds (steps past ke are
-    // zeroed at use); A fragments XDA steps ahead in a register ring, B
-    // fragments 2 ahead
-    const int nit = (ke - kb + KS - 1) / KS;
-    // the block's rows only: 32-bit offsets at any n (the whole A22 is 6.6 GB
-    // at n = 28,672)
-    const int nrow = min(XR, g.m - r0), rl = min(row, g.m - 1) - r0;
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<double *>(g.A + int64_t(r0) * g.lda), 0,
-        int((int64_t(nrow - 1) * g.lda + g.m) * 8), 0x00020000);
-    const bool rok = row < g.m;
-    double fa[XDA][4], fb[3][4][2];
+  if (kb < g.m) {
+    const int nit = (g.m - kb + KS - 1) / KS;
+    XmStep f[XDA];
 #pragma unroll
-    for (int u = 0; u < XDA; ++u) xm_load_a<VEC>(g, ra, rl, kb + KS * u, fa[u]);
-    xm_load_b(g, kb, fb[0]);
-    xm_load_b(g, kb + KS, fb[1]);
+    for (int u = 0; u < XDA; ++u) xm_load(g, colc, kb + KS * u, f[u]);
     for (int it = 0; it < nit; it += XDA) {
 #pragma unroll
       for (int u = 0; u < XDA; ++u) {
-        // scheduling barriers keep the issue order (B ahead, MFMAs, A
-        // ahead): the machine scheduler otherwise sinks the prefetches next
-        // to their uses and the in-order vmcnt then drains to 0 every step
+        // scheduling barriers keep the issue order (MFMAs on step it + u,
+        // then the load of step it + u + XDA into the freed slot): the
+        // machine scheduler otherwise sinks prefetches next to their uses
+        // and the in-order vmcnt drains to 0 every step
         const int k0 = kb + KS * (it + u);
-        xm_load_b(g, k0 + 2 * KS, fb[(u + 2) % 3]);
+        xm_mma(f[u], cok, k0, acc, g.m);
         __builtin_amdgcn_sched_barrier(0);
-        xm_mma(fa[u], fb[u % 3], rok, k0, ke, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        xm_load_a<VEC>(g, ra, rl, k0 + KS * XDA, fa[u]);
+        xm_load(g, colc, k0 + KS * XDA, f[u]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
+  // acc[i][q] = Xᵀ[16 i + lane / 16 + 4 q][r0 + lane % 16] = X[r0 + lane % 16][...]
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red[wid][(lane >> 4) + 4 * q][16 * j + (lane & 15)] = acc[j][q];
+    for (int q = 0; q < 4; ++q) red[wid][lane & 15][16 * i + (lane >> 4) + 4 * q] = acc[i][q];
   __syncthreads();
   {
     const int rr = tid >> 5, c = tid & 31;
@@ -847,28 +828,28 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
              unsigned(z1 - z0 - 1);
   __syncthreads();
   if (!s_last) return;
-  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
-    double s = 0.0;
-    for (int z = z0; z < z1; ++z) s += tg::load_partial(&g.part[size_t(z) * 1024 + e]);
-    __hip_atomic_store(&g.gpart[size_t(grp) * 1024 + e], s, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    g.tick[grp] = 0u;
-    s_last = __hip_atomic_fetch_add(&g.tick[NG], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             unsigned(NG - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
   double *Cs = &red[0][0][0], *Ts = Cs + SB_B * SB_B;
   static_assert(XW * XR * (SB_B + 1) >= 2 * SB_B * SB_B, "C and T fit in red");
   for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
-    double s = 0.0;
-    for (int q = 0; q < NG; ++q) s += tg::load_partial(&g.gpart[size_t(q) * 1024 + e]);
-    Cs[e] = s;
+    const double s = xm_sum(g.part, z0, z1, e);
+    if (NG == 1)
+      Cs[e] = s;  // one group: its last arriver forms M (no second hand-off)
+    else
+      __hip_atomic_store(&g.gpart[size_t(grp) * 1024 + e], s, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     Ts[e] = g.T[e];
+  }
+  if (NG > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      g.tick[grp] = 0u;
+      s_last = __hip_atomic_fetch_add(&g.tick[NG], 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == unsigned(NG - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int e = tid; e < SB_B * SB_B; e += 64 * XW) Cs[e] = xm_sum(g.gpart, 0, NG, e);
   }
   __syncthreads();
   for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
@@ -877,7 +858,10 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
     for (int k = 0; k <= a; ++k) v = fma(Ts[k * SB_B + a], Cs[k * SB_B + c], v);
     g.M[e] = v;
   }
-  if (tid == 0) g.tick[NG] = 0u;
+  if (tid == 0) {
+    g.tick[grp] = 0u;
+    if (NG > 1) g.tick[NG] = 0u;
+  }
 }
 
 // Single-level panels: W = X - 1/2 Y M in place over X (m x 32 each, M 32 x
@@ -1165,9 +1149,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     {
       const int G = cdiv(m, XR);
       XmArgs xa{A22, int64_t(lda), m, b.YT, Yp, Tp, b.X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
-      const bool vec = (reinterpret_cast<uintptr_t>(A22) & 15) == 0 && (lda & 1) == 0;
-      if (vec) hipLaunchKernelGGL(xm_kernel<true>, dim3(G), dim3(64 * XW), 0, st, xa);
-      else hipLaunchKernelGGL(xm_kernel<false>, dim3(G), dim3(64 * XW), 0, st, xa);
+      hipLaunchKernelGGL(xm_kernel, dim3(G), dim3(64 * XW), 0, st, xa);
       TG_CHK(hipGetLastError());
     }
     // W = X - Y M / 2 in place, then A22 -= Y W^T + W Y^T
