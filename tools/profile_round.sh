@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profile: kernel trace + stats over bench.py, then one PMC pass per
-# counter (FETCH_SIZE, WRITE_SIZE) on the bulge chase and the two HBM-bound
-# band-reduction kernels, then the per-class traffic JSON, then the default
+# counter (FETCH_SIZE, WRITE_SIZE) on the bulge chase and the two streaming
+# band-reduction kernels (X/M and the rank-64 update), then the per-class traffic JSON, then the default
 # bench line (with the CPU baseline).  Every GPU step has its own limit and
 # the steps are chained, so the first failure ends the script.
 # usage: tools/profile_round.sh OUTDIR [KERNEL_REGEX]
@@ -9,7 +9,7 @@ set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/${1:-gpurun_out/prof}
-KRE=${2:-bulge_lds_kernel|syr2k_bs_kernel|dgemm_chunked_kernel<64, 32, true, false>}
+KRE=${2:-bulge_lds_kernel|syr2k_w_kernel|xm_kernel}
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
@@ -24,7 +24,6 @@ STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | sort | sed -n 1p)
 FC=$(find "$OUT/pmc_FETCH_SIZE" -name '*counter_collection.csv' | sort | sed -n 1p)
 WC=$(find "$OUT/pmc_WRITE_SIZE" -name '*counter_collection.csv' | sort | sed -n 1p)
 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$FC" "$WC" "$STATS" \
-  bulge_chase=bulge_lds_kernel band_update=syr2k_bs_kernel \
-  "band_x_gemm=dgemm_chunked_kernel<64, 32, true, false>"
+  bulge_chase=bulge_lds_kernel band_update=syr2k_w_kernel band_xm=xm_kernel
 timeout -k 10 600 python3 bench.py > "$OUT/bench.log" 2>&1
 tail -1 "$OUT/bench.log"
