@@ -719,10 +719,7 @@ struct XmArgs {
 // YT[k + l/16][16 i + l%16], 128 B of an L2-resident row.  All workgroups
 // sweep K in the same order, so at any moment they read neighbouring strips
 // of the same rows of A22.
-#ifndef TG_XM_XDA
-#define TG_XM_XDA 8
-#endif
-constexpr int XDA = TG_XM_XDA;  // K steps (4 rows of A22 each) loaded per round per wave
+constexpr int XDA = 8;  // K steps (4 rows of A22 each) loaded per round per wave
 struct XmStep {
   double b, a[2];
 };
