@@ -73,6 +73,8 @@ def parse():
                    help="sample every k-th launch of each kernel class with HIP events")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-syrk", action="store_true")
+    p.add_argument("--no-large-n", action="store_true",
+                   help="skip the n = 12288 / 14336 solve timings in the extras")
     return p.parse_args()
 
 
@@ -182,6 +184,42 @@ def syrk_bench(g, args, device):
                             tflops_algorithmic=round(2.0 * N * n * n / dt / 1e12, 2))
         del X
     return res
+
+
+def large_n(g, args, device):
+    """The real models' down_proj widths (Qwen3-8B n = 12288, Llama-3-8B
+    n = 14336): process_hessian_alt + quantize on a synthetic H of 3n/4
+    calibration rows (as tests/test_gpu_fullsize.py), one warm-up solve and
+    one timed, with phases; at n = 12288 also the TSQR band reduction
+    (TG_SB_TSQR=1, the round-1 path these widths took before) for the
+    eigenvalue phase it changes."""
+    import copy
+    out = {}
+    for n in (12288, 14336):
+        torch.manual_seed(1)
+        acc = g.HessianAccumulator(n, device)
+        acc.add_batch(torch.randn(3 * n // 4, n, device=device).half())
+        H = acc.get_hessian()
+        del acc
+        a2 = copy.copy(args)
+        a2.n, a2.m = n, 4096
+        W = torch.randn(a2.m, n, device=device)
+        phases(g, H, W, a2)
+        ph, k = phases(g, H, W, a2)
+        ent = dict(rank_k=k, path=phases.path, solve_ms=round(sum(ph.values()), 3), phases_ms=ph)
+        if n == 12288:
+            os.environ["TG_SB_TSQR"] = "1"
+            try:
+                phases(g, H, W, a2)
+                ph2, _ = phases(g, H, W, a2)
+            finally:
+                del os.environ["TG_SB_TSQR"]
+            ent["tsqr_band_reduction"] = dict(solve_ms=round(sum(ph2.values()), 3),
+                                              eigh_values_ms=ph2["eigh_values"])
+        out[f"n{n}"] = ent
+        del H, W
+        torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(H, W, args):
@@ -400,6 +438,8 @@ def run(args):
             extra["pmc_hbm"] = pm
         if not args.no_syrk:
             extra["syrk"] = syrk_bench(g, args, device)
+        if not args.no_large_n and (args.n, args.m) == (4096, 4096):
+            extra["large_n"] = large_n(g, args, device)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(H, W, args)

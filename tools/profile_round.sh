@@ -13,11 +13,11 @@ KRE=${2:-bulge_lds_kernel|syr2k_w_kernel|xm_kernel}
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/trace_bench.log" 2>&1
+  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-large-n > "$OUT/trace_bench.log" 2>&1
 echo "trace done"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "$KRE" -f csv -d "$OUT/pmc_$C" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-syrk > "$OUT/pmc_$C.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-syrk --no-large-n > "$OUT/pmc_$C.log" 2>&1
   echo "pmc $C done"
 done
 STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | sort | sed -n 1p)
