@@ -720,22 +720,36 @@ struct XmArgs {
 // sweep K in the same order, so at any moment they read neighbouring strips
 // of the same rows of A22.
 constexpr int XDA = 8;  // K steps (4 rows of A22 each) loaded per round per wave
+// NBC 16-column blocks per workgroup (XR = 16 NBC rows of X): the YT
+// fragments of a step feed all NBC blocks, so YT's L2 -> CU traffic is
+// 16 m^2 / NBC bytes per panel against A22's 8 m^2.  NBC = 2 once the grid
+// still covers the chip (m >= XM_WIDE).
+constexpr int XM_WIDE = 6144;
+template <int NBC>
 struct XmStep {
-  double b, a[2];
+  double b[NBC], a[2];
 };
-__device__ __forceinline__ void xm_load(const XmArgs &g, int col, int k0, XmStep &f) {
+template <int NBC>
+__device__ __forceinline__ void xm_load(const XmArgs &g, const int (&col)[NBC], int k0,
+                                        XmStep<NBC> &f) {
   const int lane = threadIdx.x & 63;
   const int k = min(k0 + (lane >> 4), g.m - 1);
-  f.b = g.A[int64_t(k) * g.lda + col];
+#pragma unroll
+  for (int c = 0; c < NBC; ++c) f.b[c] = g.A[int64_t(k) * g.lda + col[c]];
   f.a[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
   f.a[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
 }
-__device__ __forceinline__ void xm_mma(const XmStep &f, bool cok, int k0, doublex4 (&acc)[2],
-                                       int m) {
-  const double b = (cok && k0 + ((threadIdx.x & 63) >> 4) < m) ? f.b : 0.0;
+template <int NBC>
+__device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[NBC], int k0,
+                                       doublex4 (&acc)[NBC][2], int m) {
+  const bool kok = k0 + ((threadIdx.x & 63) >> 4) < m;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i], b, acc[i], 0, 0, 0);
+  for (int c = 0; c < NBC; ++c) {
+    const double b = (cok[c] && kok) ? f.b[c] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      acc[c][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i], b, acc[c][i], 0, 0, 0);
+  }
 }
 // sum over z in [z0, z1) of p[z * 1024 + e], in z order, with the L1-
 // bypassing loads of a batch all in flight before the first add
@@ -754,53 +768,68 @@ __device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e)
   return s;
 }
 
+template <int NBC>
 __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
-  __shared__ double red[XW][XR][SB_B + 1];  // the last workgroup reuses it for C, T
-  __shared__ double xs[XR][SB_B + 1], ys[XR][SB_B + 1];
+  constexpr int RB = XR * NBC;                // rows of X per workgroup
+  __shared__ double red[XW][RB][SB_B + 1];   // the last workgroup reuses it for C, T
+  __shared__ double xs[RB][SB_B + 1], ys[RB][SB_B + 1];
   __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform K loop
-  const int r0 = blockIdx.x * XR;
+  const int r0 = blockIdx.x * RB;
   const int G = int(gridDim.x), NG = (G + XG - 1) / XG;
-  {
-    const int rr = tid >> 5, c = tid & 31;  // XR x 32 = 512 = blockDim
-    const int row = r0 + rr;
+  for (int e = tid; e < RB * SB_B; e += 64 * XW) {
+    const int rr = e >> 5, c = e & 31, row = r0 + rr;
     ys[rr][c] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
   }
   // wave w takes the K steps w, w + XW, ... (4 rows of A22 each)
   const int KS = 4 * XW, kb = 4 * wid;
-  const int col = r0 + (lane & 15);
-  const bool cok = col < g.m;
-  const int colc = min(col, g.m - 1);
-  doublex4 acc[2] = {doublex4{0.0, 0.0, 0.0, 0.0}, doublex4{0.0, 0.0, 0.0, 0.0}};
+  int colc[NBC];
+  bool cok[NBC];
+#pragma unroll
+  for (int c = 0; c < NBC; ++c) {
+    const int col = r0 + 16 * c + (lane & 15);
+    cok[c] = col < g.m;
+    colc[c] = min(col, g.m - 1);
+  }
+  doublex4 acc[NBC][2];
+#pragma unroll
+  for (int c = 0; c < NBC; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[c][i] = doublex4{0.0, 0.0, 0.0, 0.0};
   if (kb < g.m) {
     const int nit = (g.m - kb + KS - 1) / KS;
-    XmStep f[XDA];
+    XmStep<NBC> f[XDA];
 #pragma unroll
-    for (int u = 0; u < XDA; ++u) xm_load(g, colc, kb + KS * u, f[u]);
+    for (int u = 0; u < XDA; ++u) xm_load<NBC>(g, colc, kb + KS * u, f[u]);
+    // (the compiler drains vmcnt to 0 at the loop header -- the slots are
+    // loop-carried -- and waits only for the slot in use inside the body;
+    // unrolling 4 or 8 rounds per iteration measured no faster)
     for (int it = 0; it < nit; it += XDA) {
 #pragma unroll
       for (int u = 0; u < XDA; ++u) {
         // scheduling barriers keep the issue order (MFMAs on step it + u,
         // then the load of step it + u + XDA into the freed slot): the
         // machine scheduler otherwise sinks prefetches next to their uses
-        // and the in-order vmcnt drains to 0 every step
         const int k0 = kb + KS * (it + u);
-        xm_mma(f[u], cok, k0, acc, g.m);
+        xm_mma<NBC>(f[u], cok, k0, acc, g.m);
         __builtin_amdgcn_sched_barrier(0);
-        xm_load(g, colc, k0 + KS * XDA, f[u]);
+        xm_load<NBC>(g, colc, k0 + KS * XDA, f[u]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
-  // acc[i][q] = Xᵀ[16 i + lane / 16 + 4 q][r0 + lane % 16] = X[r0 + lane % 16][...]
+  // acc[c][i][q] = Xᵀ[16 i + lane / 16 + 4 q][r0 + 16 c + lane % 16]
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int c = 0; c < NBC; ++c)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red[wid][lane & 15][16 * i + (lane >> 4) + 4 * q] = acc[i][q];
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        red[wid][16 * c + (lane & 15)][16 * i + (lane >> 4) + 4 * q] = acc[c][i][q];
   __syncthreads();
-  {
-    const int rr = tid >> 5, c = tid & 31;
+  for (int e = tid; e < RB * SB_B; e += 64 * XW) {
+    const int rr = e >> 5, c = e & 31;
     double x = 0.0;
 #pragma unroll
     for (int w = 0; w < XW; ++w) x += red[w][rr][c];
@@ -813,7 +842,7 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
     const int a = e >> 5, c = e & 31;
     double p = 0.0;
 #pragma unroll
-    for (int rr = 0; rr < XR; ++rr) p = fma(ys[rr][a], xs[rr][c], p);
+    for (int rr = 0; rr < RB; ++rr) p = fma(ys[rr][a], xs[rr][c], p);
     __hip_atomic_store(&g.part[size_t(blockIdx.x) * 1024 + e], p, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1144,9 +1173,12 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
     // X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
     {
-      const int G = cdiv(m, XR);
+      const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
+      const int nbc = fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
+      const int G = cdiv(m, XR * nbc);
       XmArgs xa{A22, int64_t(lda), m, b.YT, Yp, Tp, b.X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
-      hipLaunchKernelGGL(xm_kernel, dim3(G), dim3(64 * XW), 0, st, xa);
+      if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
+      else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
       TG_CHK(hipGetLastError());
     }
     // W = X - Y M / 2 in place, then A22 -= Y W^T + W Y^T
