@@ -4,7 +4,7 @@
 * default: one compact-WY block per panel from CholeskyQR2 + Householder
   reconstruction (falls back per panel when the Gram matrix cannot certify Q);
 * TG_PQR_FALLBACK=1: every panel through the in-kernel grid Householder path;
-* TG_SB_TSQR=1: the TSQR tree of 256-row leaves (the large-n path).
+* TG_SB_TSQR=1: the TSQR tree of 256-row leaves (also the path past n = 65,536).
 
 Inputs cover a Wishart matrix, a graded spectrum (1e-10 .. 1), a rank-deficient
 X^T X (N < n: the late panels are numerically zero) and a block-diagonal

@@ -45,7 +45,10 @@ def rel(a, b):
     {"TG_BT_MULTI": "1"},
     {"TG_URX_TWOCHOL": "1"},
     {"TG_NO_ROCBLAS": "1"},
-], ids=lambda d: "+".join(d))
+    {"TG_NO_ROCBLAS": "1", "TG_GEMM_TILE": "128"},
+    {"TG_NO_ROCBLAS": "1", "TG_GEMM_TILE": "12864"},
+    {"TG_XM_NBC": "2"},
+], ids=lambda d: "+".join(f"{k}={v}" for k, v in d.items()))
 def test_switch_matches_default(problem, path, switches, monkeypatch):
     g, H, W = problem
     monkeypatch.setenv("TG_SPECTRAL_PATH", path)
