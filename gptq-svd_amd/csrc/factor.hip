@@ -2064,7 +2064,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
     TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr, sizeof(double) * k,
                             k, hipMemcpyDeviceToDevice, st));         // Z^T = R11 (+ ...)
     if (m > 0) {
-      TG_HIP(tg::dgemm(st, false, false, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
+      TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
       TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));  // + R12 C^T
     }
     TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));           // N = Z Z^T
@@ -2088,7 +2088,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
     hipLaunchKernelGGL(flip_transpose_kernel, gk, dim3(256), 0, st, Yr, k, U, int64_t(ldu));
     TG_LAUNCHED();                                                    // U11 = V^-1 = J R^-T J
     if (m > 0)
-      TG_HIP(tg::dgemm(st, false, false, k, m, k, 1.0, U, ldu, C, m, 0.0, U + k, ldu));  // V^-1 C
+      TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, U, ldu, C, m, 0.0, U + k, ldu));  // V^-1 C
     return 0;
   }
   CholStat h{};

@@ -8,6 +8,11 @@
 
 namespace tg {
 // C = alpha * op(A) op(B) + beta * C, row-major; op(A) is M x K, op(B) is K x N.
+// C = alpha A B + beta C, A (M x K) upper triangular row-major (zeros below
+// the diagonal are not read); own FP64 MFMA kernel.
+hipError_t dgemm_upper_a(hipStream_t st, int M, int N, int K, double alpha, const double *A,
+                         int64_t lda, const double *B, int64_t ldb, double beta, double *C,
+                         int64_t ldc);
 hipError_t dgemm(hipStream_t st, bool transA, bool transB, int M, int N, int K, double alpha,
                  const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                  double *C, int64_t ldc);

@@ -183,7 +183,10 @@ __device__ inline void epilogue(const doublex4 (&acc)[BM / 32][BN / 32], double 
 
 // 128 x 128 tiles: two workgroups per CU (LDS 2 x 74 KB) need <= 256
 // registers per lane (128 accumulators + the loop's operands and staging)
-template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK, bool MIRROR = true>
+// UPA: op(A) = A is upper triangular (row-major, A[i][c] = 0 for c < i), so
+// the tile of rows tm.. only needs K from tm (rounded down to the slab).
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool SYRK, bool MIRROR = true,
+          bool UPA = false>
 __global__ __launch_bounds__(256, BM >= 128 ? 2 : 3) void dgemm_kernel(int M, int N, int K, double alpha,
                                                     const TA_ *__restrict__ A, int64_t lda,
                                                     const TB_ *__restrict__ B, int64_t ldb,
@@ -213,8 +216,9 @@ __global__ __launch_bounds__(256, BM >= 128 ? 2 : 3) void dgemm_kernel(int M, in
     for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
 
   // split-K: workgroup z covers k in [kb, ke) and writes C + z * zstride
-  const int kb = blockIdx.z * kchunk;
+  int kb = blockIdx.z * kchunk;
   const int ke = min(K, kb + kchunk);
+  if (UPA) kb = max(kb, (tm / KC) * KC);
   C += int64_t(blockIdx.z) * zstride;
   mainloop<TA_, TB_, BM, BN, TA, TB>(A, lda, B, ldb, M, N, kb, ke, tm, tn, As, Bs, acc);
   epilogue<BM, BN, SYRK, MIRROR>(acc, alpha, beta, C, ldc, M, N, tm, tn);
@@ -252,15 +256,15 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
   epilogue<BM, BN, false>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
-template <class TA_, class TB_, int BM, int BN, bool TA, bool TB>
+template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool UPA = false>
 hipError_t launch(hipStream_t st, int M, int N, int K, double alpha, const TA_ *A, int64_t lda,
                   const TB_ *B, int64_t ldb, double beta, double *C, int64_t ldc, int splits,
                   int64_t zstride) {
   const int kchunk = splits > 1 ? ((tg::cdiv(K, splits) + KC - 1) / KC) * KC : (K > 0 ? K : 1);
   const int nz = splits > 1 ? tg::cdiv(K, kchunk) : 1;
   dim3 grid(tg::cdiv(N, BN), tg::cdiv(M, BM), nz);
-  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, TA, TB, false>), grid, dim3(256), 0, st, M,
-                     N, K, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, zstride);
+  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, TA, TB, false, true, UPA>), grid, dim3(256), 0,
+                     st, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, zstride);
   return hipGetLastError();
 }
 
@@ -382,6 +386,21 @@ hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double a
   return dispatch_t<double, double, 64, 64>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C,
                                             ldc);
 }
+// C = alpha A B + beta C with A (M x K, M <= K) upper triangular: the
+// triangle's zeros are skipped per tile (half the flops of a square A).  The
+// tiles' work then falls with the row, so the grid is ordered with the
+// heaviest rows first (blockIdx.y = 0 is the top tile row).
+hipError_t dgemm_upper_a(hipStream_t st, int M, int N, int K, double alpha, const double *A,
+                         int64_t lda, const double *B, int64_t ldb, double beta, double *C,
+                         int64_t ldc) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (gemm_tile(M, N) == 128)
+    return launch<double, double, 128, 128, false, false, true>(st, M, N, K, alpha, A, lda, B, ldb,
+                                                                beta, C, ldc, 1, 0);
+  return launch<double, double, 64, 64, false, false, true>(st, M, N, K, alpha, A, lda, B, ldb,
+                                                            beta, C, ldc, 1, 0);
+}
+
 hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, double alpha,
                          const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                          double *C, int64_t ldc) {
@@ -456,9 +475,18 @@ hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, d
 }
 
 // C = alpha * X^T X + beta * C on lower tiles, mirrored (X is K x n, ld ldx).
+// 128 x 128 tiles (two workgroups per CU, the most work per staged byte)
+// once there are enough of them for several full rounds.
 hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc) {
   if (n <= 0) return hipSuccess;
+  const int n128 = cdiv(n, 128);
+  if (n128 * (n128 + 1) / 2 >= 1024) {
+    hipLaunchKernelGGL((dgemm_kernel<double, double, 128, 128, true, false, true>),
+                       dim3(n128 * (n128 + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X,
+                       ldx, beta, C, ldc, K > 0 ? K : 1, int64_t(0));
+    return hipGetLastError();
+  }
   constexpr int BT = 64;
   const int nt = cdiv(n, BT);
   hipLaunchKernelGGL((dgemm_kernel<double, double, BT, BT, true, false, true>),
