@@ -1457,8 +1457,9 @@ __global__ __launch_bounds__(256) void trinv_diag_kernel(const double *__restric
 // already in Y, everything below the diagonal is zero).  Bottom-up: at block
 // size b = NU, 2NU, ... each pair of adjacent solved blocks merges with
 // Y12 = -(Y11 U12) Y22.  All full-size pairs of a level are independent and
-// go out as two batched GEMMs; a pair whose second block is the ragged tail
-// gets two plain GEMMs.  T holds >= n*n/4 doubles.
+// go out as two batched GEMMs, which skip the zero triangles of Y11 and Y22
+// (half their flops); a pair whose second block is the ragged tail gets two
+// plain GEMMs.  T holds >= n*n/4 doubles.
 hipError_t trinv_offdiag(hipStream_t st, const double *U, int ldu, double *Y, int ldy, int n,
                          double *T) {
   for (int b = NU; b < n; b *= 2) {
@@ -1469,11 +1470,11 @@ hipError_t trinv_offdiag(hipStream_t st, const double *U, int ldu, double *Y, in
     if (nfull > 0) {
       const int64_t bb = int64_t(b) * b, dy = int64_t(ldy) + 1, du = int64_t(ldu) + 1;
       const tg::ChunkSpec c1{2 * b, nfull, 2 * b * nfull, dy, 0, du, 0, 0, bb, b, b, b};
-      e = tg::dgemm_chunked(st, false, false, c1, 1.0, Y, ldy, U + b, ldu, 0.0, T, b);
+      e = tg::dgemm_chunked(st, false, false, c1, 1.0, Y, ldy, U + b, ldu, 0.0, T, b, 1);
       if (e != hipSuccess) return e;
       const tg::ChunkSpec c2{2 * b, nfull, 2 * b * nfull, 0, bb, dy, 0, dy, 0, b, b, b};
       e = tg::dgemm_chunked(st, false, false, c2, -1.0, T, b, Y + size_t(b) * ldy + b, ldy, 0.0,
-                            Y + b, ldy);
+                            Y + b, ldy, 2);
       if (e != hipSuccess) return e;
     }
     if (ragged) {

@@ -42,7 +42,9 @@ struct ChunkSpec {
   int64_t a_kb, a_z, b_kb, b_z, c_kb, c_z;
   int M, N, K;
 };
+// tri = 1: every chunk's A is upper triangular, 2: every chunk's B (the
+// zero triangle is skipped per tile; no transposes then).
 hipError_t dgemm_chunked(hipStream_t st, bool transA, bool transB, const ChunkSpec &cs,
                          double alpha, const double *A, int64_t lda, const double *B,
-                         int64_t ldb, double beta, double *C, int64_t ldc);
+                         int64_t ldb, double beta, double *C, int64_t ldc, int tri = 0);
 }  // namespace tg

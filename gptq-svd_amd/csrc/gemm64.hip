@@ -225,7 +225,9 @@ __global__ __launch_bounds__(256, BM >= 128 ? 2 : 3) void dgemm_kernel(int M, in
 }
 
 // Chunked variant: blockIdx.z = chunk; offsets/dims from ChunkSpec.
-template <int BM, int BN, bool TA, bool TB>
+// TRI = 1: each chunk's A is upper triangular (K from the tile's first row);
+// TRI = 2: each chunk's B is upper triangular (K up to the tile's last column).
+template <int BM, int BN, bool TA, bool TB, int TRI = 0>
 __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, double alpha,
                                                             const double *__restrict__ A,
                                                             int64_t lda,
@@ -252,7 +254,8 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
-  mainloop<double, double, BM, BN, TA, TB>(A, lda, B, ldb, M, N, 0, K, tm, tn, As, Bs, acc);
+  const int k0 = TRI == 1 ? (tm / KC) * KC : 0, k1 = TRI == 2 ? min(K, tn + BN) : K;
+  mainloop<double, double, BM, BN, TA, TB>(A, lda, B, ldb, M, N, k0, k1, tm, tn, As, Bs, acc);
   epilogue<BM, BN, false>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
@@ -403,8 +406,27 @@ hipError_t dgemm_upper_a(hipStream_t st, int M, int N, int K, double alpha, cons
 
 hipError_t dgemm_chunked(hipStream_t st, bool ta, bool tb, const ChunkSpec &cs, double alpha,
                          const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
-                         double *C, int64_t ldc) {
+                         double *C, int64_t ldc, int tri) {
   if (cs.nc <= 0) return hipSuccess;
+  if (tri != 0) {  // triangular A (1) or B (2), no transposes
+    const int hmax = std::max(cs.c, cs.m - (cs.nc - 1) * cs.c);
+    const int M = cs.M < 0 ? hmax : cs.M, N = cs.N < 0 ? hmax : cs.N;
+    if (M <= 0 || N <= 0 || ta || tb) return hipErrorInvalidValue;
+    const bool big = int64_t(cdiv(M, 128)) * cdiv(N, 128) * cs.nc >= 256 && N > 64;
+#define TG_CHT(BM_, TRI_)                                                                        \
+  hipLaunchKernelGGL((dgemm_chunked_kernel<BM_, BM_, false, false, TRI_>),                      \
+                     dim3(cdiv(N, BM_), cdiv(M, BM_), cs.nc), dim3(256), 0, st, cs, alpha, A,    \
+                     lda, B, ldb, beta, C, ldc)
+    if (big) {
+      if (tri == 1) TG_CHT(128, 1);
+      else TG_CHT(128, 2);
+    } else {
+      if (tri == 1) TG_CHT(64, 1);
+      else TG_CHT(64, 2);
+    }
+#undef TG_CHT
+    return hipGetLastError();
+  }
   const int hmax = std::max(cs.c, cs.m - (cs.nc - 1) * cs.c);
   const int M = cs.M < 0 ? hmax : cs.M, N = cs.N < 0 ? hmax : cs.N;
   if (M <= 0 || N <= 0) return hipSuccess;
