@@ -587,6 +587,90 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
   if (j < n && sub == 0) w_out[j] = 0.5 * (lo + hi);
 }
 
+// Tridiagonals too long for LDS (n > 10,240): the rows stream through LDS in
+// chunks of BIS_CH, staged by the whole workgroup.  Every slot of a workgroup
+// must count over the same unreduced block (the usual single-block case; a
+// workgroup whose slots span blocks falls back to global reads): the slots'
+// recurrences then walk the same rows in lock-step, each carrying its q
+// across the chunks.  Same arithmetic as the LDS-row count.
+constexpr int BIS_CH = 2048;
+__global__ __launch_bounds__(256) void bisect_chunk_kernel(const double *__restrict__ d,
+                                                           const double *__restrict__ e2g, int n,
+                                                           const double *__restrict__ bnd,
+                                                           const int32_t *__restrict__ bsv,
+                                                           const int32_t *__restrict__ bev,
+                                                           double *__restrict__ w_out) {
+  __shared__ double2 rows[BIS_CH];
+  __shared__ int s_b[2];
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (ML - 1);
+  const int grp_base = lane & ~(ML - 1);
+  const int j = (blockIdx.x * blockDim.x + threadIdx.x) / ML;
+  const int b0 = j < n ? bsv[j] : 0, b1 = j < n ? bev[j] : 1;
+  const int jl = j - b0;
+  const double pivmin = bnd[3];
+  const double rpiv = __builtin_amdgcn_rcp(-pivmin);
+  if (threadIdx.x == 0) {
+    const int j0 = blockIdx.x * (blockDim.x / ML);  // < n: the grid covers n slots
+    s_b[0] = bsv[j0];
+    s_b[1] = bev[j0];
+  }
+  __syncthreads();
+  const bool uni = __syncthreads_and(j >= n || (b0 == s_b[0] && b1 == s_b[1]));
+  const int B0 = s_b[0], len = s_b[1] - s_b[0];
+  double lo = bnd[0], hi = bnd[1];
+  for (int round = 0; round < ROUNDS; ++round) {
+    const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
+    int c = 0;
+    if (!uni) {
+      if (j < n) c = sturm_count(d + b0, e2g + b0, b1 - b0, x, pivmin);
+    } else {
+      double q = 0.0;
+      auto stepq = [&](double2 v) {
+        const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(q), pivmin, 5);  // OLE
+        const double r0 = __builtin_amdgcn_rcp(q);
+        const double qe = vsel(tiny, -pivmin, q);
+        c += qe < 0.0;
+        double r = vsel(tiny, rpiv, r0);
+        r = fma(fma(-qe, r, 1.0), r, r);
+        q = fma(-v.y, r, v.x - x);
+      };
+      for (int c0 = 0; c0 < len; c0 += BIS_CH) {
+        const int cn = min(BIS_CH, len - c0);
+        __syncthreads();  // the previous chunk's readers are done
+        for (int k = threadIdx.x; k < cn; k += blockDim.x) {
+          const int a = B0 + c0 + k;
+          rows[k] = make_double2(d[a], c0 + k > 0 ? e2g[a - 1] : 0.0);
+        }
+        __syncthreads();
+        int k0 = 0;
+        if (c0 == 0) {
+          q = rows[0].x - x;
+          k0 = 1;
+        }
+        for (; k0 + 8 <= cn; k0 += 8) {
+          double2 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = rows[k0 + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) stepq(v[u]);
+        }
+        for (; k0 < cn; ++k0) stepq(rows[k0]);
+      }
+      const double qe = fabs(q) <= pivmin ? -pivmin : q;
+      c += qe < 0.0;
+    }
+    const unsigned long long m = __ballot(j < n && c <= jl);
+    const unsigned long long gm = ML == 64 ? ~0ull : ((1ull << (ML & 63)) - 1) << grp_base;
+    const int a = __popcll(m & gm);
+    const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
+    const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
+    lo = a > 0 ? xa1 : lo;
+    hi = a < ML ? xa : hi;
+  }
+  if (j < n && sub == 0) w_out[j] = 0.5 * (lo + hi);
+}
+
 // e^2 (e[n-1] = 0 padding)
 __global__ void square_kernel(const double *__restrict__ e, int n, double *__restrict__ e2) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1225,14 +1309,14 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.es, n, w.acol);
   TG_LAUNCHED();
   auto btok = tg::prof_begin(st, tg::PROF_BISECT, 16.0 * n, 0.0);
-  if (lds <= 160 * 1024) {
+  if (lds <= 160 * 1024 && !getenv("TG_BISECT_CHUNK")) {  // env: tests force the chunked kernel
     if (lds > 64 * 1024)
       TG_HIP(hipFuncSetAttribute((const void *)bisect_kernel<true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(bisect_kernel<true>, dim3(blocks), dim3(256), lds, st, w.d, w.acol, n, bnd,
                        w.bs, w.be, w.wraw);
   } else {
-    hipLaunchKernelGGL(bisect_kernel<false>, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
+    hipLaunchKernelGGL(bisect_chunk_kernel, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
                        w.bs, w.be, w.wraw);
   }
   tg::prof_end(st, btok);

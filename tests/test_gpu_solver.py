@@ -102,6 +102,12 @@ def eig_problem(kind, n, seed):
         Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
         lam = np.concatenate([np.full(n // 4, 2.0), np.linspace(0.1, 1.0, n - n // 4)])
         return (Q * lam) @ Q.T
+    if kind == "blocks":   # block diagonal: the tridiagonal splits into unreduced blocks
+        a = n // 3
+        H = np.zeros((n, n))
+        H[:a, :a] = eig_problem("wishart", a, seed + 1)
+        H[a:, a:] = 3.0 * eig_problem("wishart", n - a, seed + 2)
+        return H
     raise ValueError(kind)
 
 
@@ -145,6 +151,16 @@ def test_eigh(lib, kind, n):
 def test_eigh_one_stage(lib, monkeypatch, kind, n):
     """The one-stage dlatrd-style reduction (TG_EIGH_TWOSTAGE=0) stays correct."""
     monkeypatch.setenv("TG_EIGH_TWOSTAGE", "0")
+    test_eigh(lib, kind, n)
+
+
+@pytest.mark.parametrize("kind,n", [("wishart", 777), ("graded", 300), ("clustered", 256),
+                                    ("blocks", 600), ("wishart", 1), ("wishart", 4200)])
+def test_eigh_bisect_chunked(lib, monkeypatch, kind, n):
+    """The chunked-LDS bisection (n > 10,240 in production; TG_BISECT_CHUNK forces
+    it): rows staged in 2048-row chunks, slots spanning split blocks fall back
+    to global reads (the "blocks" case), 4200 rows = three chunks."""
+    monkeypatch.setenv("TG_BISECT_CHUNK", "1")
     test_eigh(lib, kind, n)
 
 
