@@ -47,6 +47,17 @@ constexpr int ML = TG_ML;  // multisection lanes per eigenvalue
 // (ML+1)^ROUNDS > 2^57: the Gershgorin interval shrinks below one ulp
 constexpr int ROUNDS = ML == 16 ? 14 : (ML == 32 ? 12 : 10);
 static_assert(ML == 16 || ML == 32 || ML == 64, "ML");
+// Shared first rounds (ML = 16, n >= GRID_MIN_N): Sturm counts of the first
+// unreduced block [0, be[0]) at the 17^4 - 1 points of a uniform grid of the
+// Gershgorin interval, computed once for all of that block's eigenvalues
+// (each one's first four 17-sections would evaluate points of this grid);
+// they then start from their grid cells and run ROUNDS - 4 rounds.  The first
+// block is the one that matters: a rank-deficient H gives T = one block of
+// about the rank followed by 1 x 1 blocks (n = 4096, k = 3058: [0, 3128) and
+// 962 single rows).
+constexpr int GRID_ROUNDS = ML == 16 ? 4 : 0;
+constexpr int GRID_PTS = ML == 16 ? 17 * 17 * 17 * 17 - 1 : 1;
+constexpr int GRID_MIN_N = 1024;
 constexpr int SPLITK = 8;
 
 struct Tri {
@@ -72,6 +83,7 @@ struct Tri {
   int32_t *be;   // n   end (exclusive) of that block
   int32_t *slot; // n   slot of the j-th smallest eigenvalue
   unsigned *cnt; // reduction tickets
+  int32_t *gcnt; // GRID_PTS  Sturm counts of T at the bisection grid points
   int32_t *cl;   // 2 + 4n  cluster lists: [0] small count, [1] big count, small (start, len)
                  //         pairs from 2, big pairs from 2 + 2n
 };
@@ -109,6 +121,7 @@ void tri_layout(A &ar, int n, Tri *t) {
   take(q.bs, n);
   take(q.be, n);
   take(q.slot, n);
+  take(q.gcnt, GRID_PTS);
   take(q.cl, 2 + 4 * size_t(n));
 }
 
@@ -396,35 +409,40 @@ __device__ inline int sturm_count(const double *__restrict__ d, const double *__
   return c;
 }
 
-// sturm_count over LDS rows de[k] = {d[k], e2[k-1]} (one 16-byte read per
-// step), same arithmetic: the reciprocal of q and the pivmin test of q run side
-// by side and the clamp selects between rcp(q) and rcp(-pivmin) (v_cndmask,
-// no branch), so the clamp is off the serial chain.
+// One step of the count over an LDS row v = {d[k], e2[k-1]}: the pivot q of
+// row k-1 is counted (negative, or clamped to -pivmin when |q| <= pivmin: both
+// are q <= pivmin) and replaced by row k's.  The reciprocal of q and its Newton
+// step run unconditionally; a tiny q then selects the refined reciprocal of
+// -pivmin instead (v_cndmask, no branch), so the clamp is off the serial chain.
+__device__ inline void sturm_step(double &q, int &c, double2 v, double x, double pivmin,
+                                  double rpivn) {
+  const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(q), pivmin, 5);  // OLE
+  c += q <= pivmin;
+  const double r0 = __builtin_amdgcn_rcp(q);
+  const double r = vsel(tiny, rpivn, fma(fma(-q, r0, 1.0), r0, r0));
+  q = fma(-v.y, r, v.x - x);
+}
+__device__ inline double rcp_pivmin(double pivmin) {  // 1/(-pivmin), one Newton step
+  const double r = __builtin_amdgcn_rcp(-pivmin);
+  return fma(fma(pivmin, r, 1.0), r, r);
+}
+
+// sturm_count over LDS rows de[k] = {d[k], e2[k-1]} (one 16-byte read per step).
 __device__ inline int sturm_count_rows(const double2 *__restrict__ de, int n, double x,
                                        double pivmin) {
-  const double rpiv = __builtin_amdgcn_rcp(-pivmin);
+  const double rpivn = rcp_pivmin(pivmin);
   double q = de[0].x - x;
   int c = 0;
-  auto stepq = [&](double2 v) {
-    const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(q), pivmin, 5);  // OLE
-    const double r0 = __builtin_amdgcn_rcp(q);
-    const double qe = vsel(tiny, -pivmin, q);
-    c += qe < 0.0;
-    double r = vsel(tiny, rpiv, r0);
-    r = fma(fma(-qe, r, 1.0), r, r);
-    q = fma(-v.y, r, v.x - x);
-  };
   int k0 = 1;
   for (; k0 + 8 <= n; k0 += 8) {
     double2 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = de[k0 + u];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) stepq(v[u]);
+    for (int u = 0; u < 8; ++u) sturm_step(q, c, v[u], x, pivmin, rpivn);
   }
-  for (; k0 < n; ++k0) stepq(de[k0]);
-  const double qe = fabs(q) <= pivmin ? -pivmin : q;
-  return c + (qe < 0.0);
+  for (; k0 < n; ++k0) sturm_step(q, c, de[k0], x, pivmin, rpivn);
+  return c + (q <= pivmin);
 }
 
 // Gershgorin bounds, ||T||_1 and pivmin: one workgroup.
@@ -542,13 +560,73 @@ __global__ __launch_bounds__(256) void rank_sort_kernel(const double *__restrict
   }
 }
 
+// Grid point g of the Gershgorin interval [lo, hi] (g = -1 / GRID_PTS: the ends).
+__device__ inline double grid_x(double lo, double hi, int g) {
+  return g < 0 ? lo : (g >= GRID_PTS ? hi : lo + (hi - lo) * double(g + 1) / double(GRID_PTS + 1));
+}
+
+// Sturm counts of the first block [0, be[0]) at every grid point, one thread
+// each; rows staged through LDS.
+constexpr int GRID_CH = 2048;
+__global__ __launch_bounds__(256) void grid_count_kernel(const double *__restrict__ d,
+                                                         const double *__restrict__ e2g, int n,
+                                                         const double *__restrict__ bnd,
+                                                         const int32_t *__restrict__ bev,
+                                                         int32_t *__restrict__ gcnt) {
+  __shared__ double2 rows[GRID_CH];
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  n = bev[0];
+  const double pivmin = bnd[3], rpivn = rcp_pivmin(pivmin);
+  const double x = grid_x(bnd[0], bnd[1], g);
+  double q = 0.0;
+  int c = 0;
+  for (int c0 = 0; c0 < n; c0 += GRID_CH) {
+    const int cn = min(GRID_CH, n - c0);
+    __syncthreads();
+    for (int k = threadIdx.x; k < cn; k += blockDim.x)
+      rows[k] = make_double2(d[c0 + k], c0 + k > 0 ? e2g[c0 + k - 1] : 0.0);
+    __syncthreads();
+    int k0 = 0;
+    if (c0 == 0) {
+      q = rows[0].x - x;
+      k0 = 1;
+    }
+    for (; k0 + 8 <= cn; k0 += 8) {
+      double2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = rows[k0 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sturm_step(q, c, v[u], x, pivmin, rpivn);
+    }
+    for (; k0 < cn; ++k0) sturm_step(q, c, rows[k0], x, pivmin, rpivn);
+  }
+  if (g < GRID_PTS) gcnt[g] = c + (q <= pivmin);
+}
+
+// Starting interval of eigenvalue j of the first block: the grid cell
+// [x_{g-1}, x_g) with count(x_{g-1}) <= j < count(x_g) (binary search; the
+// ends count 0 and n, so a cell is found even if rounding broke monotonicity).
+__device__ inline void grid_start(const int32_t *__restrict__ gcnt, int j, const double *bnd,
+                                  double &lo, double &hi) {
+  int a = -1, b = GRID_PTS;  // count(a) <= j < count(b)
+  while (b - a > 1) {
+    const int m = (a + b) >> 1;
+    if (gcnt[m] > j) b = m;
+    else a = m;
+  }
+  lo = grid_x(bnd[0], bnd[1], a);
+  hi = grid_x(bnd[0], bnd[1], b);
+}
+
 // LDS: d and e^2 staged in LDS (n <= 10240); otherwise e2 holds e^2 in global memory.
+// gcnt (null: no grid): a wave whose slots are all in the first block starts them from their grid cells.
 template <bool LDS>
 __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ d,
                                                      const double *__restrict__ e2g, int n,
                                                      const double *__restrict__ bnd,
                                                      const int32_t *__restrict__ bsv,
                                                      const int32_t *__restrict__ bev,
+                                                     const int32_t *__restrict__ gcnt,
                                                      double *__restrict__ w_out) {
   extern __shared__ double sh[];
   const double *dd = d, *ee2 = e2g;
@@ -567,38 +645,46 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
   const int jl = j - b0;
   const double pivmin = bnd[3];
   double lo = bnd[0], hi = bnd[1];
-  for (int round = 0; round < ROUNDS; ++round) {
+  // slots of the first block start from their grid cells and need GRID_ROUNDS
+  // fewer rounds; the wave runs its longest slot's count, the others idle
+  const bool sg = gcnt && j < n && b0 == 0;
+  if (sg) grid_start(gcnt, j, bnd, lo, hi);
+  const int my_rounds = sg ? ROUNDS - GRID_ROUNDS : ROUNDS;
+  const int rounds = __ballot(j < n && !sg) ? ROUNDS : ROUNDS - GRID_ROUNDS;
+  for (int round = 0; round < rounds; ++round) {
+    const bool act = j < n && round < my_rounds;
     const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
     int c = 0;
-    if (j < n)
+    if (act)
       c = LDS ? sturm_count_rows(rows + b0, b1 - b0, x, pivmin)
               : sturm_count(dd + b0, ee2 + b0, b1 - b0, x, pivmin);
     // lanes with count(x) <= jl have x <= lambda_jl
-    const unsigned long long m = __ballot(j < n && c <= jl);
+    const unsigned long long m = __ballot(act && c <= jl);
     const unsigned long long gm = ML == 64 ? ~0ull : ((1ull << (ML & 63)) - 1) << grp_base;
     const int a = __popcll(m & gm);
     const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
     const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
-    const double nlo = a > 0 ? xa1 : lo;
-    const double nhi = a < ML ? xa : hi;
-    lo = nlo;
-    hi = nhi;
+    if (act) {
+      lo = a > 0 ? xa1 : lo;
+      hi = a < ML ? xa : hi;
+    }
   }
   if (j < n && sub == 0) w_out[j] = 0.5 * (lo + hi);
 }
 
 // Tridiagonals too long for LDS (n > 10,240): the rows stream through LDS in
-// chunks of BIS_CH, staged by the whole workgroup.  Every slot of a workgroup
-// must count over the same unreduced block (the usual single-block case; a
-// workgroup whose slots span blocks falls back to global reads): the slots'
-// recurrences then walk the same rows in lock-step, each carrying its q
-// across the chunks.  Same arithmetic as the LDS-row count.
+// chunks of BIS_CH, staged by the whole workgroup.  The staged block is that of
+// the workgroup's first slot; its slots' recurrences walk the same rows in
+// lock-step, each carrying its q across the chunks (same arithmetic as the
+// LDS-row count).  Slots of other blocks (a workgroup straddling a split:
+// in practice the 1 x 1 blocks after the first one) count from global memory.
 constexpr int BIS_CH = 2048;
 __global__ __launch_bounds__(256) void bisect_chunk_kernel(const double *__restrict__ d,
                                                            const double *__restrict__ e2g, int n,
                                                            const double *__restrict__ bnd,
                                                            const int32_t *__restrict__ bsv,
                                                            const int32_t *__restrict__ bev,
+                                                           const int32_t *__restrict__ gcnt,
                                                            double *__restrict__ w_out) {
   __shared__ double2 rows[BIS_CH];
   __shared__ int s_b[2];
@@ -609,32 +695,29 @@ __global__ __launch_bounds__(256) void bisect_chunk_kernel(const double *__restr
   const int b0 = j < n ? bsv[j] : 0, b1 = j < n ? bev[j] : 1;
   const int jl = j - b0;
   const double pivmin = bnd[3];
-  const double rpiv = __builtin_amdgcn_rcp(-pivmin);
+  const double rpivn = rcp_pivmin(pivmin);
   if (threadIdx.x == 0) {
     const int j0 = blockIdx.x * (blockDim.x / ML);  // < n: the grid covers n slots
     s_b[0] = bsv[j0];
     s_b[1] = bev[j0];
   }
   __syncthreads();
-  const bool uni = __syncthreads_and(j >= n || (b0 == s_b[0] && b1 == s_b[1]));
   const int B0 = s_b[0], len = s_b[1] - s_b[0];
+  const bool mine = j < n && b0 == B0 && b1 == s_b[1];
   double lo = bnd[0], hi = bnd[1];
-  for (int round = 0; round < ROUNDS; ++round) {
+  const bool sg = gcnt && j < n && b0 == 0;
+  if (sg) grid_start(gcnt, j, bnd, lo, hi);
+  const int my_rounds = sg ? ROUNDS - GRID_ROUNDS : ROUNDS;
+  // workgroup-uniform trip counts (the chunk loop's barriers)
+  const int rounds = __syncthreads_or(j < n && !sg) ? ROUNDS : ROUNDS - GRID_ROUNDS;
+  for (int round = 0; round < rounds; ++round) {
+    const bool act = j < n && round < my_rounds;
     const double x = lo + (hi - lo) * double(sub + 1) / double(ML + 1);
     int c = 0;
-    if (!uni) {
-      if (j < n) c = sturm_count(d + b0, e2g + b0, b1 - b0, x, pivmin);
-    } else {
+    if (act && !mine) c = sturm_count(d + b0, e2g + b0, b1 - b0, x, pivmin);
+    if (__syncthreads_or(act && mine)) {
+      const bool run = act && mine;
       double q = 0.0;
-      auto stepq = [&](double2 v) {
-        const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(q), pivmin, 5);  // OLE
-        const double r0 = __builtin_amdgcn_rcp(q);
-        const double qe = vsel(tiny, -pivmin, q);
-        c += qe < 0.0;
-        double r = vsel(tiny, rpiv, r0);
-        r = fma(fma(-qe, r, 1.0), r, r);
-        q = fma(-v.y, r, v.x - x);
-      };
       for (int c0 = 0; c0 < len; c0 += BIS_CH) {
         const int cn = min(BIS_CH, len - c0);
         __syncthreads();  // the previous chunk's readers are done
@@ -643,30 +726,33 @@ __global__ __launch_bounds__(256) void bisect_chunk_kernel(const double *__restr
           rows[k] = make_double2(d[a], c0 + k > 0 ? e2g[a - 1] : 0.0);
         }
         __syncthreads();
-        int k0 = 0;
-        if (c0 == 0) {
-          q = rows[0].x - x;
-          k0 = 1;
-        }
-        for (; k0 + 8 <= cn; k0 += 8) {
-          double2 v[8];
+        if (run) {
+          int k0 = 0;
+          if (c0 == 0) {
+            q = rows[0].x - x;
+            k0 = 1;
+          }
+          for (; k0 + 8 <= cn; k0 += 8) {
+            double2 v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = rows[k0 + u];
+            for (int u = 0; u < 8; ++u) v[u] = rows[k0 + u];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) stepq(v[u]);
+            for (int u = 0; u < 8; ++u) sturm_step(q, c, v[u], x, pivmin, rpivn);
+          }
+          for (; k0 < cn; ++k0) sturm_step(q, c, rows[k0], x, pivmin, rpivn);
         }
-        for (; k0 < cn; ++k0) stepq(rows[k0]);
       }
-      const double qe = fabs(q) <= pivmin ? -pivmin : q;
-      c += qe < 0.0;
+      if (run) c += q <= pivmin;
     }
-    const unsigned long long m = __ballot(j < n && c <= jl);
+    const unsigned long long m = __ballot(act && c <= jl);
     const unsigned long long gm = ML == 64 ? ~0ull : ((1ull << (ML & 63)) - 1) << grp_base;
     const int a = __popcll(m & gm);
     const double xa1 = __shfl(x, grp_base + (a > 0 ? a - 1 : 0));
     const double xa = __shfl(x, grp_base + (a < ML ? a : ML - 1));
-    lo = a > 0 ? xa1 : lo;
-    hi = a < ML ? xa : hi;
+    if (act) {
+      lo = a > 0 ? xa1 : lo;
+      hi = a < ML ? xa : hi;
+    }
   }
   if (j < n && sub == 0) w_out[j] = 0.5 * (lo + hi);
 }
@@ -1308,16 +1394,38 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   TG_LAUNCHED();
   hipLaunchKernelGGL(square_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.es, n, w.acol);
   TG_LAUNCHED();
+  if (getenv("TG_TRI_BLOCKS")) {  // development: the unreduced block structure of T
+    std::vector<int32_t> hb(n), he(n);
+    TG_HIP(hipMemcpyAsync(hb.data(), w.bs, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    TG_HIP(hipMemcpyAsync(he.data(), w.be, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    TG_HIP(hipStreamSynchronize(st));
+    std::vector<int> len;
+    for (int i = 0; i < n; i = he[i]) len.push_back(he[i] - hb[i]);
+    std::vector<int> srt(len);
+    std::sort(srt.rbegin(), srt.rend());
+    int ones = 0;
+    for (int l : len) ones += l == 1;
+    fprintf(stderr, "T blocks: n %d, %zu blocks, %d of size 1, largest", n, len.size(), ones);
+    for (size_t i = 0; i < srt.size() && i < 6; ++i) fprintf(stderr, " %d", srt[i]);
+    fprintf(stderr, "; first block [%d, %d)\n", hb[0], he[0]);
+  }
   auto btok = tg::prof_begin(st, tg::PROF_BISECT, 16.0 * n, 0.0);
+  const int32_t *gcnt = nullptr;
+  if (GRID_ROUNDS > 0 && n >= GRID_MIN_N && !getenv("TG_BISECT_NOGRID")) {
+    hipLaunchKernelGGL(grid_count_kernel, dim3(tg::cdiv(GRID_PTS, 256)), dim3(256), 0, st, w.d,
+                       w.acol, n, bnd, w.be, w.gcnt);
+    TG_LAUNCHED();
+    gcnt = w.gcnt;
+  }
   if (lds <= 160 * 1024 && !getenv("TG_BISECT_CHUNK")) {  // env: tests force the chunked kernel
     if (lds > 64 * 1024)
       TG_HIP(hipFuncSetAttribute((const void *)bisect_kernel<true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     hipLaunchKernelGGL(bisect_kernel<true>, dim3(blocks), dim3(256), lds, st, w.d, w.acol, n, bnd,
-                       w.bs, w.be, w.wraw);
+                       w.bs, w.be, gcnt, w.wraw);
   } else {
     hipLaunchKernelGGL(bisect_chunk_kernel, dim3(blocks), dim3(256), 0, st, w.d, w.acol, n, bnd,
-                       w.bs, w.be, w.wraw);
+                       w.bs, w.be, gcnt, w.wraw);
   }
   tg::prof_end(st, btok);
   TG_LAUNCHED();

@@ -408,9 +408,76 @@ __device__ __forceinline__ void trinv_upper32(Get get, const double *rd, double 
   }
 }
 
+// Two independent inverses at once (the Householder reconstruction's U^-1 and
+// Y1^-T): the same blocked steps with matrix A on waves 0-1 and B on waves 2-3
+// where a step has at most 128 items, both per thread where it has 256, so the
+// two share every barrier and their dependent fma chains overlap.
+template <class GetA, class GetB>
+__device__ __forceinline__ void trinv2_upper32(GetA geta, const double *rda, double (*XA)[33],
+                                               double (*tmpA)[33], GetB getb, const double *rdb,
+                                               double (*XB)[33], double (*tmpB)[33]) {
+  const int tid = otid();
+  for (int e = tid; e < 1024; e += PT) {
+    XA[e >> 5][e & 31] = 0.0;
+    XB[e >> 5][e & 31] = 0.0;
+  }
+  __syncthreads();
+  auto diag = [&](auto get, const double *rd, double (*X)[33], int t) {
+    const int bb = 8 * (t >> 3), c = t & 7;
+    double x[8];
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      double acc = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = i + 1; k < 8; ++k) acc = fma(-get(bb + i, bb + k), x[k], acc);
+      x[i] = (i <= c) ? acc * (rd ? rd[bb + i] : 1.0) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) X[bb + i][bb + c] = x[i];
+  };
+  if (tid < 32) diag(geta, rda, XA, tid);
+  else if (tid >= 128 && tid < 160) diag(getb, rdb, XB, tid - 128);
+  __syncthreads();
+#pragma unroll
+  for (int lev = 0; lev < 2; ++lev) {
+    const int hb = lev == 0 ? 8 : 16;
+    auto prod1 = [&](auto get, double (*X)[33], double (*tmp)[33], int t) {
+      const int blk = t / (hb * hb), r = (t / hb) % hb, c = t % hb;
+      const int o = blk * 2 * hb;
+      double acc = 0.0;
+      for (int k = 0; k <= c; ++k) acc = fma(get(o + r, o + hb + k), X[o + hb + k][o + hb + c], acc);
+      tmp[o + r][o + hb + c] = acc;
+    };
+    auto prod2 = [&](double (*X)[33], double (*tmp)[33], int t) {
+      const int blk = t / (hb * hb), r = (t / hb) % hb, c = t % hb;
+      const int o = blk * 2 * hb;
+      double acc = 0.0;
+      for (int k = r; k < hb; ++k) acc = fma(X[o + r][o + k], tmp[o + k][o + hb + c], acc);
+      X[o + r][o + hb + c] = -acc;
+    };
+    if (lev == 0) {  // 2 blocks of 8 x 8: 128 items per matrix
+      if (tid < 128) prod1(geta, XA, tmpA, tid);
+      else prod1(getb, XB, tmpB, tid - 128);
+      __syncthreads();
+      if (tid < 128) prod2(XA, tmpA, tid);
+      else prod2(XB, tmpB, tid - 128);
+    } else {  // one 16 x 16 block: 256 items per matrix
+      prod1(geta, XA, tmpA, tid);
+      prod1(getb, XB, tmpB, tid);
+      __syncthreads();
+      prod2(XA, tmpA, tid);
+      prod2(XB, tmpB, tid);
+    }
+    __syncthreads();
+  }
+}
+
 // Wave 0 of workgroup 0: LU of I - Cq S (Householder reconstruction) into
 // Ut (U), Cq (Y1, unit lower), sv (S), uinv; out of line so that its pivot
-// chain is scheduled on its own.
+// chain is scheduled on its own.  Step j publishes column j + 1 (which holds
+// the next pivot) before the rest of its update and row j + 1 after it, so
+// the next step's pivot chain (sign, reciprocal) starts while the row is
+// still in flight.
 __device__ __forceinline__ void lu_hr() {
   PqrSm &sm = s_pq;
   const int lane = otid() & 63;
@@ -422,6 +489,18 @@ __device__ __forceinline__ void lu_hr() {
       c[l] = sm.Cq[i][16 * h + l];
       lw[l] = 0.0;
     }
+    double svr = 0.0;  // lane j: S_jj
+    // row / column of step j in bcast[2 (j & 1)] / bcast[2 (j & 1) + 1]; the
+    // lanes not holding column j write a trash slot of their own
+    auto put_row = [&](double *buf) {
+      double2 *d2 = reinterpret_cast<double2 *>(buf + 16 * h);
+#pragma unroll
+      for (int l = 0; l < 8; ++l) d2[l] = make_double2(c[2 * l], c[2 * l + 1]);
+    };
+    if (i == 0) put_row(sm.bcast[0]);
+    sm.bcast[1][h == 0 ? i : 32 + lane] = c[0];
+    wave_lds_sync();
+    double qjj = sm.bcast[1][0], cij = sm.bcast[1][i];  // step j's pivot and column entry
     // L_ij = -S_jj C^(j)_ij / U_jj, U_jj = 1 + |C^(j)_jj|, S_jj = -sign(C^(j)_jj),
     // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl.  No per-entry masks: rows <= j take
     // l = 0; the working columns < j (and j, once L_ij is in lw) are dead and
@@ -429,16 +508,7 @@ __device__ __forceinline__ void lu_hr() {
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       const int hj = j >> 4, cj = j & 15;
-      // double-buffered row / column: the next step's writes need not wait for these reads
-      double *buf = sm.bcast[2 * (j & 1)], *cbuf = sm.bcast[2 * (j & 1) + 1];
-      if (i == j) {  // row j (its two half-rows: lanes j and j + 32)
-        double2 *d2 = reinterpret_cast<double2 *>(buf + 16 * h);
-#pragma unroll
-        for (int l = 0; l < 8; ++l) d2[l] = make_double2(c[2 * l], c[2 * l + 1]);
-      }
-      cbuf[h == hj ? i : 32 + lane] = c[cj];  // column j; the other lanes write their own trash slot
-      wave_lds_sync();
-      const double qjj = buf[j], cij = cbuf[i];
+      const double *buf = sm.bcast[2 * (j & 1)];
       double rw[16];
       const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
 #pragma unroll
@@ -450,12 +520,30 @@ __device__ __forceinline__ void lu_hr() {
       // S_jj = -sign(C_jj) (as a sign copy, no compare on the chain)
       const double ms = copysign(1.0, qjj);
       const double ru = rcp_nr(1.0 + fabs(qjj));
-      if (lane == 0) sm.sv[j] = -ms;
+      svr = lane == j ? -ms : svr;
       const double lij = i > j ? ms * cij * ru : 0.0;
       if (h == hj) lw[cj] = lij;
+      if (j + 1 < 32) {
+        const int hn = (j + 1) >> 4, cn = (j + 1) & 15;
+        double *nbuf = sm.bcast[2 * ((j + 1) & 1)], *ncbuf = sm.bcast[2 * ((j + 1) & 1) + 1];
+        c[cn] = fma(-lij, rw[cn], c[cn]);
+        ncbuf[h == hn ? i : 32 + lane] = c[cn];
+        wave_lds_sync();
+        const double qn = ncbuf[j + 1], cn_i = ncbuf[i];  // read back at once: the next pivot chain
+        __builtin_amdgcn_sched_barrier(0);  // column store and reads issue before the rest of the update
 #pragma unroll
-      for (int l = 0; l < 16; ++l) c[l] = fma(-lij, rw[l], c[l]);
+        for (int l = 0; l < 16; ++l)
+          if (l != cn) c[l] = fma(-lij, rw[l], c[l]);
+        if (i == j + 1) put_row(nbuf);
+        wave_lds_sync();
+        qjj = qn;
+        cij = cn_i;
+      } else {
+#pragma unroll
+        for (int l = 0; l < 16; ++l) c[l] = fma(-lij, rw[l], c[l]);
+      }
     }
+    if (lane < 32) sm.sv[lane] = svr;
     wave_lds_sync();
     DBG_STAMP_T(20, 0)
 #pragma unroll
@@ -511,10 +599,10 @@ __device__ __forceinline__ void hr_top_ool() {
     const int i2 = e >> 5, cc = e & 31;
     g.A[(g.r0 + int64_t(i2)) * g.lda + g.p + cc] = (i2 <= cc) ? sm.sv[i2] * sm.Ra[i2][cc] : 0.0;
   }
-  trinv_upper32([&](int i, int k) { return sm.Ut[i][k]; }, sm.uinv, UI, Tmp);
-  // Y1^-T = (Y1^T)^-1 (unit upper), into RgI's slot? RgI is still needed: use Tm for it
-  trinv_upper32([&](int i, int k) { return sm.Cq[k][i]; }, nullptr, sm.Tm, Tmp);
-  __syncthreads();
+  // U^-1 and Y1^-T = (Y1^T)^-1 (unit upper, into Tm); Lt (this pass's factor,
+  // already folded into RgI and Ra) is the second scratch
+  trinv2_upper32([&](int i, int k) { return sm.Ut[i][k]; }, sm.uinv, UI, Tmp,
+                 [&](int i, int k) { return sm.Cq[k][i]; }, nullptr, sm.Tm, sm.Lt);
   DBG_STAMP(18)
   if (tid < 32) sm.dsum[tid] = -sm.sv[tid];
   // T = U Y1^-T (into Tmp, then Tm), M1 = RgI (-S) U^-1

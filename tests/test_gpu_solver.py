@@ -125,7 +125,8 @@ def run_eigh(lib, H, k):
 
 @pytest.mark.parametrize("kind,n", [("wishart", 200), ("wishart", 777), ("lowrank", 512),
                                     ("graded", 300), ("clustered", 256), ("wishart", 1), ("wishart", 2),
-                                    ("wishart", 33)])
+                                    ("wishart", 33), ("graded", 1200), ("blocks", 1500),
+                                    ("clustered", 1100)])
 def test_eigh(lib, kind, n):
     H = eig_problem(kind, n, n)
     L = np.linalg.eigvalsh(H)
@@ -155,11 +156,13 @@ def test_eigh_one_stage(lib, monkeypatch, kind, n):
 
 
 @pytest.mark.parametrize("kind,n", [("wishart", 777), ("graded", 300), ("clustered", 256),
-                                    ("blocks", 600), ("wishart", 1), ("wishart", 4200)])
+                                    ("blocks", 600), ("wishart", 1), ("wishart", 4200),
+                                    ("blocks", 2100)])
 def test_eigh_bisect_chunked(lib, monkeypatch, kind, n):
     """The chunked-LDS bisection (n > 10,240 in production; TG_BISECT_CHUNK forces
     it): rows staged in 2048-row chunks, slots spanning split blocks fall back
-    to global reads (the "blocks" case), 4200 rows = three chunks."""
+    to global reads (the "blocks" case), 4200 rows = three chunks.  n >= 1024
+    also takes the shared grid of first rounds (slots of the first block)."""
     monkeypatch.setenv("TG_BISECT_CHUNK", "1")
     test_eigh(lib, kind, n)
 
