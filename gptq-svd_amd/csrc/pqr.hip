@@ -472,87 +472,99 @@ __device__ __forceinline__ void trinv2_upper32(GetA geta, const double *rda, dou
   }
 }
 
-// Wave 0 of workgroup 0: LU of I - Cq S (Householder reconstruction) into
-// Ut (U), Cq (Y1, unit lower), sv (S), uinv; out of line so that its pivot
-// chain is scheduled on its own.  Step j publishes column j + 1 (which holds
-// the next pivot) before the rest of its update and row j + 1 after it, so
-// the next step's pivot chain (sign, reciprocal) starts while the row is
-// still in flight.
+// Workgroup 0: LU of I - Cq S (Householder reconstruction) into Ut (U), Cq
+// (Y1, unit lower), sv (S), uinv.  All four waves: thread t holds row t >> 3,
+// columns 4 (t & 7) .. + 3, so a step is a few dozen instructions per wave (a
+// single wave holding 16 entries per lane spent ~1.5k cycles per pivot pair,
+// issue-bound).  Two pivots per barrier: step j (even) reads rows j, j + 1 and
+// columns j, j + 1 as left by step j - 2; every thread forms L_{j+1,j}, the
+// updated pivot U_{j+1,j+1} and its row's updated column j + 1 entry itself
+// (the same fma a sequential step does, so the factors are bit-identical),
+// then applies both rank-1 terms.  Columns j + 2, j + 3 are published before
+// the rest of the update, rows j + 2, j + 3 after it (double-buffered).
 __device__ __forceinline__ void lu_hr() {
   PqrSm &sm = s_pq;
-  const int lane = otid() & 63;
-  {
-    const int i = lane & 31, h = lane >> 5;
-    double c[16], lw[16];  // working rows (U part live) and the L entries of row i
+  const int tid = otid();
+  const int i = tid >> 3, g = tid & 7;
+  double c[4], lw[4];
 #pragma unroll
-    for (int l = 0; l < 16; ++l) {
-      c[l] = sm.Cq[i][16 * h + l];
-      lw[l] = 0.0;
+  for (int l = 0; l < 4; ++l) {
+    c[l] = sm.Cq[i][4 * g + l];
+    lw[l] = 0.0;
+  }
+  double svr = 0.0;  // thread j < 32: S_jj
+  // parity p: rows j, j + 1 at bcast[2p][0..31], [32..63]; columns j, j + 1 at
+  // bcast[2p + 1][0..31], [32..63] (entry of row i at i)
+  auto put_rows = [&](int j2, double *rb) {
+    if (i == j2 || i == j2 + 1) {
+      double2 *d2 = reinterpret_cast<double2 *>(rb + 32 * (i - j2) + 4 * g);
+      d2[0] = make_double2(c[0], c[1]);
+      d2[1] = make_double2(c[2], c[3]);
     }
-    double svr = 0.0;  // lane j: S_jj
-    // row / column of step j in bcast[2 (j & 1)] / bcast[2 (j & 1) + 1]; the
-    // lanes not holding column j write a trash slot of their own
-    auto put_row = [&](double *buf) {
-      double2 *d2 = reinterpret_cast<double2 *>(buf + 16 * h);
-#pragma unroll
-      for (int l = 0; l < 8; ++l) d2[l] = make_double2(c[2 * l], c[2 * l + 1]);
-    };
-    if (i == 0) put_row(sm.bcast[0]);
-    sm.bcast[1][h == 0 ? i : 32 + lane] = c[0];
-    wave_lds_sync();
-    double qjj = sm.bcast[1][0], cij = sm.bcast[1][i];  // step j's pivot and column entry
-    // L_ij = -S_jj C^(j)_ij / U_jj, U_jj = 1 + |C^(j)_jj|, S_jj = -sign(C^(j)_jj),
-    // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl.  No per-entry masks: rows <= j take
-    // l = 0; the working columns < j (and j, once L_ij is in lw) are dead and
-    // only ever feed dead columns.
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int hj = j >> 4, cj = j & 15;
-      const double *buf = sm.bcast[2 * (j & 1)];
-      double rw[16];
-      const double2 *b2 = reinterpret_cast<const double2 *>(buf + 16 * h);
-#pragma unroll
-      for (int l = 0; l < 8; ++l) {
-        const double2 v = b2[l];
-        rw[2 * l] = v.x;
-        rw[2 * l + 1] = v.y;
-      }
-      // S_jj = -sign(C_jj) (as a sign copy, no compare on the chain)
-      const double ms = copysign(1.0, qjj);
-      const double ru = rcp_nr(1.0 + fabs(qjj));
-      svr = lane == j ? -ms : svr;
-      const double lij = i > j ? ms * cij * ru : 0.0;
-      if (h == hj) lw[cj] = lij;
-      if (j + 1 < 32) {
-        const int hn = (j + 1) >> 4, cn = (j + 1) & 15;
-        double *nbuf = sm.bcast[2 * ((j + 1) & 1)], *ncbuf = sm.bcast[2 * ((j + 1) & 1) + 1];
-        c[cn] = fma(-lij, rw[cn], c[cn]);
-        ncbuf[h == hn ? i : 32 + lane] = c[cn];
-        wave_lds_sync();
-        const double qn = ncbuf[j + 1], cn_i = ncbuf[i];  // read back at once: the next pivot chain
-        __builtin_amdgcn_sched_barrier(0);  // column store and reads issue before the rest of the update
-#pragma unroll
-        for (int l = 0; l < 16; ++l)
-          if (l != cn) c[l] = fma(-lij, rw[l], c[l]);
-        if (i == j + 1) put_row(nbuf);
-        wave_lds_sync();
-        qjj = qn;
-        cij = cn_i;
-      } else {
-#pragma unroll
-        for (int l = 0; l < 16; ++l) c[l] = fma(-lij, rw[l], c[l]);
-      }
+  };
+  auto put_cols = [&](int j2, double *cb) {
+    if (g == (j2 >> 2)) {
+      cb[i] = c[j2 & 3];
+      cb[32 + i] = c[(j2 & 3) + 1];
     }
-    if (lane < 32) sm.sv[lane] = svr;
-    wave_lds_sync();
-    DBG_STAMP_T(20, 0)
+  };
+  put_cols(0, sm.bcast[1]);
+  put_rows(0, sm.bcast[0]);
+  // L_ij = -S_jj C^(j)_ij / U_jj, U_jj = 1 + |C^(j)_jj|, S_jj = -sign(C^(j)_jj),
+  // C^(j+1)_il = C^(j)_il - L_ij C^(j)_jl.  No per-entry masks: rows <= j take
+  // l = 0; the working columns < j (and j, once L_ij is in lw) are dead and
+  // only ever feed dead columns.
 #pragma unroll
-    for (int l = 0; l < 16; ++l) {
-      const int col = 16 * h + l;
-      sm.Ut[i][col] = (col == i) ? 1.0 + fabs(c[l]) : (col > i ? -sm.sv[col] * c[l] : 0.0);
-      sm.Cq[i][col] = (col < i) ? lw[l] : (col == i ? 1.0 : 0.0);
-      if (col == i) sm.uinv[i] = rcp_nr(1.0 + fabs(c[l]));
+  for (int j = 0; j < 32; j += 2) {
+    const double *rb = sm.bcast[2 * ((j >> 1) & 1)], *cb = sm.bcast[2 * ((j >> 1) & 1) + 1];
+    __syncthreads();
+    const double qjj = cb[j], cj1j = cb[j + 1];            // C_jj, C_{j+1,j}
+    const double cjj1 = cb[32 + j], cj1j1 = cb[32 + j + 1];  // C_{j,j+1}, C_{j+1,j+1}
+    const double cij = cb[i], cij1 = cb[32 + i];           // C_ij, C_{i,j+1}
+    double r0[4], r1[4];
+    {
+      const double2 *a2 = reinterpret_cast<const double2 *>(rb + 4 * g);
+      const double2 *b2 = reinterpret_cast<const double2 *>(rb + 32 + 4 * g);
+      const double2 a = a2[0], b = a2[1], u = b2[0], v = b2[1];
+      r0[0] = a.x; r0[1] = a.y; r0[2] = b.x; r0[3] = b.y;
+      r1[0] = u.x; r1[1] = u.y; r1[2] = v.x; r1[3] = v.y;
     }
+    const double ms0 = copysign(1.0, qjj);
+    const double ru0 = rcp_nr(1.0 + fabs(qjj));
+    const double lij = i > j ? ms0 * cij * ru0 : 0.0;
+    const double lj1 = ms0 * cj1j * ru0;  // row j + 1's (as its own thread forms it)
+    const double piv1 = fma(-lj1, cjj1, cj1j1);
+    const double cij1u = fma(-lij, cjj1, cij1);
+    const double ms1 = copysign(1.0, piv1);
+    const double ru1 = rcp_nr(1.0 + fabs(piv1));
+    const double lij1 = i > j + 1 ? ms1 * cij1u * ru1 : 0.0;
+    svr = tid == j ? -ms0 : (tid == j + 1 ? -ms1 : svr);
+    if (g == (j >> 2)) {
+      lw[j & 3] = lij;
+      lw[(j & 3) + 1] = lij1;
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) r1[l] = fma(-lj1, r0[l], r1[l]);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      c[l] = fma(-lij, r0[l], c[l]);
+      c[l] = fma(-lij1, r1[l], c[l]);
+    }
+    if (j + 2 < 32) {
+      const int np = ((j >> 1) + 1) & 1;
+      put_cols(j + 2, sm.bcast[2 * np + 1]);
+      put_rows(j + 2, sm.bcast[2 * np]);
+    }
+  }
+  if (tid < 32) sm.sv[tid] = svr;
+  __syncthreads();
+  DBG_STAMP_T(20, 0)
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const int col = 4 * g + l;
+    sm.Ut[i][col] = (col == i) ? 1.0 + fabs(c[l]) : (col > i ? -sm.sv[col] * c[l] : 0.0);
+    sm.Cq[i][col] = (col < i) ? lw[l] : (col == i ? 1.0 : 0.0);
+    if (col == i) sm.uinv[i] = rcp_nr(1.0 + fabs(c[l]));
   }
 }
 
@@ -566,7 +578,7 @@ __device__ __forceinline__ void lu_hr() {
 __device__ __forceinline__ void hr_top_ool() {
   PqrSm &sm = s_pq;
   const PqrArgs &g = sm.ga;
-  const int tid = otid(), wid = tid >> 6;
+  const int tid = otid();
   double(*UI)[33] = sm.Gs;
   double(*Tmp)[33] = reinterpret_cast<double(*)[33]>(&sm.MB[0][0]);  // MB is written last
   DBG_STAMP(16)
@@ -591,7 +603,7 @@ __device__ __forceinline__ void hr_top_ool() {
   }
   mm32<XS, 33, 33>(&sm.Cq[0][0], &sm.Xs[0][0], &sm.RgI[0][0], nullptr);
   __syncthreads();
-  if (wid == 0) lu_hr();
+  lu_hr();
   __syncthreads();
   DBG_STAMP(17)
   // the band block S R (lower storage: the upper part of A is never read again)
