@@ -115,8 +115,11 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 #ifndef TG_BULGE_FLAG_L2
 #define TG_BULGE_FLAG_L2 1
 #endif
-#ifndef TG_BULGE_WDEFER
-#define TG_BULGE_WDEFER 0
+#ifndef TG_BULGE_SPLIT
+#define TG_BULGE_SPLIT 3  // bit 0: wave 0 takes half of the write-back; bit 1: wave 3 half of the load
+#endif
+#ifndef TG_BULGE_GLDS
+#define TG_BULGE_GLDS 0  // the column loads go straight to LDS (global_load_lds_dwordx4)
 #endif
 #ifndef TG_BULGE_STATS
 #define TG_BULGE_STATS 0  // per-step s_memrealtime stamps (build-time: they slow every step)
@@ -434,11 +437,14 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #if TG_BULGE_STATS
   uint64_t sw = 0, stk = 0, sbar = 0, nsteps = 0;
 #endif
-  __shared__ double R[RING][LDB];
+  // one spare slot: an LDS-DMA load of a column pair whose first slot is the
+  // ring's last lands its second column there (copied to slot 0 afterwards)
+  __shared__ double R[RING + TG_BULGE_GLDS][LDB];
   __shared__ WaveScratch wsc[NCW];
   __shared__ Refl rfl[G_SW][2];
   __shared__ int sh_G;
   __shared__ int sh_dead;  // a wait of this workgroup gave up: no further waits
+  __shared__ unsigned sh_wdone[2];  // write-back half h drained for step number sh_wdone[h] - 1
   // wave index as an SGPR: every role branch below is a scalar (SCC) branch, no exec masks
   const int tid = threadIdx.x, wlane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -453,6 +459,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     const unsigned chosen = expect == 0 ? x + 1 : expect;
     sh_G = (chosen == x + 1) ? 0 : -1;
     sh_dead = 0;
+    sh_wdone[0] = sh_wdone[1] = 0;
   }
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(sh_G) < 0) return;  // uniform: no exec-masked kernel body
@@ -463,7 +470,12 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   constexpr int SC1 = 16;                 // cache policy bit of the L1-bypassing loads
   constexpr int NTC = LDB / 2;            // 16-B chunks per column
   constexpr int PFN = SB_B * NTC / BT + 1;  // chunks per thread of a whole-workgroup load
-  constexpr int PW = SB_B * NTC / 64;       // chunks per lane of the loader wave
+  // halves of each step's write-back (NH) and load (NHL), 1 KB blocks by parity
+  constexpr int NH = (TG_BULGE_SPLIT & 1) ? 2 : 1;
+  constexpr int NHL = (TG_BULGE_SPLIT & 2) ? 2 : 1;
+  constexpr int NBLK = SB_B * NTC / 64;  // 1 KB blocks per step's load
+  constexpr int PW = NBLK / NHL;         // blocks (chunks per lane) of one load half
+  unsigned nstep = 0;  // steps this workgroup has run over all its groups (sh_wdone's clock)
   while (true) {
     if (wid == 0) {
       // a stalled launch: stop taking groups (the results are poisoned anyway)
@@ -532,9 +544,121 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     for (int t = 0; t < total; ++t) {
       BSTAMP(c0t)
       HB(1)
+      // Transfers of step t, each split in NH halves (64-chunk blocks by parity):
+      // write-back of the columns step t-1 retired (drained, then the last half
+      // to drain publishes t) and the load of the columns step t+1 adds (after
+      // the producer's progress covers them).  One wave moves ~16 KB per
+      // ~1.5 us, so with TG_BULGE_SPLIT the left-block waves (the lightest
+      // tasks) take the second halves: wave 0 stores before its task, wave 3
+      // loads after its task.
+      auto wb_issue = [&](int half) {
+        const int nl = group_low(n, nsw, j0, g, t);
+        // wave-uniform trip count (scalar loop), the tail masked by an if
+        const int lim = (nl - wb) * NTC;
+        for (int b0 = 64 * half; b0 < lim; b0 += 64 * NH) {
+          const int idx = b0 + wlane;
+          if (idx < lim) {
+            const int c = wb + idx / NTC, h = idx % NTC;
+            const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+            const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                   (c * LDB + 2 * h) * 8, 0, 0);
+          }
+        }
+      };
+      auto wb_finish = [&](int half) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (NH == 1) {
+          publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
+        } else {
+          // each half marks its word, then reads the other's: LDS serves one
+          // CU's requests in order, so the later of the two sees both marks
+          // (both publishing the same step is harmless)
+          __hip_atomic_store(&sh_wdone[half], nstep + 1, __ATOMIC_SEQ_CST,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+          const unsigned o = __hip_atomic_load(&sh_wdone[half ^ 1], __ATOMIC_SEQ_CST,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (__builtin_amdgcn_readfirstlane(o) >= nstep + 1)
+            publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
+        }
+      };
+      // the load as two parts (issue after the poll; LDS writes once the data is in)
+      auto load_issue = [&](int half, double2 (&buf)[PW]) -> bool {
+        const int nh = group_high(n, j0, t + 1);
+        if (!(t + 1 < total && nh > ld)) return false;
+        const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
+        if (known < need) {
+          HB(4)
+          // the column loads below issue after the poll has returned
+          known = max(need, wait_wave(need));
+          HB(5)
+        }
+#pragma unroll
+        for (int u = 0; u < PW; ++u) {
+          const int idx = wlane + 64 * (half + NHL * u);
+          const int c = min(ld + idx / NTC, nh - 1), h = idx % NTC;
+          const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
+          buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                                __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+        }
+        return true;
+      };
+      auto load_finish = [&](int half, const double2 (&buf)[PW]) {
+        const int nh = group_high(n, j0, t + 1);
+#pragma unroll
+        for (int u = 0; u < PW; ++u) {
+          const int idx = wlane + 64 * (half + NHL * u);
+          const int c = ld + idx / NTC, h = idx % NTC;
+          if (c < nh) {
+            R[rslot(c)][2 * h] = buf[u].x;
+            R[rslot(c)][2 * h + 1] = buf[u].y;
+          }
+        }
+        HB(10)
+      };
+#if TG_BULGE_GLDS
+      // 1 KB block = a column pair, one global_load_lds_dwordx4 per block
+      // (LDS destination = wave-uniform base + 16 B x lane, so a pair needs
+      // contiguous slots: the spare slot RING takes the wrapped second column)
+      auto load_half = [&](int half) {
+        const int nh = group_high(n, j0, t + 1);
+        if (!(t + 1 < total && nh > ld)) return;
+        const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
+        if (known < need) {
+          HB(4)
+          known = max(need, wait_wave(need));
+          HB(5)
+        }
+        bool wrap = false;
+#pragma unroll
+        for (int u = 0; u < PW; ++u) {
+          const int blk = half + NHL * u;
+          const int c0 = ld + 2 * blk;
+          if (c0 < nh) {  // wave-uniform
+            const int idx = wlane + 64 * blk;
+            const int c = min(ld + idx / NTC, nh - 1), h = idx % NTC;
+            __builtin_amdgcn_global_load_lds(
+                (const void *)(B + (c * LDB + 2 * h)),
+                (__attribute__((address_space(3))) void *)&R[rslot(c0)][0], 16, 0, SC1);
+            wrap |= rslot(c0) == RING - 1 && c0 + 1 < nh;
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wrap) {  // wave-uniform
+          R[0][wlane] = R[RING][wlane];
+        }
+        HB(10)
+      };
+#else
+      auto load_half = [&](int half) {
+        double2 buf[PW];
+        if (load_issue(half, buf)) load_finish(half, buf);
+      };
+#endif
       if (wid < NCW) {
         const int pair = wid / 3, role = wid % 3;
         const int s = t - LAG * pair;
+        if (NH == 2 && wid == 0) wb_issue(1);
         if (pair < g && s >= 0 && s < ntasks(n, j0 + pair)) {
           const int jj = j0 + pair, r1 = jj + 1 + s * SB_B;
           const bool nx = s + 1 < ntasks(n, jj);
@@ -549,67 +673,22 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
         } else if (pair < g && pair > 0 && s == -1 && role == 2) {
           first_refl(R, n, j0 + pair, rfl[pair][(t + 1) & 1]);
         }
+        if (NH == 2 && wid == 0) wb_finish(1);
+        if (NHL == 2 && wid == 3) load_half(1);
       } else if (wid == NCW) {
-#if TG_BULGE_WDEFER
-        // writer: the stores of step t-1 had a step to drain; publish t-1 first
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (t > 0) publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t - 1));
-#endif
         // writer: retire the columns step t-1 left behind, drain, publish t
-        const int nl = group_low(n, nsw, j0, g, t);
-        // wave-uniform trip count (scalar loop), the tail masked by an if
-        const int lim = (nl - wb) * NTC;
-        for (int b0 = 0; b0 < lim; b0 += 64) {
-          const int idx = b0 + wlane;
-          if (idx < lim) {
-            const int c = wb + idx / NTC, h = idx % NTC;
-            const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
-            const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                   (c * LDB + 2 * h) * 8, 0, 0);
-          }
-        }
+        wb_issue(0);
         HB(8)
-#if !TG_BULGE_WDEFER
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
-#endif
+        wb_finish(0);
         HB(9)
       } else {
         // loader: the columns step t + 1 adds
-        const int nh = group_high(n, j0, t + 1);
-        if (t + 1 < total && nh > ld) {
-          const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
-          if (known < need) {
-            HB(4)
-            // the column loads below issue after the poll has returned
-            known = max(need, wait_wave(need));
-            HB(5)
-          }
-          double2 buf[PW];
-#pragma unroll
-          for (int u = 0; u < PW; ++u) {
-            const int idx = wlane + 64 * u;
-            const int c = min(ld + idx / NTC, nh - 1), h = idx % NTC;
-            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
-            buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
-                                  __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
-          }
-#pragma unroll
-          for (int u = 0; u < PW; ++u) {
-            const int idx = wlane + 64 * u;
-            const int c = ld + idx / NTC, h = idx % NTC;
-            if (c < nh) {
-              R[rslot(c)][2 * h] = buf[u].x;
-              R[rslot(c)][2 * h + 1] = buf[u].y;
-            }
-          }
-          HB(10)
-        }
+        load_half(0);
       }
       BSTAMP(c1t)
       HB(2)
       __syncthreads();
+      ++nstep;
       if (t + 1 < total) ld = max(ld, group_high(n, j0, t + 1));
       wb = max(wb, group_low(n, nsw, j0, g, t));
 #if TG_BULGE_STATS

@@ -2,7 +2,7 @@
 # Build A/B variants of libtruncgptq.so that differ in one translation unit's
 # -D switches (development tool; results in gptq-svd_amd/variants/, git-ignored
 # .so files that travel to the GPU box).
-#   tools/build_variants.sh bulge "TG_BULGE_WDEFER=1" "TG_BULGE_PF2=1" ...
+#   tools/build_variants.sh bulge "TG_BULGE_SPLIT=0" "TG_BULGE_SPLIT=3" ...
 # Each argument after the unit is one variant: space-separated NAME=VALUE defines.
 set -e
 HERE=$(cd "$(dirname "$0")/.." && pwd)
