@@ -118,9 +118,6 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 #ifndef TG_BULGE_SPLIT
 #define TG_BULGE_SPLIT 3  // bit 0: wave 0 takes half of the write-back; bit 1: wave 3 half of the load
 #endif
-#ifndef TG_BULGE_GLDS
-#define TG_BULGE_GLDS 0  // the column loads go straight to LDS (global_load_lds_dwordx4)
-#endif
 #ifndef TG_BULGE_STATS
 #define TG_BULGE_STATS 0  // per-step s_memrealtime stamps (build-time: they slow every step)
 #endif
@@ -437,9 +434,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #if TG_BULGE_STATS
   uint64_t sw = 0, stk = 0, sbar = 0, nsteps = 0;
 #endif
-  // one spare slot: an LDS-DMA load of a column pair whose first slot is the
-  // ring's last lands its second column there (copied to slot 0 afterwards)
-  __shared__ double R[RING + TG_BULGE_GLDS][LDB];
+  __shared__ double R[RING][LDB];
   __shared__ WaveScratch wsc[NCW];
   __shared__ Refl rfl[G_SW][2];
   __shared__ int sh_G;
@@ -616,45 +611,10 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
         }
         HB(10)
       };
-#if TG_BULGE_GLDS
-      // 1 KB block = a column pair, one global_load_lds_dwordx4 per block
-      // (LDS destination = wave-uniform base + 16 B x lane, so a pair needs
-      // contiguous slots: the spare slot RING takes the wrapped second column)
-      auto load_half = [&](int half) {
-        const int nh = group_high(n, j0, t + 1);
-        if (!(t + 1 < total && nh > ld)) return;
-        const unsigned need = unsigned(min(group_need(t + 1), ptotal + 1));
-        if (known < need) {
-          HB(4)
-          known = max(need, wait_wave(need));
-          HB(5)
-        }
-        bool wrap = false;
-#pragma unroll
-        for (int u = 0; u < PW; ++u) {
-          const int blk = half + NHL * u;
-          const int c0 = ld + 2 * blk;
-          if (c0 < nh) {  // wave-uniform
-            const int idx = wlane + 64 * blk;
-            const int c = min(ld + idx / NTC, nh - 1), h = idx % NTC;
-            __builtin_amdgcn_global_load_lds(
-                (const void *)(B + (c * LDB + 2 * h)),
-                (__attribute__((address_space(3))) void *)&R[rslot(c0)][0], 16, 0, SC1);
-            wrap |= rslot(c0) == RING - 1 && c0 + 1 < nh;
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (wrap) {  // wave-uniform
-          R[0][wlane] = R[RING][wlane];
-        }
-        HB(10)
-      };
-#else
       auto load_half = [&](int half) {
         double2 buf[PW];
         if (load_issue(half, buf)) load_finish(half, buf);
       };
-#endif
       if (wid < NCW) {
         const int pair = wid / 3, role = wid % 3;
         const int s = t - LAG * pair;
