@@ -1169,9 +1169,16 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
 // Gram-Schmidt twice (GEMMs against the finished columns) over MGS_MAX-column
 // panels, each panel finished by mgs_cols_kernel.
 constexpr int MGS_MAX = 64;
+// Clusters of at most MGS_SMALL columns are re-orthogonalised by
+// mgs_cols_kernel (all at once, one workgroup each); wider ones panel by
+// panel (MGS_MAX columns): block Gram-Schmidt twice against the finished
+// panels, then CholeskyQR2 of the panel (cq_* kernels below) -- MGS within a
+// 64-column panel is 4032 dependent dot/axpy steps over strided rows (88 ms
+// per panel at n = 8192), the panel's Gram matrix is one pass.
+constexpr int MGS_SMALL = 8;
 
 __global__ void cluster_scan_kernel(const double *__restrict__ w_asc, int n, int k, int first,
-                                    const double *__restrict__ bnd, double reltol,
+                                    const double *__restrict__ bnd, double reltol, int small,
                                     int32_t *__restrict__ cl) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const double gap = reltol * bnd[2];
@@ -1181,7 +1188,7 @@ __global__ void cluster_scan_kernel(const double *__restrict__ w_asc, int n, int
     int end = start + 1;
     while (end < k && fabs(wd[-(end - 1)] - wd[-end]) <= gap) ++end;
     if (end - start > 1) {
-      int32_t *dst = end - start <= MGS_MAX ? cl + 2 + 2 * ns++ : cl + 2 + 2 * n + 2 * nb++;
+      int32_t *dst = end - start <= small ? cl + 2 + 2 * ns++ : cl + 2 + 2 * n + 2 * nb++;
       dst[0] = start;
       dst[1] = end - start;
     }
@@ -1193,9 +1200,13 @@ __global__ void cluster_scan_kernel(const double *__restrict__ w_asc, int n, int
 
 // Modified Gram-Schmidt twice ("twice is enough") over the columns
 // [start, start + len) of Z (n x k), one workgroup per (start, len) entry.
+// With `only_if` non-null it runs only when *only_if != 0 (the fallback of a
+// panel whose CholeskyQR2 was refused).
 __global__ __launch_bounds__(256) void mgs_cols_kernel(const int32_t *__restrict__ list, int n,
-                                                       int k, double *__restrict__ Z) {
+                                                       int k, double *__restrict__ Z,
+                                                       const int *__restrict__ only_if) {
   __shared__ double scratch[8];
+  if (only_if && *only_if == 0) return;
   const int start = list[2 * blockIdx.x], end = start + list[2 * blockIdx.x + 1];
   for (int c = start; c < end; ++c) {
     for (int pass = 0; pass < 2; ++pass)
@@ -1212,6 +1223,134 @@ __global__ __launch_bounds__(256) void mgs_cols_kernel(const int32_t *__restrict
     const double inv = 1.0 / sqrt(nrm);
     for (int i = threadIdx.x; i < n; i += blockDim.x) Z[size_t(i) * k + c] *= inv;
     __syncthreads();
+  }
+}
+
+// CholeskyQR2 of the panel P = Z[:, p0 : p0 + pw] (pw <= MGS_MAX), in place:
+// twice { G = P^T P (partials over row blocks, summed in a fixed order),
+// G = R^T R, P <- P R^-1 }.  Q = P R^-1 spans the same leading columns as P
+// (R upper triangular), as Gram-Schmidt's result does.  A round whose
+// Cholesky meets a column with less than 1e-5 of its norm left after the
+// previous columns (kappa too large for two rounds) sets *bad and every later
+// step of the panel is skipped; mgs_cols_kernel then takes the panel.
+constexpr int CQ_ROWS = 32;  // rows staged per LDS round of the Gram kernel
+
+__global__ __launch_bounds__(256) void cq_gram_kernel(const double *__restrict__ Z, int n, int k,
+                                                      int p0, int pw, int rows_per,
+                                                      const int *__restrict__ bad,
+                                                      double *__restrict__ part) {
+  __shared__ double S[CQ_ROWS][MGS_MAX + 1];
+  if (*bad) return;
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * rows_per, r1 = min(n, r0 + rows_per);
+  double acc[16];  // entry idx = tid + 256 q: (a, b) = (idx / 64, idx % 64)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+  for (int rb = r0; rb < r1; rb += CQ_ROWS) {
+    for (int idx = tid; idx < CQ_ROWS * MGS_MAX; idx += 256) {
+      const int rr = idx / MGS_MAX, c = idx % MGS_MAX, r = rb + rr;
+      S[rr][c] = (r < r1 && c < pw) ? Z[size_t(r) * k + p0 + c] : 0.0;
+    }
+    __syncthreads();
+    for (int rr = 0; rr < CQ_ROWS; ++rr) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int idx = tid + 256 * q;
+        acc[q] += S[rr][idx / MGS_MAX] * S[rr][idx % MGS_MAX];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) part[size_t(blockIdx.x) * MGS_MAX * MGS_MAX + tid + 256 * q] = acc[q];
+}
+
+// Sum of the partials, Cholesky G = R^T R (upper, right-looking), R^-1 by
+// column (one thread per column, back substitution) -> Rinv (row-major 64 x 64).
+__global__ __launch_bounds__(256) void cq_chol_kernel(const double *__restrict__ part, int nparts,
+                                                      int pw, double *__restrict__ Rinv,
+                                                      int *__restrict__ bad) {
+  __shared__ double G[MGS_MAX][MGS_MAX + 1];
+  __shared__ double d0[MGS_MAX];
+  __shared__ int sbad;
+  if (*bad) return;
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < MGS_MAX * MGS_MAX; idx += 256) {
+    double sum = 0.0;
+    for (int p = 0; p < nparts; ++p) sum += part[size_t(p) * MGS_MAX * MGS_MAX + idx];
+    G[idx / MGS_MAX][idx % MGS_MAX] = sum;
+  }
+  if (tid == 0) sbad = 0;
+  __syncthreads();
+  if (tid < pw) d0[tid] = G[tid][tid];
+  __syncthreads();
+  for (int j = 0; j < pw; ++j) {
+    if (tid == 0) {
+      const double dj = G[j][j];
+      if (!(dj > 1e-10 * d0[j]) || !(d0[j] > 0.0)) sbad = 1;
+      G[j][j] = sqrt(fmax(dj, 1e-300));
+    }
+    __syncthreads();
+    if (tid > j && tid < pw) G[j][tid] /= G[j][j];
+    __syncthreads();
+    for (int idx = tid; idx < MGS_MAX * MGS_MAX; idx += 256) {
+      const int a = idx / MGS_MAX, b = idx % MGS_MAX;
+      if (a > j && b >= a && b < pw) G[a][b] -= G[j][a] * G[j][b];
+    }
+    __syncthreads();
+  }
+  if (sbad) {
+    if (tid == 0) *bad = 1;
+    return;
+  }
+  // column c of R^-1: x_c = 1 / R_cc, x_i = -(sum_{j = i+1..c} R_ij x_j) / R_ii
+  if (tid < MGS_MAX) {
+    const int c = tid;
+    double x[MGS_MAX];
+#pragma unroll
+    for (int i = 0; i < MGS_MAX; ++i) x[i] = 0.0;
+    if (c < pw) {
+      x[c] = 1.0 / G[c][c];
+      for (int i = c - 1; i >= 0; --i) {
+        double acc = 0.0;
+        for (int j = i + 1; j <= c; ++j) acc += G[i][j] * x[j];
+        x[i] = -acc / G[i][i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MGS_MAX; ++i) Rinv[i * MGS_MAX + c] = i <= c ? x[i] : 0.0;
+  }
+}
+
+// P <- P R^-1, one row per thread: out[j] = sum_{b <= j} P[r][b] Rinv[b][j].
+__global__ __launch_bounds__(256) void cq_apply_kernel(double *__restrict__ Z, int n, int k, int p0,
+                                                       int pw, const double *__restrict__ Rinv,
+                                                       const int *__restrict__ bad) {
+  __shared__ double Ri[MGS_MAX][MGS_MAX];
+  if (*bad) return;
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < MGS_MAX * MGS_MAX; idx += 256) Ri[idx / MGS_MAX][idx % MGS_MAX] = Rinv[idx];
+  __syncthreads();
+  const int r = blockIdx.x * 256 + tid;
+  if (r >= n) return;
+  double *row = Z + size_t(r) * k + p0;
+  // 16 outputs at a time, last block first: block jb reads row[b] only for
+  // b < 16 (jb + 1), none of which a later-written block has touched (Rinv
+  // is zero below its diagonal, so the sums need no b <= j test)
+  for (int jb = MGS_MAX / 16 - 1; jb >= 0; --jb) {
+    if (jb * 16 >= pw) continue;
+    double out[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) out[jj] = 0.0;
+    const int bmax = min(pw, jb * 16 + 16);
+    for (int b = 0; b < bmax; ++b) {
+      const double zb = row[b];
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) out[jj] += zb * Ri[b][jb * 16 + jj];
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+      if (jb * 16 + jj < pw) row[jb * 16 + jj] = out[jj];
   }
 }
 
@@ -1496,14 +1635,19 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   {
     const char *ot = getenv("TG_INVIT_ORTOL");
     const double ortol = ot ? atof(ot) : 1e-6;
+    // panel path: X (p x pw) + Gram partials + Rinv + flag in w.lu (3 n^2 doubles)
+    const int cq_np = std::max(1, std::min(64, n / 256));
+    const size_t cq_need = size_t(k) * MGS_MAX + size_t(cq_np + 1) * MGS_MAX * MGS_MAX + 1;
+    const bool cq = cq_need <= 3 * size_t(n) * n && !getenv("TG_ORTH_MGS");  // (tests set it)
     hipLaunchKernelGGL(cluster_scan_kernel, dim3(1), dim3(64), 0, st, w_asc, n, k, first, bnd,
-                       ortol, w.cl);
+                       ortol, cq ? MGS_SMALL : MGS_MAX, w.cl);
     TG_LAUNCHED();
     int32_t cnt[2] = {0, 0};
     TG_HIP(hipMemcpyAsync(cnt, w.cl, sizeof(cnt), hipMemcpyDeviceToHost, st));
     TG_HIP(hipStreamSynchronize(st));
     if (cnt[0] > 0) {
-      hipLaunchKernelGGL(mgs_cols_kernel, dim3(cnt[0]), dim3(256), 0, st, w.cl + 2, n, k, w.Z);
+      hipLaunchKernelGGL(mgs_cols_kernel, dim3(cnt[0]), dim3(256), 0, st, w.cl + 2, n, k, w.Z,
+                         nullptr);
       TG_LAUNCHED();
     }
     if (cnt[1] > 0) {
@@ -1522,6 +1666,11 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
       TG_HIP(hipMemcpyAsync(plist, pan.data(), sizeof(int32_t) * pan.size(),
                             hipMemcpyHostToDevice, st));
       double *X = w.lu;  // (cluster columns done) x MGS_MAX scratch
+      double *part = X + size_t(k) * MGS_MAX;
+      double *Rinv = part + size_t(cq_np) * MGS_MAX * MGS_MAX;
+      int *bad = reinterpret_cast<int *>(Rinv + MGS_MAX * MGS_MAX);
+      const int rows_per = tg::cdiv(tg::cdiv(n, cq_np), CQ_ROWS) * CQ_ROWS;
+      const int np = tg::cdiv(n, rows_per);
       int e = 0;
       for (int c = 0; c < cnt[1]; ++c) {
         const int cs = big[2 * c], cl = big[2 * c + 1];
@@ -1533,7 +1682,18 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
             TG_HIP(tg::dgemm(st, false, false, n, pw, p, -1.0, w.Z + cs, k, X, pw, 1.0, w.Z + p0,
                              k));
           }
-          hipLaunchKernelGGL(mgs_cols_kernel, dim3(1), dim3(256), 0, st, plist + 2 * e, n, k, w.Z);
+          if (cq) {
+            TG_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+            for (int round = 0; round < 2; ++round) {
+              hipLaunchKernelGGL(cq_gram_kernel, dim3(np), dim3(256), 0, st, w.Z, n, k, p0, pw,
+                                 rows_per, bad, part);
+              hipLaunchKernelGGL(cq_chol_kernel, dim3(1), dim3(256), 0, st, part, np, pw, Rinv, bad);
+              hipLaunchKernelGGL(cq_apply_kernel, dim3(tg::cdiv(n, 256)), dim3(256), 0, st, w.Z, n,
+                                 k, p0, pw, Rinv, bad);
+            }
+          }
+          hipLaunchKernelGGL(mgs_cols_kernel, dim3(1), dim3(256), 0, st, plist + 2 * e, n, k, w.Z,
+                             cq ? bad : nullptr);
           TG_LAUNCHED();
         }
       }

@@ -50,6 +50,7 @@ def rel(a, b):
     {"TG_XM_NBC": "2"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
+    {"TG_ORTH_MGS": "1"},
 ], ids=lambda d: "+".join(f"{k}={v}" for k, v in d.items()))
 def test_switch_matches_default(problem, path, switches, monkeypatch):
     g, H, W = problem
