@@ -22,6 +22,7 @@ Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import logging
 import os
 import sys
 import time
@@ -74,7 +75,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-syrk", action="store_true")
     p.add_argument("--no-large-n", action="store_true",
-                   help="skip the n = 12288 / 14336 solve timings in the extras")
+                   help="skip the n = 8192 / 12288 / 14336 / 28672 solve timings in the extras")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the end-to-end Qwen3-8B-shaped quantize wall-clock")
+    p.add_argument("--e2e-layers", type=int, default=36)
+    p.add_argument("--e2e-samples", type=int, default=128)
     return p.parse_args()
 
 
@@ -187,15 +192,16 @@ def syrk_bench(g, args, device):
 
 
 def large_n(g, args, device):
-    """The real models' down_proj widths (Qwen3-8B n = 12288, Llama-3-8B
-    n = 14336): process_hessian_alt + quantize on a synthetic H of 3n/4
+    """The real models' widths (Llama-3-70B q/o n = 8192, Qwen3-8B down
+    n = 12288, Llama-3-8B down n = 14336, Llama-3-70B down n = 28672):
+    process_hessian_alt + quantize on a synthetic H of 3n/4
     calibration rows (as tests/test_gpu_fullsize.py), one warm-up solve and
     one timed, with phases; at n = 12288 also the TSQR band reduction
     (TG_SB_TSQR=1, the round-1 path these widths took before) for the
     eigenvalue phase it changes."""
     import copy
     out = {}
-    for n in (12288, 14336):
+    for n in (8192, 12288, 14336, 28672):
         torch.manual_seed(1)
         acc = g.HessianAccumulator(n, device)
         acc.add_batch(torch.randn(3 * n // 4, n, device=device).half())
@@ -204,22 +210,128 @@ def large_n(g, args, device):
         a2 = copy.copy(args)
         a2.n, a2.m = n, 4096
         W = torch.randn(a2.m, n, device=device)
-        phases(g, H, W, a2)
+        if n < 28672:  # one warm-up solve (the 28,672 one is seconds long and warm anyway)
+            phases(g, H, W, a2)
         ph, k = phases(g, H, W, a2)
         ent = dict(rank_k=k, path=phases.path, solve_ms=round(sum(ph.values()), 3), phases_ms=ph)
         if n == 12288:
+            prev = os.environ.get("TG_SB_TSQR")
             os.environ["TG_SB_TSQR"] = "1"
             try:
                 phases(g, H, W, a2)
                 ph2, _ = phases(g, H, W, a2)
             finally:
-                del os.environ["TG_SB_TSQR"]
+                if prev is None:
+                    del os.environ["TG_SB_TSQR"]
+                else:
+                    os.environ["TG_SB_TSQR"] = prev
             ent["tsqr_band_reduction"] = dict(solve_ms=round(sum(ph2.values()), 3),
                                               eigh_values_ms=ph2["eigh_values"])
         out[f"n{n}"] = ent
         del H, W
         torch.cuda.empty_cache()
     return out
+
+
+QWEN3_8B = dict(vocab_size=151936, hidden_size=4096, intermediate_size=12288,
+                num_hidden_layers=36, num_attention_heads=32, num_key_value_heads=8, head_dim=128,
+                max_position_embeddings=40960, rope_theta=1000000.0, rms_norm_eps=1e-6,
+                tie_word_embeddings=False)
+
+
+def e2e_qwen3_shape(args, device):
+    """The second half of BASELINE.json's metric: end-to-end quantize
+    wall-clock of a Qwen3-8B-shaped model (the reference's `metrics.total_time`,
+    quantize.py:101, :257-260 -- 1522-1534 s on A100).  No
+    weights exist in this image, so the model is random-init (fp16, N(0, 0.02)
+    linears, unit norms) with Qwen3-8B's exact `Qwen3Config` dimensions, fed
+    128 random 2048-token sequences (the reference's n_samples x seq_len) in
+    batches of 32 (run_benchmark.py:111-127): every stage runs at production
+    shape -- calibration forwards, SYRK at N = 262,144 for n = 4096 and
+    12,288, four solves and seven gptq_fwrd per layer, the re-forward.
+    Settings: eigh, 4-bit asym g128, eps 1e-4 energy (BASELINE configs[3]'s
+    solver path; the rank k depends on the random activations).  Timing only:
+    the weights are random, so no PPL."""
+    from transformers import Qwen3Config, Qwen3ForCausalLM
+    from gptq_svd_amd import harness
+    cfg = Qwen3Config(**dict(QWEN3_8B, num_hidden_layers=args.e2e_layers))
+    cfg._attn_implementation = "sdpa"
+    t0 = time.perf_counter()
+    with torch.device("meta"):
+        model = Qwen3ForCausalLM(cfg)
+    model = model.to(dtype=torch.float16).to_empty(device=device)
+    gen = torch.Generator(device=device).manual_seed(0)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if p.dim() == 2:
+                p.normal_(0.0, 0.02, generator=gen)
+            else:
+                p.fill_(1.0)
+        model.model.rotary_emb = type(model.model.rotary_emb)(config=cfg, device=device)
+    model.eval()
+    ids = torch.randint(0, cfg.vocab_size, (args.e2e_samples, 2048), generator=gen,
+                        device=device).cpu()
+    ids = [ids[i:i + 1] for i in range(ids.shape[0])]
+    torch.cuda.synchronize()
+    t_init = time.perf_counter() - t0
+    clock = harness.StageClock()
+    # one progress line per layer on stderr (a long run must not look hung)
+    log = logging.getLogger()
+    hd = logging.StreamHandler(sys.stderr)
+    hd.addFilter(lambda r: "completed in" in r.getMessage())
+    old_level = log.level
+    log.addHandler(hd)
+    log.setLevel(logging.INFO)
+    try:
+        res = harness.quantize_model(model, ids, mode="eigh", w_bits=4, group_size=128,
+                                     sym=False, eps=1e-4, threshold_method="energy",
+                                     batch_size=32, device=device, clock=clock)
+    finally:
+        log.removeHandler(hd)
+        log.setLevel(old_level)
+    stages = {k: round(v, 3) for k, v in sorted(clock.totals().items())}
+    ranks = {}
+    for st in res["layer_stats"]:
+        nm = st["name"].split(".", 1)[1]
+        ranks.setdefault(nm, []).append(st["rank"])
+    med = {nm: int(sorted(v)[len(v) // 2]) for nm, v in ranks.items()}
+    del model
+    torch.cuda.empty_cache()
+    return dict(total_s=round(res["total_time"], 2), layers=args.e2e_layers,
+                samples=args.e2e_samples, seq_len=2048, batch_size=32,
+                stages_s=stages, stage_counts=dict(sorted(clock.counts.items())),
+                median_rank=med, model_init_s=round(t_init, 2),
+                reference_total_s="1522-1534 (A100 40GB, real weights, 36 layers)",
+                note="random-init weights with Qwen3-8B's dimensions: timing only, no PPL")
+
+
+def ar1_solve(g, args, device):
+    """SURVEY.md §8(d)'s second synthetic distribution, timed like the main
+    layer: X = Z L^T with L L^T the AR(1) rho = 0.9 covariance + 1e-6 I
+    (gaussian_corr, benchmarks.py:18-28, :50-54), 3072 x 4096 fp16 rows;
+    k ~ 2982 at eps 1e-4 in the survey's run."""
+    n = args.n
+    idx = torch.arange(n, device=device)
+    Sigma = 0.9 ** (idx[None, :] - idx[:, None]).abs().double()
+    L = torch.linalg.cholesky(Sigma + 1e-6 * torch.eye(n, dtype=torch.float64, device=device))
+    gen = torch.Generator(device=device).manual_seed(7)
+    X = (torch.randn(args.tokens, n, generator=gen, device=device) @ L.float().T).half()
+    acc = g.HessianAccumulator(n, device)
+    acc.add_batch(X)
+    H = acc.get_hessian()
+    W = torch.randn(args.m, n, generator=gen, device=device)
+    del acc, X, L, Sigma
+    solve(g, H, W, args)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        k, _ = solve(g, H, W, args)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    ph, _ = phases(g, H, W, args)
+    return dict(rank_k=k, ms_per_solve=round(ms, 3), cols_per_s=round(n / ms * 1e3, 1),
+                path=phases.path, phases_ms=ph)
 
 
 def cpu_baseline(H, W, args):
@@ -433,6 +545,8 @@ def run(args):
         extra["phases_ms"] = ph
         extra["spectral_path"] = phases.path
         extra["kernel_ms_per_step"] = shares
+        if (args.n, args.m) == (4096, 4096):
+            extra["ar1_rho0.9"] = ar1_solve(g, args, device)
         pm = pmc_summary(args)
         if pm:
             extra["pmc_hbm"] = pm
@@ -440,6 +554,11 @@ def run(args):
             extra["syrk"] = syrk_bench(g, args, device)
         if not args.no_large_n and (args.n, args.m) == (4096, 4096):
             extra["large_n"] = large_n(g, args, device)
+        if not args.no_e2e and world == 1:
+            try:
+                extra["e2e_qwen3_8b_shape"] = e2e_qwen3_shape(args, device)
+            except Exception as exc:  # the solver line stands without it
+                extra["e2e_qwen3_8b_shape"] = dict(error=f"{type(exc).__name__}: {exc}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(H, W, args)

@@ -25,6 +25,7 @@
 //  3. Fallback (rank-deficient or numerically singular panels, m < 64):
 //     Householder column by column over the grid, one barrier per column
 //     (one reduction gives the column norm and every w = P^T v entry).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -1007,7 +1008,29 @@ namespace tg {
 // One row per thread, 256 rows per workgroup, every workgroup resident (one
 // per CU: the row block and the factor tiles fill its LDS): panels of up to
 // 256 x 256 rows (n <= 65,568), the largest down_proj (n = 28,672) needs 112.
-int pqr_rows_per_thread(int m) { return m <= PQR_NWMAX * PT ? 1 : 0; }
+// The workers meet at grid barriers, so all cdiv(m, PT) of them must be
+// resident at once: the single-level path is only taken when they fit the
+// device's CUs at the kernel's occupancy (a smaller device or partition falls
+// back to the TSQR band reduction instead of stalling into the spin timeout).
+static int pqr_resident_workers() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cached[dev] == 0) {
+    int ncu = 0, occ = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pqr_kernel, PT, 0) != hipSuccess)
+      occ = 0;
+    cached[dev] = std::max(0, ncu) * std::max(0, occ);
+    if (cached[dev] == 0) cached[dev] = -1;
+  }
+  return std::max(0, cached[dev]);
+}
+
+int pqr_rows_per_thread(int m) {
+  return m <= PQR_NWMAX * PT && cdiv(m, PT) <= pqr_resident_workers() ? 1 : 0;
+}
 
 hipError_t panel_qr(hipStream_t st, double *A, int lda, int p, int r0, int m, double *Y,
                     double *YT, double *T, double *part, double *bc, unsigned *cnt,

@@ -12,6 +12,10 @@ the dequantised weight back; then re-run the calibration batches through the
 quantised layer to produce the next layer's inputs.
 
 What differs, deliberately:
+* a calibration pass stops each batch at the group's first linear (a
+  forward pre-hook accumulates its input and ends the pass): the reference
+  runs the whole layer and throws the output away (quantize.py:139-148), so
+  H is the same and the layer's remaining work is skipped;
 * no ``cleanup()`` (gc + empty_cache + device synchronize) after every batch
   and every module (quantize.py:28-35): activations and H stay resident and
   the work is stream-ordered -- 288 GB of HBM holds a whole layer's
@@ -31,7 +35,8 @@ What differs, deliberately:
   is the all-reduce (SUM) of the ranks' FP64 sums x^T x and sample counts,
   divided by the total count -- the single-process H up to the order of the
   FP64 additions; every rank factorises that H (the solver is
-  deterministic, so every rank holds the same U, perm); each linear's rows
+  deterministic, so every rank holds the same U, perm -- checked by a
+  fingerprint reduction before any row is quantised); each linear's rows
   are quantised by their owning rank (``dist.shard_rows``; rows are
   independent given U and perm) and all-gathered, so every rank writes the
   same dequantised weight.  The reference places a 70B model's layers
@@ -53,7 +58,7 @@ from .gptq_utils import (HessianAccumulator, Quantizer, gptq_fwrd, log_quantizat
                          pack_quantized, process_hessian, process_hessian_alt)
 
 __all__ = ["get_layers", "get_sequenced_groups", "capture_initial_inputs", "quantize_model",
-           "adaptive_eps"]
+           "adaptive_eps", "StageClock", "check_factor_agrees"]
 
 
 def get_layers(model: nn.Module) -> nn.ModuleList:
@@ -128,6 +133,35 @@ class _Stop(Exception):
     pass
 
 
+class StageClock:
+    """Per-stage device time of the layer loop, from HIP events recorded on
+    the current stream (no host sync until ``totals()``).  Stage names:
+    capture, calib_forward, syrk, allreduce, factor_n<n>, quantize,
+    reforward; ``calib_forward`` excludes the SYRK launches inside it."""
+
+    def __init__(self):
+        self._spans: Dict[str, list] = {}
+        self.counts: Dict[str, int] = {}
+
+    def start(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, name: str, ev0) -> None:
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self._spans.setdefault(name, []).append((ev0, ev1))
+        self.counts[name] = self.counts.get(name, 0) + 1
+
+    def totals(self) -> Dict[str, float]:
+        torch.cuda.synchronize()
+        out = {k: sum(a.elapsed_time(b) for a, b in v) / 1e3 for k, v in self._spans.items()}
+        if "calib_forward" in out and "syrk" in out:
+            out["calib_forward"] -= out["syrk"]
+        return out
+
+
 def capture_initial_inputs(model: nn.Module, input_ids_list: Sequence[torch.Tensor],
                            device="cuda", batch_size: int = 1):
     """Inputs of the first decoder layer for every calibration sequence, plus
@@ -189,6 +223,31 @@ def allreduce_hessian(acc, pg=None) -> None:
     acc.n_samples = int(tgdist.all_reduce_sum(cnt, pg).item())
 
 
+def check_factor_agrees(R: torch.Tensor, perm: torch.Tensor, pg=None) -> None:
+    """Every rank factorises the same all-reduced H and must hold the same
+    (U, perm, k); rows quantised with different factors would be stitched
+    into one weight silently.  A fingerprint (k, a position-weighted sum of
+    perm, sum and sum of squares of U) is reduced by MIN and MAX; any
+    difference raises on every rank."""
+    import torch.distributed as dist
+    world, _ = _world(pg)
+    if world == 1:
+        return
+    n = perm.numel()
+    pos = torch.arange(1, n + 1, dtype=torch.float64, device=perm.device)
+    Rd = R.to(torch.float64)
+    fp = torch.stack([torch.tensor(float(R.shape[0]), dtype=torch.float64, device=R.device),
+                      (perm.to(torch.float64) * pos).sum(), Rd.sum(), (Rd * Rd).sum()])
+    lo, hi = fp.clone(), fp.clone()
+    if fp.is_cuda and dist.get_backend(pg) == "gloo":
+        lo, hi = lo.cpu(), hi.cpu()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=pg)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=pg)
+    if not torch.equal(lo, hi):
+        raise RuntimeError("ranks disagree on the factorisation of the shared Hessian "
+                           f"(fingerprint min {lo.tolist()} max {hi.tolist()})")
+
+
 def quantize_linear_sharded(W: torch.Tensor, R: torch.Tensor, perm: torch.Tensor,
                             w_bits: int, group_size: int, sym: bool, block_size: int,
                             use_triton: bool, pg=None):
@@ -224,7 +283,8 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
                    threshold_method: str = "mean_trimmed", actorder: bool = False,
                    damp_percent: float = 0.01, use_adaptive_eps: bool = False,
                    batch_size: int = 8, device="cuda", block_size: int = 1024,
-                   pack: bool = False, offload: bool = False, pg=None) -> Dict[str, Any]:
+                   pack: bool = False, offload: bool = False, pg=None, early_stop: bool = True,
+                   clock: Optional[StageClock] = None) -> Dict[str, Any]:
     """Quantise every sequenced linear of `model` in place (layer by layer).
 
     mode "eigh" = TruncGPTQ (process_hessian_alt + gptq_fwrd(use_triton=True));
@@ -234,6 +294,11 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     the model stays where it is (a whole 8B/70B model fits in 288 GB).
     `pg`: process group of the multi-GPU mode (module docstring); it is on
     whenever torch.distributed is initialised with more than one rank.
+    `early_stop`: a calibration pass ends each batch at the group's first
+    linear -- its input is accumulated into H, then the rest of the layer is
+    skipped (the reference runs the whole layer and discards the output,
+    quantize.py:139-148, so H is the same).  `clock`: a StageClock that
+    receives per-stage device times.
     Returns {"layer_stats": [...], "total_time": s, "packed": {name: tensors}}.
     """
     if mode not in ("eigh", "gptq"):
@@ -241,11 +306,17 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     t_start = time.time()
     world, rank = _world(pg)
     if world > 1:
-        input_ids_list = list(input_ids_list)[rank::world]
-        if not input_ids_list:
-            raise ValueError(f"rank {rank}: fewer calibration sequences than ranks ({world})")
+        input_ids_list = list(input_ids_list)
+        # the same test on every rank, so all of them raise together
+        if len(input_ids_list) < world:
+            raise ValueError(f"fewer calibration sequences ({len(input_ids_list)}) than ranks "
+                             f"({world})")
+        input_ids_list = input_ids_list[rank::world]
+    ev = clock.start() if clock else None
     inps, layer_kwargs = capture_initial_inputs(model, input_ids_list, device=device,
                                                 batch_size=batch_size)
+    if clock:
+        clock.stop("capture", ev)
     kw = {k: _to(v, device) for k, v in layer_kwargs.items()}
     kw["use_cache"] = False
     outs = torch.zeros_like(inps)
@@ -262,10 +333,24 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
             x = inps[j: j + batch_size]
             kwb = kw if x.shape[0] == cap else {k: _batch_slice(v, cap, x.shape[0])
                                                  for k, v in kw.items()}
-            out = layer(x, **kwb)
+            try:
+                out = layer(x, **kwb)
+            except _Stop:
+                continue
             if dst is not None:
                 out = out[0] if isinstance(out, (tuple, list)) else out
                 dst[j: j + out.shape[0]] = out
+
+    def accumulate(acc):
+        def hook(mod, args, kwargs):
+            x = args[0] if args else kwargs["input"]
+            ev = clock.start() if clock else None
+            acc.add_batch(x.detach())
+            if clock:
+                clock.stop("syrk", ev)
+            if early_stop:
+                raise _Stop
+        return hook
 
     for i, layer in enumerate(layers):
         t_layer = time.time()
@@ -276,12 +361,19 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
             cur_eps = adaptive_eps(names[0], eps) if use_adaptive_eps else eps
             first = _submodule(layer, names[0])
             acc = HessianAccumulator(first.weight.shape[1], device=device)
-            hook = first.register_forward_hook(lambda m, a, o: acc.add_batch(a[0].detach()))
+            hook = first.register_forward_pre_hook(accumulate(acc), with_kwargs=True)
+            ev = clock.start() if clock else None
             try:
                 run_layer(layer, None)
             finally:
                 hook.remove()
+            if clock:
+                clock.stop("calib_forward", ev)
+                ev = clock.start()
             allreduce_hessian(acc, pg)
+            if clock and world > 1:
+                clock.stop("allreduce", ev)
+                ev = clock.start()
             H = acc.get_hessian()
             del acc
             if mode == "eigh":
@@ -290,7 +382,12 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
             else:
                 R, perm = process_hessian(H, actorder=actorder, damp_percent=damp_percent)
                 R_x = None
+            if clock:
+                clock.stop(f"factor_n{H.shape[0]}", ev)
             del H
+            if world > 1:
+                check_factor_agrees(R, perm, pg)
+            ev = clock.start() if clock else None
             for name in names:
                 sub = _submodule(layer, name)
                 q = Quantizer(w_bits=w_bits, group_size=group_size, sym=sym)
@@ -313,8 +410,13 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
                 used = k if mode == "eigh" else "N/A"
                 logging.info(f"   {name: <15} | Rank: {str(used): <4} | Time: {dt:.2f}s")
                 stats.append({"name": full, "rank": used, "time": dt})
+            if clock:
+                clock.stop("quantize", ev)
             del R, R_x, perm
+        ev = clock.start() if clock else None
         run_layer(layer, outs)
+        if clock:
+            clock.stop("reforward", ev)
         inps, outs = outs, inps
         if offload:
             layers[i] = layer.to("cpu")

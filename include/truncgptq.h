@@ -28,7 +28,9 @@ int tg_version(void);
 
 /* Sampled HIP-event timing of the hot kernel classes (for bench roofline
  * reporting).  Classes: 0 tri_symv, 1 cross_gemm, 2 quant_block, 3 tri_syr2k,
- * 4 pivot_step, 5 bisect, 6 inverse_iteration, 7 back_transform.
+ * 4 pivot_step, 5 bisect, 6 inverse_iteration, 7 back_transform, 8 bulge_chase,
+ * 9 tsqr_leaf (the panel QR kernels), 10 band_update, 11 q1_apply, 12 q2_apply
+ * (the order of PROF_CLASSES in gptq-svd_amd/_lib.py).
  * tg_profile_query synchronises on the recorded events. */
 int tg_profile_enable(int on, int every);
 int tg_profile_reset(void);

@@ -104,6 +104,51 @@ def test_fullsize_end_to_end(g, bench_layer, oracle_mod):
     assert mism <= 6e-4
 
 
+@pytest.fixture(scope="module")
+def ar1_layer(g, oracle_mod):
+    """SURVEY.md §8(d)'s second synthetic distribution at full size:
+    gaussian_corr, AR(1) rho = 0.9 (benchmarks.py:18-28, :50-54), 3072 x 4096
+    fp16 rows, eps 1e-4 energy (k ~ 2982 in the survey's run)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from synth import make_x
+    n = m = 4096
+    X = make_x("ar1", 3072, n, torch.Generator().manual_seed(5))
+    acc = g.HessianAccumulator(n, DEV)
+    acc.add_batch(X.to(DEV))
+    H = acc.get_hessian()
+    W = torch.randn(m, n, generator=torch.Generator().manual_seed(6))
+    f = oracle_mod.process_hessian_alt(H.cpu().numpy(), 1e-4, "energy")
+    return H, W, f
+
+
+@pytest.mark.parametrize("path", ["kept", "complement"])
+def test_fullsize_ar1_factor(g, ar1_layer, path, monkeypatch):
+    monkeypatch.setenv("TG_SPECTRAL_PATH", path)
+    H, _, f = ar1_layer
+    U, R_x, perm, S, k = g.truncated_spectral_factor(H, 1e-4, "energy")
+    print(f"AR(1) 4096^2: k = {k}")
+    assert g.truncated_spectral_factor.last_path[0] == path
+    assert k == f.k and 2900 <= k <= 3072
+    assert np.array_equal(perm.cpu().numpy(), f.perm)
+    assert rel(S.cpu().numpy(), f.S) <= 1e-12
+    assert rel(U.cpu().numpy(), f.U) <= 1e-8
+    assert rel(R_x.cpu().numpy(), f.R_x) <= 1e-8
+
+
+def test_fullsize_ar1_end_to_end(g, ar1_layer, oracle_mod):
+    H, W, f = ar1_layer
+    R, R_x, perm = g.process_hessian_alt(H, 1e-4, "energy")
+    q = g.Quantizer(4, 128, False)
+    Wq, k = g.gptq_fwrd(W.to(DEV), R, q, perm, block_size=1024)
+    ref, _ = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 4, 128, False, 1024,
+                                  gemm="torch", impl="c", nthreads=16)
+    mism = float(np.mean(Wq.cpu().numpy() != ref))
+    print(f"AR(1) 4096^2 end-to-end code mismatch vs oracle (MKL order): {mism:.2e}")
+    assert mism <= 6e-4
+
+
 @pytest.mark.parametrize("n,path", [(8192, "kept"), (8192, "complement"), (12288, "complement"),
                                     (14336, "complement"), (14336, "kept"),
                                     (28672, "complement"), (28672, "kept")])

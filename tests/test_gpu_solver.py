@@ -207,7 +207,7 @@ def test_end_to_end_golden(g, name, path, monkeypatch):
     Wq, k = g.gptq_fwrd(t(d["W"]), R, q, perm, block_size=int(d["block_size"]), R_x=R_x)
     mism = float(np.mean(Wq.cpu().numpy() != d["final_W"]))
     print(f"{name}: code mismatch vs reference {mism:.2e}")
-    assert mism <= 2e-3
+    assert mism <= 6e-4  # the reference's own Triton-vs-loop disagreement
 
 
 def test_bulge_stall_reported(lib, monkeypatch):
