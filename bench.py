@@ -169,7 +169,11 @@ def phases(g, H, W, args):
 
 
 def syrk_bench(g, args, device):
-    """Hessian accumulation (A1), reported separately."""
+    """Hessian accumulation (A1), reported separately.
+    `tflops_kernel` counts the flops the kernel issues (the lower 128 x 128
+    tiles, diagonal tiles whole: 2 N T 128^2), so its fraction of the FP64
+    MFMA peak is <= 1; `tflops_reference_count` is the reference's full
+    2 N n^2 addmm count (the kernel does about half of it)."""
     res = {}
     n = args.n
     for rows, reps in ((args.tokens, 1), (65536, 4)):
@@ -185,8 +189,13 @@ def syrk_bench(g, args, device):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         N = rows * reps
+        nt = -(-n // 128)
+        kernel_flops = 2.0 * N * (nt * (nt + 1) // 2) * 128 * 128  # lower 128-tiles
+        tf = kernel_flops / dt / 1e12
         res[f"N{N}"] = dict(ms=round(dt * 1e3, 3),
-                            tflops_algorithmic=round(2.0 * N * n * n / dt / 1e12, 2))
+                            flops_kernel=kernel_flops, tflops_kernel=round(tf, 2),
+                            frac_fp64_mfma_peak=round(tf / PEAKS["fp64_mfma"][1], 4),
+                            tflops_reference_count=round(2.0 * N * n * n / dt / 1e12, 2))
         del X
     return res
 

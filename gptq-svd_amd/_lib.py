@@ -30,6 +30,8 @@ _SIGS = {
     "tg_last_error": ([], ctypes.c_char_p),
     "tg_version": ([], _i),
     "tg_syrk_accum": ([_vp, _vp, _i, _i64, _i, _i64, _vp, _i], _i),
+    "tg_syrk_workspace_size": ([_i], _sz),
+    "tg_syrk_accum_ws": ([_vp, _vp, _i, _i64, _i, _i64, _vp, _i, _vp, _sz], _i),
     "tg_scale_f64": ([_vp, _vp, _i64, _d, _vp], _i),
     "tg_profile_enable": ([_i, _i], _i),
     "tg_profile_reset": ([], _i),

@@ -59,6 +59,12 @@ struct ProfTok {
 ProfTok prof_begin(hipStream_t st, int id, double bytes, double flops);
 void prof_end(hipStream_t st, ProfTok tok);
 
+// 16-bit Hessian SYRK (syrk.hip)
+size_t syrk16_workspace_size();
+bool syrk16_supported(const void *X, int n, int64_t ldx);
+hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n, int64_t ldx,
+                  double *H, int64_t ldh, void *ws);
+
 }  // namespace tg
 
 #define TG_ARG(cond, idx, msg)                                   \

@@ -35,7 +35,8 @@ __all__ = [
 # A1  (gptq_utils.py:213-228)
 # ---------------------------------------------------------------------------
 class HessianAccumulator:
-    """H += x^T x in float64 (FP64 MFMA SYRK kernel); get_hessian() = H / N."""
+    """H += x^T x in float64 (FP64 MFMA SYRK kernel; fp16 / bf16 inputs take
+    the dedicated 16-bit SYRK of syrk.hip); get_hessian() = H / N."""
 
     def __init__(self, in_features, device, dtype=torch.float64):
         if dtype != torch.float64:
@@ -43,6 +44,7 @@ class HessianAccumulator:
         self.H = torch.zeros((in_features, in_features), device=device, dtype=dtype)
         _lib.require_cuda(self.H, "HessianAccumulator device")
         self.n_samples = 0
+        self._ws = None
 
     def add_batch(self, x):                                   # gptq_utils.py:218-223
         if x.dim() == 3:
@@ -57,8 +59,10 @@ class HessianAccumulator:
             raise RuntimeError(f"add_batch: expected {self.H.shape[0]} features, got {n}")
         if rows:
             with torch.cuda.device(self.H.device):
-                call("tg_syrk_accum", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
-                     x.stride(0), ptr(self.H), self.H.shape[0])
+                if self._ws is None:  # the 16-bit SYRK's partial-tile scratch
+                    self._ws = workspace(_lib.lib.tg_syrk_workspace_size(n), self.H.device)
+                call("tg_syrk_accum_ws", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
+                     x.stride(0), ptr(self.H), self.H.shape[0], ptr(self._ws), self._ws.numel())
         self.n_samples += rows
 
     def get_hessian(self):                                    # gptq_utils.py:225-228

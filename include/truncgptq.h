@@ -48,6 +48,16 @@ enum tg_rank_rule { TG_RULE_NONE = 0, TG_RULE_ENERGY = 1, TG_RULE_MEAN_TRIMMED =
 int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n, int64_t ldx,
                   double *H, int ldh);
 
+/* The same update with a caller workspace (tg_syrk_workspace_size bytes, a
+ * device constant independent of n and rows): fp16 / bf16 X with n and ldx
+ * multiples of 8 and a 16-byte aligned X take the dedicated 16-bit SYRK
+ * (syrk.hip: X kept 16-bit in LDS, stream-K over the lower 128 x 128 tiles,
+ * partial tiles summed in a fixed order -- deterministic for a given
+ * device); other inputs fall back to tg_syrk_accum. */
+size_t tg_syrk_workspace_size(int n);
+int tg_syrk_accum_ws(void *stream, const void *X, int x_dtype, int64_t rows, int n, int64_t ldx,
+                     double *H, int ldh, void *ws, size_t ws_bytes);
+
 /* Replaces HessianAccumulator.get_hessian `self.H / self.n_samples`
  * (gptq_utils.py:225-228).  inv_n > 0: out = H * inv_n; inv_n < 0:
  * out = H / (-inv_n) (exact true division, the reference's semantics).

@@ -138,15 +138,29 @@ def test_fullsize_ar1_factor(g, ar1_layer, path, monkeypatch):
 
 
 def test_fullsize_ar1_end_to_end(g, ar1_layer, oracle_mod):
+    """Own H -> own U/perm -> codes.  Against the oracle in our cross-block
+    order (the k-ordered fma chain) the codes differ only through U's ~1e-10
+    difference; against the oracle in MKL's SGEMM order (the reference's CPU
+    run) they differ as much as the two orders differ from each other on the
+    SAME U -- the AR(1) spectrum amplifies the cross-block rounding, so the
+    bar is that disagreement (the reference's own order sensitivity on this
+    input) or 6e-4, whichever is larger."""
     H, W, f = ar1_layer
     R, R_x, perm = g.process_hessian_alt(H, 1e-4, "energy")
     q = g.Quantizer(4, 128, False)
     Wq, k = g.gptq_fwrd(W.to(DEV), R, q, perm, block_size=1024)
-    ref, _ = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 4, 128, False, 1024,
-                                  gemm="torch", impl="c", nthreads=16)
-    mism = float(np.mean(Wq.cpu().numpy() != ref))
-    print(f"AR(1) 4096^2 end-to-end code mismatch vs oracle (MKL order): {mism:.2e}")
-    assert mism <= 6e-4
+    Wq = Wq.cpu().numpy()
+    ref_fma, _ = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 4, 128, False, 1024,
+                                      gemm="fma", impl="c", nthreads=16)
+    ref_mkl, _ = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 4, 128, False, 1024,
+                                      gemm="torch", impl="c", nthreads=16)
+    m_fma = float(np.mean(Wq != ref_fma))
+    m_mkl = float(np.mean(Wq != ref_mkl))
+    m_orders = float(np.mean(ref_fma != ref_mkl))
+    print(f"AR(1) 4096^2 code mismatch: vs oracle fma order {m_fma:.2e}, vs MKL order "
+          f"{m_mkl:.2e}; the two orders on the oracle's U: {m_orders:.2e}")
+    assert m_fma <= 5e-5
+    assert m_mkl <= max(6e-4, 1.25 * m_orders)
 
 
 @pytest.mark.parametrize("n,path", [(8192, "kept"), (8192, "complement"), (12288, "complement"),
