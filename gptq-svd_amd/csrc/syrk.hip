@@ -6,8 +6,8 @@
 // inputs are exact in FP64, every product is formed and summed in FP64.
 //
 // Layout and schedule:
-//  * a workgroup (4 waves as 2 x 2, 64 x 64 per wave = 4 x 4 MFMA blocks)
-//    owns one 128 x 128 tile of H at a time and streams the two 128-column
+//  * a workgroup (8 waves as 2 x 4, 64 x 32 per wave = 4 x 2 MFMA blocks;
+//    two workgroups per CU) owns one 128 x 128 tile of H at a time and streams the two 128-column
 //    strips of X it needs (tile row I, tile column J) in slabs of 32 rows;
 //  * X stays 16-bit in LDS: a strip slab is 128 columns x 32 rows, column
 //    major, 64 B per column, its four 16-B chunks (8 consecutive rows each)
@@ -15,14 +15,14 @@
 //    fragment reads of a wave hit 64 distinct banks; lane group g = lane >> 4
 //    takes rows 8g..8g+7 of the slab, so one 16-B read holds the lane's
 //    operand for 8 consecutive MFMA steps (converted to FP64 in registers);
-//  * global loads are 16 B per lane (8 columns of one row), two slabs ahead,
+//  * global loads are 16 B per lane (8 columns of one row), one slab ahead,
 //    written to LDS as row pairs (one ds_write_b32 per column);
-//  * stream-K: the lower tiles' slabs form one list (tile-major), cut into
-//    equal contiguous ranges, one per resident workgroup (grid = CUs x
-//    occupancy), so every workgroup does the same work and the launch has no
-//    tail round.  A tile finished inside one range is added to H directly;
-//    a tile cut between ranges leaves partial tiles in the workspace, and
-//    `syrk_fixup_kernel` adds them to H in range order (deterministic).
+//  * a persistent grid (CUs x 2 workgroups) takes work units from an atomic
+//    queue: whole tiles first, then the last round's tiles cut into four
+//    chunks of K; a whole tile is added to H directly, a chunk leaves a
+//    partial tile in the workspace and `syrk_fixup_kernel` adds a tile's
+//    chunks to H in chunk order -- the decomposition is static, so H is
+//    deterministic whichever workgroup ran which unit.
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 
@@ -39,7 +39,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BT = 128;  // tile edge
 constexpr int KC = 32;   // rows of X per slab
-constexpr int NT = 256;  // threads per workgroup
+constexpr int NT = 512;  // threads per workgroup
 
 template <bool BF16>
 __device__ inline double h2d(unsigned bits16) {
@@ -59,14 +59,14 @@ struct SyrkArgs {
   int64_t ldh;
   int T;          // lower tiles
   int NS;         // slabs per tile
-  int64_t W;      // T * NS
-  int G;          // workgroups (ranges)
-  double *piece;  // G x 2 x BT x BT partial tiles
+  int head;       // tiles 0 .. head - 1: one unit each (whole K), added to H directly
+  int Tt;         // tiles head .. T - 1: NC units each (K in chunks of CK slabs)
+  int NC, CK;
+  int U;          // units = head + Tt * NC
+  double *piece;  // Tt x NC x BT x BT partial tiles (chunk c of tail tile i at i * NC + c)
+  unsigned *next; // unit queue head (zeroed before the launch)
+  unsigned long long *stamps;  // TG_SYRK_STAMPS: per workgroup {start, end, xcc} (else null)
 };
-
-__device__ inline int64_t range_begin(const SyrkArgs &a, int g) {
-  return a.W * g / a.G;
-}
 
 __device__ inline void tile_of(int b, int &I, int &J) {
   I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
@@ -75,144 +75,152 @@ __device__ inline void tile_of(int b, int &I, int &J) {
   J = b - I * (I + 1) / 2;
 }
 
-// Global -> registers: this thread's two rows (2rp, 2rp + 1) of 8 columns
-// (cg * 8 ..) of both strips.
+// Global -> registers: thread t stages strip t >> 8 (0 = tile row I's
+// columns, 1 = tile column J's), rows 2rp, 2rp + 1 of the slab (rp =
+// (t >> 4) & 15), columns cg * 8 .. cg * 8 + 7 (cg = t & 15).
 struct Stage {
-  u32x4 v[2][2];  // [strip][row]
+  u32x4 v[2];  // [row]
   __device__ inline void load(const SyrkArgs &a, int c0A, int c0B, int64_t k0) {
-    const int t = threadIdx.x, cg = t & 15, rp = t >> 4;
+    const int t = threadIdx.x, cg = t & 15, rp = (t >> 4) & 15, sp = t >> 8;
+    const int c = (sp == 0 ? c0A : c0B) + cg * 8;
+    const bool cok = c < a.n;  // n % 8 == 0: a chunk is all in or all out
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = (s == 0 ? c0A : c0B) + cg * 8;
-      const bool cok = c < a.n;  // n % 8 == 0: a chunk is all in or all out
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int64_t k = k0 + 2 * rp + r;
-        const bool ok = cok && k < a.rows;
-        const int64_t kc = ok ? k : 0;
-        const int cc = ok ? c : 0;
-        u32x4 x = *reinterpret_cast<const u32x4 *>(a.X + kc * a.ldx + cc);
-        v[s][r] = ok ? x : u32x4{0u, 0u, 0u, 0u};
-      }
+    for (int r = 0; r < 2; ++r) {
+      const int64_t k = k0 + 2 * rp + r;
+      const bool ok = cok && k < a.rows;
+      const int64_t kc = ok ? k : 0;
+      const int cc = ok ? c : 0;
+      u32x4 x = *reinterpret_cast<const u32x4 *>(a.X + kc * a.ldx + cc);
+      v[r] = ok ? x : u32x4{0u, 0u, 0u, 0u};
     }
   }
   // registers -> LDS: column c, rows 2rp, 2rp+1 as one 4-byte word
   __device__ inline void store(unsigned short *SA, unsigned short *SB) const {
-    const int t = threadIdx.x, cg = t & 15, rp = t >> 4;
+    const int t = threadIdx.x, cg = t & 15, rp = (t >> 4) & 15, sp = t >> 8;
     const int k = 2 * rp, q = k >> 3, kin = k & 7;
+    unsigned short *S = sp == 0 ? SA : SB;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      unsigned short *S = s == 0 ? SA : SB;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = cg * 8 + j;
-        const unsigned lo = (v[s][0][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-        const unsigned hi = (v[s][1][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-        *reinterpret_cast<unsigned *>(S + c * KC + ((q ^ swz(c)) << 3) + kin) = lo | (hi << 16);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      const unsigned lo = (v[0][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+      const unsigned hi = (v[1][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+      *reinterpret_cast<unsigned *>(S + c * KC + ((q ^ swz(c)) << 3) + kin) = lo | (hi << 16);
     }
   }
 };
 
-// A wave's operands of one slab: for each of its 4 + 4 MFMA blocks, the 8
-// rows of its lane group (one ds_read_b128 each).
+// Wave w of the 8 owns rows wm * 64 .. + 63 (4 MFMA blocks) and columns
+// wn * 32 .. + 31 (2 blocks) of the tile, wm = w >> 2, wn = w & 3.
+constexpr int FI = 4, FJ = 2;
+
+// A wave's operands of half a slab: for each of its 4 + 2 MFMA blocks, 4
+// rows of its lane group (rows 8g + 4h .. + 3, one ds_read_b64 each).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 struct Frags {
-  u32x4 a[4], b[4];
-  __device__ inline void read(const unsigned short *SA, const unsigned short *SB) {
+  u32x2 a[FI], b[FJ];
+  __device__ inline void read(const unsigned short *SA, const unsigned short *SB, int h) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int wm = w >> 1, wn = w & 1, g = lane >> 4, r = lane & 15;
+    const int wm = w >> 2, wn = w & 3, g = lane >> 4, r = lane & 15;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < FI; ++i) {
       const int c = wm * 64 + i * 16 + r;
-      a[i] = *reinterpret_cast<const u32x4 *>(SA + c * KC + ((g ^ swz(c)) << 3));
+      a[i] = *reinterpret_cast<const u32x2 *>(SA + c * KC + ((g ^ swz(c)) << 3) + 4 * h);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = wn * 64 + j * 16 + r;
-      b[j] = *reinterpret_cast<const u32x4 *>(SB + c * KC + ((g ^ swz(c)) << 3));
+    for (int j = 0; j < FJ; ++j) {
+      const int c = wn * 32 + j * 16 + r;
+      b[j] = *reinterpret_cast<const u32x2 *>(SB + c * KC + ((g ^ swz(c)) << 3) + 4 * h);
     }
   }
 };
 
 template <bool BF16>
-__device__ inline void slab_mfma(const Frags &f, doublex4 (&acc)[4][4]) {
+__device__ inline void half_slab_mfma(const Frags &f, doublex4 (&acc)[FI][FJ]) {
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    double av[4], bv[4];
+  for (int kk = 0; kk < 4; ++kk) {
+    double av[FI], bv[FJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) av[i] = h2d<BF16>((f.a[i][kk >> 1] >> ((kk & 1) * 16)) & 0xffffu);
+    for (int i = 0; i < FI; ++i) av[i] = h2d<BF16>((f.a[i][kk >> 1] >> ((kk & 1) * 16)) & 0xffffu);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[j] = h2d<BF16>((f.b[j][kk >> 1] >> ((kk & 1) * 16)) & 0xffffu);
+    for (int j = 0; j < FJ; ++j) bv[j] = h2d<BF16>((f.b[j][kk >> 1] >> ((kk & 1) * 16)) & 0xffffu);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < FJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
   }
 }
 
-__device__ inline void lds_drain_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-template <bool BF16, int OCC>
-__global__ __launch_bounds__(NT, OCC) void syrk16_kernel(SyrkArgs a) {
-  // [stage][strip]; at the top of slab s the two stages hold slabs s and s + 1
-  __shared__ __attribute__((aligned(16))) unsigned short S[2][2][BT * KC];
+// Two workgroups of eight waves per CU: four waves per SIMD, two of which
+// keep the f64 MFMA pipe full (one wave alone issues an f64 MFMA only every
+// ~128 cycles: tools/mfma64_peak.hip), while the others wait at their
+// workgroup's barrier or on LDS.
+template <bool BF16>
+__global__ __launch_bounds__(NT, 4) void syrk16_kernel(SyrkArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned short S[2][2][BT * KC];  // [stage][strip]
+  __shared__ unsigned s_unit;
   const int g = blockIdx.x;
-  const int64_t w0 = range_begin(a, g), w1 = range_begin(a, g + 1);
+  if (a.stamps && threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    a.stamps[3 * g] = __builtin_amdgcn_s_memrealtime();
+    a.stamps[3 * g + 2] = x;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int t_first = int(w0 / a.NS);
-  int64_t w = w0;
-  while (w < w1) {
-    const int t = int(w / a.NS);
-    const int s0 = int(w - int64_t(t) * a.NS);
-    const int s1 = int(std::min<int64_t>(a.NS, s0 + (w1 - w)));
-    w += s1 - s0;
+  const int wm = wv >> 2, wn = wv & 3;
+  while (true) {
+    __syncthreads();  // s_unit and the LDS stages of the previous unit are free
+    if (threadIdx.x == 0) s_unit = atomicAdd(a.next, 1u);
+    __syncthreads();
+    const int u = int(s_unit);
+    if (u >= a.U) break;
+    int t, s0, s1, slot = -1;
+    if (u < a.head) {
+      t = u, s0 = 0, s1 = a.NS;
+    } else {  // tail: chunk-major, so units running together share their rows of X
+      const int v = u - a.head, c = v / a.Tt, i = v - c * a.Tt;
+      t = a.head + i;
+      s0 = c * a.CK;
+      s1 = min(a.NS, s0 + a.CK);
+      slot = i * a.NC + c;
+    }
     int I, J;
     tile_of(t, I, J);
     const int tm = I * BT, tn = J * BT;
-    doublex4 acc[4][4];
+    doublex4 acc[FI][FJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
-    // prologue: slabs s0, s0 + 1 into LDS, s0 + 2 into registers, frags of s0
+      for (int j = 0; j < FJ; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
     Stage st;
     st.load(a, tm, tn, int64_t(s0) * KC);
     st.store(S[0][0], S[0][1]);
-    if (s0 + 1 < s1) {
-      st.load(a, tm, tn, int64_t(s0 + 1) * KC);
-      st.store(S[1][0], S[1][1]);
-    }
-    if (s0 + 2 < s1) st.load(a, tm, tn, int64_t(s0 + 2) * KC);
+    if (s0 + 1 < s1) st.load(a, tm, tn, int64_t(s0 + 1) * KC);
     __syncthreads();
-    Frags f, fn;
-    f.read(S[0][0], S[0][1]);
-    lds_drain_barrier();  // every wave has its slab-s0 operands: stage 0 is free
+    int cur = 0;
     for (int s = s0; s < s1; ++s) {
-      const int b = (s - s0) & 1;
-      if (s + 1 < s1) fn.read(S[b ^ 1][0], S[b ^ 1][1]);  // slab s + 1, for the next step
-      slab_mfma<BF16>(f, acc);
-      if (s + 2 < s1) {
-        st.store(S[b][0], S[b][1]);  // slab s + 2 over slab s (its operands are in f)
-        if (s + 3 < s1) st.load(a, tm, tn, int64_t(s + 3) * KC);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        Frags f;
+        f.read(S[cur][0], S[cur][1], h);
+        half_slab_mfma<BF16>(f, acc);
       }
-      lds_drain_barrier();
-      f = fn;
+      if (s + 1 < s1) {
+        st.store(S[cur ^ 1][0], S[cur ^ 1][1]);
+        if (s + 2 < s1) st.load(a, tm, tn, int64_t(s + 2) * KC);
+      }
+      __syncthreads();
+      cur ^= 1;
     }
-    const bool whole = s0 == 0 && s1 == a.NS;
-    if (whole) {  // H += acc on the tile, mirrored
+    if (slot < 0) {  // H += acc on the tile, mirrored
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < FJ; ++j)
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int gi = tm + wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
-            const int gj = tn + wn * 64 + j * 16 + (lane & 15);
+            const int gj = tn + wn * 32 + j * 16 + (lane & 15);
             if (gi < a.n && gj < a.n) {
               double *p = a.H + int64_t(gi) * a.ldh + gj;
               const double v = *p + acc[i][j][rr];
@@ -220,60 +228,42 @@ __global__ __launch_bounds__(NT, OCC) void syrk16_kernel(SyrkArgs a) {
               if (I != J) a.H[int64_t(gj) * a.ldh + gi] = v;
             }
           }
-    } else {  // partial tile: slot 0 = the range's first tile, 1 = its last
-      double *P = a.piece + (int64_t(g) * 2 + (t == t_first ? 0 : 1)) * (BT * BT);
+    } else {  // partial tile of a tail tile's chunk
+      double *P = a.piece + int64_t(slot) * (BT * BT);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < FJ; ++j)
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int li = wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
-            const int lj = wn * 64 + j * 16 + (lane & 15);
+            const int lj = wn * 32 + j * 16 + (lane & 15);
             P[li * BT + lj] = acc[i][j][rr];
           }
     }
   }
+  if (a.stamps) {
+    __syncthreads();
+    if (threadIdx.x == 0) a.stamps[3 * g + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
-// Tiles cut between ranges: H += sum of the pieces in range order, mirrored.
+// Tail tiles: H += their chunks' partial tiles in chunk order, mirrored.
 __global__ __launch_bounds__(NT) void syrk_fixup_kernel(SyrkArgs a) {
-  const int t = blockIdx.x;
-  const int64_t t0 = int64_t(t) * a.NS, t1 = t0 + a.NS;
-  // first range with w1 > t0
-  int glo = int(t0 * a.G / a.W);
-  while (glo > 0 && range_begin(a, glo) > t0) --glo;
-  while (range_begin(a, glo + 1) <= t0) ++glo;
-  if (range_begin(a, glo) <= t0 && range_begin(a, glo + 1) >= t1) return;  // whole in one range
+  const int i = blockIdx.x, t = a.head + i;
+  const int nc = min(a.NC, tg::cdiv(a.NS, a.CK));  // chunks with rows
   int I, J;
   tile_of(t, I, J);
   const int tm = I * BT, tn = J * BT;
   for (int e = threadIdx.x; e < BT * BT; e += NT) {
     const int li = e / BT, lj = e % BT;
     const int gi = tm + li, gj = tn + lj;
-    double v = 0.0;
-    const bool in = gi < a.n && gj < a.n;
-    if (in) v = a.H[int64_t(gi) * a.ldh + gj];
-    for (int gg = glo; gg < a.G && range_begin(a, gg) < t1; ++gg) {
-      const int slot = (range_begin(a, gg) / a.NS == t) ? 0 : 1;
-      v += a.piece[(int64_t(gg) * 2 + slot) * (BT * BT) + e];
-    }
-    if (in) {
-      a.H[int64_t(gi) * a.ldh + gj] = v;
-      if (I != J) a.H[int64_t(gj) * a.ldh + gi] = v;
-    }
+    if (gi >= a.n || gj >= a.n) continue;
+    double v = a.H[int64_t(gi) * a.ldh + gj];
+    for (int c = 0; c < nc; ++c) v += a.piece[(int64_t(i) * a.NC + c) * (BT * BT) + e];
+    a.H[int64_t(gi) * a.ldh + gj] = v;
+    if (I != J) a.H[int64_t(gj) * a.ldh + gi] = v;
   }
-}
-
-// Workgroups per CU: 2 (two waves per SIMD from two workgroups, whose
-// barriers fall at different times) or 1 (all 512 registers for one wave);
-// TG_SYRK_OCC=1|2 picks one (development switch, read once).
-int syrk_occ() {
-  static const int occ = [] {
-    const char *e = getenv("TG_SYRK_OCC");
-    return (e && atoi(e) == 1) ? 1 : 2;
-  }();
-  return occ;
 }
 
 int resident_groups() {
@@ -285,11 +275,11 @@ int resident_groups() {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         ncu < 1)
       ncu = 256;
-    const hipError_t e = syrk_occ() == 1
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk16_kernel<false, 1>, NT, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk16_kernel<false, 2>, NT, 0);
-    if (e != hipSuccess || occ < 1) occ = 1;
-    cached[dev] = ncu * std::min(occ, syrk_occ());
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk16_kernel<false>, NT, 0) !=
+            hipSuccess ||
+        occ < 1)
+      occ = 1;
+    cached[dev] = ncu * std::min(occ, 2);
   }
   return cached[dev];
 }
@@ -298,14 +288,25 @@ int resident_groups() {
 
 namespace tg {
 
+constexpr int NCMAX = 4;  // chunks per tail tile
+
+// Layout: partial tiles (G tail tiles x NCMAX chunks), the queue head, the
+// TG_SYRK_STAMPS clocks (3 words per workgroup).
 size_t syrk16_workspace_size() {
-  return sizeof(double) * size_t(resident_groups()) * 2 * BT * BT;
+  const size_t G = resident_groups();
+  return sizeof(double) * (G * NCMAX * BT * BT + 64 + 3 * G);
 }
 
 bool syrk16_supported(const void *X, int n, int64_t ldx) {
   return n % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
 }
 
+// Decomposition (static, so H does not depend on which workgroup ran what):
+// the last min(T, G) tiles are cut into NCMAX chunks of K, every other tile
+// is one unit; units are handed out by an atomic queue, so a workgroup that
+// runs faster (the older of the two on a CU wins the issue arbitration: their
+// times differ by up to 1.8x, TG_SYRK_STAMPS) simply takes more of them, and
+// the last round is made of quarter tiles.
 hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n, int64_t ldx,
                   double *H, int64_t ldh, void *ws) {
   SyrkArgs a{};
@@ -318,19 +319,27 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   const int nt = cdiv(n, BT);
   a.T = nt * (nt + 1) / 2;
   a.NS = cdiv(rows, KC);
-  a.W = int64_t(a.T) * a.NS;
-  a.G = int(std::min<int64_t>(resident_groups(), a.W));
+  const int G = resident_groups();
+  a.Tt = std::min(a.T, G);
+  a.head = a.T - a.Tt;
+  a.NC = std::min(NCMAX, a.NS);
+  a.CK = cdiv(a.NS, a.NC);
+  a.U = a.head + a.Tt * a.NC;
   a.piece = static_cast<double *>(ws);
-  if (syrk_occ() == 1) {
-    if (bf16) hipLaunchKernelGGL((syrk16_kernel<true, 1>), dim3(a.G), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((syrk16_kernel<false, 1>), dim3(a.G), dim3(NT), 0, st, a);
-  } else {
-    if (bf16) hipLaunchKernelGGL((syrk16_kernel<true, 2>), dim3(a.G), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((syrk16_kernel<false, 2>), dim3(a.G), dim3(NT), 0, st, a);
-  }
-  hipError_t e = hipGetLastError();
+  double *tail = a.piece + int64_t(G) * NCMAX * BT * BT;
+  a.next = reinterpret_cast<unsigned *>(tail);
+  // development switch (read per call): per-workgroup start / end clocks and
+  // XCD, for tools/syrk_time.py
+  a.stamps = getenv("TG_SYRK_STAMPS") ? reinterpret_cast<unsigned long long *>(tail + 64) : nullptr;
+  hipError_t e = hipMemsetAsync(a.next, 0, sizeof(unsigned), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(syrk_fixup_kernel, dim3(a.T), dim3(NT), 0, st, a);
+  const int grid = std::min(G, a.U);
+  if (bf16)
+    hipLaunchKernelGGL(syrk16_kernel<true>, dim3(grid), dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL(syrk16_kernel<false>, dim3(grid), dim3(NT), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(syrk_fixup_kernel, dim3(a.Tt), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
-"""One synthetic layer of width n (H from 3n/4 fp16 rows, as the bench's
-large_n extras) through process_hessian_alt + quantize, REPS times
+"""One synthetic layer of width n (H from ROWS x n fp16 rows, default 3n/4 as
+the bench's large_n extras; ROWS=2 gives a full-rank H like a real layer's) through process_hessian_alt + quantize, REPS times
 (development tool: run plain or under rocprofv3 --kernel-trace --stats)."""
 import os
 import sys
@@ -12,10 +12,12 @@ import gptq_svd_amd.gptq_utils as g  # noqa: E402
 
 n = int(os.environ.get("N", "12288"))
 reps = int(os.environ.get("REPS", "2"))
+rows = int(float(os.environ.get("ROWS", "0.75")) * n)  # calibration rows (x n)
 dev = torch.device("cuda")
 torch.manual_seed(1)
 acc = g.HessianAccumulator(n, dev)
-acc.add_batch(torch.randn(3 * n // 4, n, device=dev).half())
+for r0 in range(0, rows, 16384):
+    acc.add_batch(torch.randn(min(16384, rows - r0), n, device=dev).half())
 H = acc.get_hessian()
 del acc
 W = torch.randn(4096, n, device=dev)

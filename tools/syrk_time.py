@@ -33,3 +33,28 @@ for n in [int(a) for a in sys.argv[1:]] or [4096, 12288]:
               f"({flops / dt / 1e12 / 78.6:.3f} of FP64 MFMA peak)", flush=True)
     del X, acc
     torch.cuda.empty_cache()
+
+if __import__("os").environ.get("TG_SYRK_STAMPS"):
+    # per-workgroup spread of one call (the library wrote {start, end, xcc} per
+    # workgroup after the partial tiles; 100 MHz clock)
+    import numpy as np
+    for n in [int(a) for a in sys.argv[1:]] or [4096, 12288]:
+        rows = 65536
+        X = torch.randn(rows, n, device=dev).half()
+        acc = g.HessianAccumulator(n, dev)
+        acc.add_batch(X)
+        acc.add_batch(X)
+        torch.cuda.synchronize()
+        G = (acc._ws.numel() // 8 - 64) // (4 * 128 * 128 + 3)
+        off = (G * 4 * 128 * 128 + 64) * 8
+        st = acc._ws[off:off + 24 * G].view(torch.int64).cpu().numpy().reshape(G, 3)
+        t0 = st[:, 0].min()
+        s, e, x = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0, st[:, 2]
+        d = e - s
+        print(f"n={n}: G={G}, start spread {s.max():.1f} us, end min/median/max "
+              f"{e.min():.0f}/{np.median(e):.0f}/{e.max():.0f} us, duration min/median/max "
+              f"{d.min():.0f}/{np.median(d):.0f}/{d.max():.0f} us")
+        print("  per XCD median duration (us):",
+              [round(float(np.median(d[x == i])), 0) for i in range(8) if (x == i).any()])
+        order = np.argsort(d)
+        print("  slowest workgroups:", [(int(i), round(float(d[i])), int(x[i])) for i in order[-6:]])
