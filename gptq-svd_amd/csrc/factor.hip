@@ -1359,27 +1359,50 @@ static void launch_potrf_inv(hipStream_t st, double *U, int ldu, int p, int pb, 
   hipLaunchKernelGGL(potrf_inv_4w_kernel<4>, dim3(1), dim3(256), 0, st, U, ldu, p, pb, Wb, info);
 }
 
+// Two-level blocking: NU-row panels inside strips of CS = 256 rows.  A
+// panel's rank-NU update only reaches the rest of its strip; the rows below
+// the strip get one rank-CS update per strip (a quarter of the passes over
+// the trailing matrix, and at K = 256 the update is MFMA-bound instead of
+// HBM-bound: at k = 12,288 the 192 rank-64 updates streamed ~150 GB).  When
+// k == n the trailing matrix is symmetric and that update is a SYRK on the
+// lower tiles, mirrored (half the flops of the square).  The strip update
+// writes the whole trailing square (lower tiles mirrored): later panels read
+// only its upper triangle.
+constexpr int CS = 256;
+
 hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, double *Wb,
                            int *info) {
   // (a depth-1 look-ahead on a side stream measured +0.4 ms: the event
   // waits cost more than the overlap; removed)
-  for (int p = 0; p < k; p += NU) {
-    const int pb = std::min(NU, k - p);
-    launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int c0 = p + pb;
-    if (c0 < n) {
-      // in place: one 64-row tile covers the panel's rows, so each workgroup
-      // reads its columns of G12 fully before writing them
-      double *P = U + size_t(p) * ldu + c0;
-      e = tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
+  for (int s0 = 0; s0 < k; s0 += CS) {
+    const int se = std::min(k, s0 + CS);
+    for (int p = s0; p < se; p += NU) {
+      const int pb = std::min(NU, se - p);
+      launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
+      hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
+      const int c0 = p + pb;
+      if (c0 < n) {
+        // in place: one 64-row tile covers the panel's rows, so each workgroup
+        // reads its columns of G12 fully before writing them
+        double *P = U + size_t(p) * ldu + c0;
+        e = tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
+        if (e != hipSuccess) return e;
+      }
+      if (c0 < se) {  // the rest of the strip
+        const double *P = U + size_t(p) * ldu + c0;
+        e = tg::dgemm(st, true, false, se - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
+                      U + size_t(c0) * ldu + c0, ldu);
+        if (e != hipSuccess) return e;
+      }
     }
-    if (c0 < k) {
-      const double *P = U + size_t(p) * ldu + c0;
-      e = tg::dgemm(st, true, false, k - c0, n - c0, pb, -1.0, P, ldu, P, ldu, 1.0,
-                    U + size_t(c0) * ldu + c0, ldu);
+    if (se < k) {  // rows below the strip: one rank-(se - s0) update
+      const double *Q = U + size_t(s0) * ldu + se;
+      const hipError_t e =
+          k == n ? tg::dsyrk_tn(st, n - se, se - s0, -1.0, Q, ldu, 1.0, U + size_t(se) * ldu + se,
+                                ldu)
+                 : tg::dgemm(st, true, false, k - se, n - se, se - s0, -1.0, Q, ldu, Q, ldu, 1.0,
+                             U + size_t(se) * ldu + se, ldu);
       if (e != hipSuccess) return e;
     }
   }

@@ -259,6 +259,209 @@ __global__ __launch_bounds__(256) void dgemm_chunked_kernel(tg::ChunkSpec cs, do
   epilogue<BM, BN, false>(acc, alpha, beta, C, ldc, M, N, tm, tn);
 }
 
+// ---------------------------------------------------------------------------
+// 8-wave FP64 GEMM: 128 x 128 tiles, 512 threads as 2 x 4 waves of 64 x 32
+// (4 x 2 MFMA blocks, 64 accumulator registers), two workgroups per CU, so
+// four waves per SIMD keep the f64 MFMA pipe fed (one wave alone issues an
+// f64 MFMA only every ~128 cycles, two reach 97-99% of peak:
+// tools/mfma64_peak.hip).  K in slabs of 16 through a double-buffered k-major
+// LDS image (one barrier per slab), 16-byte global loads when the operand
+// is 16-byte aligned with an even leading dimension (VEC), 8-byte otherwise.
+// SYRK: blockIdx.x enumerates the lower tiles, the result is mirrored.
+// ---------------------------------------------------------------------------
+constexpr int G8_T = 128, G8_KC = 16, G8_P = G8_T + 16, G8_NT = 512;
+
+// Two doubles of X at [row, idx], [row, idx + 1] (X row-major, ld), zero
+// outside rows < R, idx < L; one 16-byte load when both are inside and VEC.
+template <bool VEC>
+__device__ inline void ld2(const double *__restrict__ X, int64_t ld, int row, int R, int idx, int L,
+                           double &v0, double &v1) {
+  const bool rok = row < R;
+  if (VEC && rok && idx + 1 < L) {
+    const double2 v = *reinterpret_cast<const double2 *>(X + int64_t(row) * ld + idx);
+    v0 = v.x;
+    v1 = v.y;
+    return;
+  }
+  const int rc = rok ? row : 0;
+  const double a = X[int64_t(rc) * ld + min(idx, L - 1)];
+  const double b = X[int64_t(rc) * ld + min(idx + 1, L - 1)];
+  v0 = (rok && idx < L) ? a : 0.0;
+  v1 = (rok && idx + 1 < L) ? b : 0.0;
+}
+
+// Staging of op(X)[r0 .. r0 + 128) x [k0 .. k0 + 16) (op(X) is R x K) into
+// the k-major image S[k][r], four doubles per thread in two pairs.
+//  KCONT (op(X)[r][k] = X[r * ld + k]): pair p holds k = 2 (t >> 7) + 8p, +1
+//    of row r = t & 127 (16 consecutive rows per 16-lane group: the two
+//    8-byte LDS stores per pair are conflict-free);
+//  else (op(X)[r][k] = X[k * ld + r]): pair p holds rows 2 (t & 63), +1 of
+//    k = (t >> 6) + 8p (one 16-byte LDS store, a wave writes 1 KB contiguous).
+template <bool KCONT, bool VEC>
+struct Stg8 {
+  double v[4];
+  __device__ inline void load(const double *__restrict__ X, int64_t ld, int R, int K, int r0,
+                              int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (KCONT) {
+        const int r = t & 127, k = 2 * (t >> 7) + 8 * p;
+        ld2<VEC>(X, ld, r0 + r, R, k0 + k, K, v[2 * p], v[2 * p + 1]);
+      } else {
+        const int r = 2 * (t & 63), k = (t >> 6) + 8 * p;
+        ld2<VEC>(X, ld, k0 + k, K, r0 + r, R, v[2 * p], v[2 * p + 1]);
+      }
+    }
+  }
+  __device__ inline void store(double (*S)[G8_P]) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (KCONT) {
+        const int r = t & 127, k = 2 * (t >> 7) + 8 * p;
+        S[k][r] = v[2 * p];
+        S[k + 1][r] = v[2 * p + 1];
+      } else {
+        const int r = 2 * (t & 63), k = (t >> 6) + 8 * p;
+        *reinterpret_cast<double2 *>(&S[k][r]) = double2{v[2 * p], v[2 * p + 1]};
+      }
+    }
+  }
+};
+
+// swz (plain GEMM, 1-D grid): block b runs on XCD b % 8 under round-robin
+// dispatch (speed only), so the tiles are dealt to the XCDs in contiguous
+// ranges, walked 8 tile rows at a time: the workgroups one L2 serves at a
+// time cover an 8 x 8 block of tiles and share their row and column panels.
+template <bool TA, bool TB, bool VA, bool VB, bool SYRK>
+__global__ __launch_bounds__(G8_NT, 4) void dgemm8_kernel(int M, int N, int K, double alpha,
+                                                          const double *__restrict__ A, int64_t lda,
+                                                          const double *__restrict__ B, int64_t ldb,
+                                                          double beta, double *__restrict__ C,
+                                                          int64_t ldc, int swz) {
+  __shared__ __attribute__((aligned(16))) double As[2][G8_KC][G8_P];
+  __shared__ __attribute__((aligned(16))) double Bs[2][G8_KC][G8_P];
+  int tm, tn;
+  if (SYRK) {
+    const int b = blockIdx.x;
+    int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= b) ++I;
+    while (I * (I + 1) / 2 > b) --I;
+    tm = I * G8_T;
+    tn = (b - I * (I + 1) / 2) * G8_T;
+  } else if (swz) {
+    const int tmn = tg::cdiv(M, G8_T), tnn = tg::cdiv(N, G8_T), nb = tmn * tnn;
+    const int per = tg::cdiv(nb, 8);
+    const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (L >= nb) return;
+    const int GM = 8, gsz = GM * tnn, grp = L / gsz, r = L - grp * gsz;
+    const int rows = min(GM, tmn - grp * GM);
+    tm = (grp * GM + r % rows) * G8_T;
+    tn = (r / rows) * G8_T;
+  } else {
+    tm = blockIdx.y * G8_T;
+    tn = blockIdx.x * G8_T;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  doublex4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  // op(A) = A (M x K, k contiguous) or A^T (A is K x M); op(B) is K x N and
+  // is staged as op(B)^T (N x K): k contiguous iff B is stored transposed
+  Stg8<!TA, VA> sa;
+  Stg8<TB, VB> sb;
+  if (K > 0) {
+    sa.load(A, lda, M, K, tm, 0);
+    sb.load(B, ldb, N, K, tn, 0);
+    sa.store(As[0]);
+    sb.store(Bs[0]);
+    if (G8_KC < K) {
+      sa.load(A, lda, M, K, tm, G8_KC);
+      sb.load(B, ldb, N, K, tn, G8_KC);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = 0; k0 < K; k0 += G8_KC) {
+#pragma unroll
+      for (int kk = 0; kk < G8_KC; kk += 4) {
+        double af[4], bf[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = As[cur][kk + (lane >> 4)][wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = Bs[cur][kk + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      if (k0 + G8_KC < K) {
+        sa.store(As[cur ^ 1]);
+        sb.store(Bs[cur ^ 1]);
+        if (k0 + 2 * G8_KC < K) {
+          sa.load(A, lda, M, K, tm, k0 + 2 * G8_KC);
+          sb.load(B, ldb, N, K, tn, k0 + 2 * G8_KC);
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = tm + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        const int gj = tn + wn * 32 + j * 16 + (lane & 15);
+        if (gi < M && gj < N) {
+          double *pc = C + int64_t(gi) * ldc + gj;
+          const double v = beta == 0.0 ? alpha * acc[i][j][r] : alpha * acc[i][j][r] + beta * *pc;
+          *pc = v;
+          if (SYRK && tm != tn) C[int64_t(gj) * ldc + gi] = v;
+        }
+      }
+}
+
+inline bool vec_ok(const double *X, int64_t ld) {
+  return (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (ld & 1) == 0;
+}
+
+template <bool TA, bool TB, bool SYRK>
+hipError_t launch8_v(hipStream_t st, dim3 grid, bool va, bool vb, int M, int N, int K,
+                     double alpha, const double *A, int64_t lda, const double *B, int64_t ldb,
+                     double beta, double *C, int64_t ldc, int swz = 0) {
+#define TG_L8(VA_, VB_)                                                                      \
+  hipLaunchKernelGGL((dgemm8_kernel<TA, TB, VA_, VB_, SYRK>), grid, dim3(G8_NT), 0, st, M, N, K, \
+                     alpha, A, lda, B, ldb, beta, C, ldc, swz)
+  if (va && vb) TG_L8(true, true);
+  else if (va) TG_L8(true, false);
+  else if (vb) TG_L8(false, true);
+  else TG_L8(false, false);
+#undef TG_L8
+  return hipGetLastError();
+}
+
+hipError_t launch8(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
+                   const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                   double *C, int64_t ldc) {
+  // TG_GEMM_SWZ=0 keeps the 2-D grid (development switch, read per call)
+  const char *e = getenv("TG_GEMM_SWZ");
+  const int swz = (e && e[0] == '0') ? 0 : 1;
+  const int nb = tg::cdiv(N, G8_T) * tg::cdiv(M, G8_T);
+  const dim3 grid = swz ? dim3(8 * tg::cdiv(nb, 8)) : dim3(tg::cdiv(N, G8_T), tg::cdiv(M, G8_T));
+  const bool va = vec_ok(A, lda), vb = vec_ok(B, ldb);
+  if (!ta && !tb) return launch8_v<false, false, false>(st, grid, va, vb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, swz);
+  if (!ta && tb) return launch8_v<false, true, false>(st, grid, va, vb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, swz);
+  if (ta && !tb) return launch8_v<true, false, false>(st, grid, va, vb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, swz);
+  return launch8_v<true, true, false>(st, grid, va, vb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, swz);
+}
+
 template <class TA_, class TB_, int BM, int BN, bool TA, bool TB, bool UPA = false>
 hipError_t launch(hipStream_t st, int M, int N, int K, double alpha, const TA_ *A, int64_t lda,
                   const TB_ *B, int64_t ldb, double beta, double *C, int64_t ldc, int splits,
@@ -362,11 +565,22 @@ static int gemm_tile(int M, int N) {
   return double(t) >= 0.85 * double(rounds * slots128) ? 128 : 64;
 }
 
+// Which GEMM runs the large tiles: TG_GEMM_IMPL=own8 (default: the 8-wave
+// kernel), own (the 4-wave 128 x 128 kernel), rocblas (Tensile, for A/B
+// measurement); read per call (development switch).
+static int gemm_impl() {
+  const char *e = getenv("TG_GEMM_IMPL");
+  if (!e) return 2;
+  if (e[0] == 'r') return 0;
+  return (e[0] == 'o' && e[1] == 'w' && e[2] == 'n' && e[3] == '8') ? 2 : 1;
+}
+
 hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double alpha,
                  const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                  double *C, int64_t ldc) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  if (use_blas(M, N, K, A, B, C)) {
+  const int impl = gemm_impl();
+  if (impl == 0 && use_blas(M, N, K, A, B, C)) {
     if (rocblas_handle h = blas_handle(st)) {
       // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
       const rocblas_status rs = rocblas_dgemm(
@@ -380,6 +594,8 @@ hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double a
     // C = beta * C (alpha * 0): run with K = 0 -> the kernel writes beta*C
   }
   const int tile = gemm_tile(M, N);
+  if (tile == 128 && impl == 2 && C != A && C != B)
+    return launch8(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
   if (tile == 128)
     return dispatch_t<double, double, 128, 128>(st, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
                                                 C, ldc);
@@ -503,6 +719,12 @@ hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X,
                     double beta, double *C, int64_t ldc) {
   if (n <= 0) return hipSuccess;
   const int n128 = cdiv(n, 128);
+  if (n128 * (n128 + 1) / 2 >= 1024 && gemm_impl() == 2 && C != X) {
+    const dim3 grid(n128 * (n128 + 1) / 2);
+    return vec_ok(X, ldx)
+        ? launch8_v<true, false, true>(st, grid, true, true, n, n, K, alpha, X, ldx, X, ldx, beta, C, ldc)
+        : launch8_v<true, false, true>(st, grid, false, false, n, n, K, alpha, X, ldx, X, ldx, beta, C, ldc);
+  }
   if (n128 * (n128 + 1) / 2 >= 1024) {
     hipLaunchKernelGGL((dgemm_kernel<double, double, 128, 128, true, false, true>),
                        dim3(n128 * (n128 + 1) / 2), dim3(256), 0, st, n, n, K, alpha, X, ldx, X,

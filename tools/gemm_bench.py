@@ -10,6 +10,9 @@ from gptq_svd_amd import _lib as lib  # noqa: E402
 dev = torch.device("cuda")
 cases = [  # (name, ta, tb, M, N, K, beta)
     ("NN 4096^3", 0, 0, 4096, 4096, 4096, 0.0),
+    ("NN 12288^2 K12288", 0, 0, 12288, 12288, 12288, 0.0),
+    ("TN trail 12k K64", 1, 0, 12160, 12160, 64, 1.0),
+    ("TN trail 12k K256", 1, 0, 12032, 12032, 256, 1.0),
     ("TN G=A^T A", 1, 0, 3058, 4096, 3058, 0.0),
     ("TN trail K64", 1, 0, 2994, 4032, 64, 1.0),
     ("TN trail K32", 1, 0, 2994, 4032, 32, 1.0),
@@ -31,7 +34,9 @@ for name, ta, tb, M, N, K, beta in cases:
     opB = B.T if tb else B
     def ref():
         torch.addmm(C, opA, opB, beta=beta, out=C) if beta else torch.mm(opA, opB, out=C)
-    for fn, lab in ((ours, "tg"), (ref, "torch")):
+    for fn, lab in ((ours, "own8"), (ours, "own8-2d"), (ours, "rocblas"), (ref, "torch")):
+        os.environ["TG_GEMM_IMPL"] = lab.split("-")[0]
+        os.environ["TG_GEMM_SWZ"] = "0" if lab.endswith("-2d") else "1"
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
