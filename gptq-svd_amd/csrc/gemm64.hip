@@ -11,8 +11,6 @@
 // 16 (k-major images so fragment reads are 16 consecutive doubles).
 // f64 MFMA C/D layout (differs from f32!): col = lane & 15,
 // row = (lane >> 4) + 4 * reg  (MI355X guide §3).
-#include <rocblas/rocblas.h>
-
 #include <algorithm>
 #include <cstdlib>
 #include <unordered_map>
@@ -513,36 +511,6 @@ hipError_t syrk_t(hipStream_t st, const T *X, int64_t rows, int n, int64_t ldx, 
 
 }  // namespace
 
-namespace {
-// Plain (unfused, non-aliasing) large GEMMs go to rocBLAS's Tensile DGEMM
-// (~65 TF/s on MI355X vs ~36-40 TF/s for dgemm_kernel above).  One handle per
-// thread and device, bound to the caller's stream on every call; its device
-// workspace is disabled (size 0), so the library still allocates nothing.
-rocblas_handle blas_handle(hipStream_t st) {
-  thread_local std::unordered_map<int, rocblas_handle> handles;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  auto it = handles.find(dev);
-  rocblas_handle h = nullptr;
-  if (it == handles.end()) {
-    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-    rocblas_set_workspace(h, nullptr, 0);
-    handles.emplace(dev, h);
-  } else {
-    h = it->second;
-  }
-  return rocblas_set_stream(h, st) == rocblas_status_success ? h : nullptr;
-}
-
-bool use_blas(int M, int N, int K, const double *A, const double *B, const double *C) {
-  const bool off = getenv("TG_NO_ROCBLAS") != nullptr;  // read per call (tests set it)
-  if (off || K < 32 || double(M) * N * K < double(1 << 28)) return false;
-  // rocBLAS does not allow C to alias an operand (chol_upper_rows' in-place
-  // panel solve does; it stays on dgemm_kernel)
-  return C != A && C != B;
-}
-}  // namespace
-
 namespace tg {
 // Tile of the own DGEMM: TG_GEMM_TILE=128|12864|64 forces one (development
 // switch, read per call).  Otherwise 128 x 128 (two workgroups per CU, the
@@ -565,13 +533,13 @@ static int gemm_tile(int M, int N) {
   return double(t) >= 0.85 * double(rounds * slots128) ? 128 : 64;
 }
 
-// Which GEMM runs the large tiles: TG_GEMM_IMPL=own8 (default: the 8-wave
-// kernel), own (the 4-wave 128 x 128 kernel), rocblas (Tensile, for A/B
-// measurement); read per call (development switch).
+// Which kernel runs the large tiles: TG_GEMM_IMPL=own8 (default: the 8-wave
+// kernel) or own (the 4-wave 128 x 128 kernel); read per call (development
+// switch).  No vendor BLAS is linked: tools/gemm_bench.py times both against
+// torch's hipBLASLt on the solver's shapes.
 static int gemm_impl() {
   const char *e = getenv("TG_GEMM_IMPL");
   if (!e) return 2;
-  if (e[0] == 'r') return 0;
   return (e[0] == 'o' && e[1] == 'w' && e[2] == 'n' && e[3] == '8') ? 2 : 1;
 }
 
@@ -580,16 +548,6 @@ hipError_t dgemm(hipStream_t st, bool ta, bool tb, int M, int N, int K, double a
                  double *C, int64_t ldc) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const int impl = gemm_impl();
-  if (impl == 0 && use_blas(M, N, K, A, B, C)) {
-    if (rocblas_handle h = blas_handle(st)) {
-      // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
-      const rocblas_status rs = rocblas_dgemm(
-          h, tb ? rocblas_operation_transpose : rocblas_operation_none,
-          ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &alpha, B,
-          rocblas_int(ldb), A, rocblas_int(lda), &beta, C, rocblas_int(ldc));
-      if (rs == rocblas_status_success) return hipSuccess;
-    }
-  }
   if (K <= 0) {
     // C = beta * C (alpha * 0): run with K = 0 -> the kernel writes beta*C
   }

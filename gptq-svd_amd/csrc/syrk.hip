@@ -27,6 +27,7 @@
 #include <hip/hip_fp16.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "../../include/truncgptq.h"
@@ -38,7 +39,8 @@ typedef double doublex4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BT = 128;  // tile edge
-constexpr int KC = 32;   // rows of X per slab
+constexpr int KC = 32;   // rows of X per sub-slab (one LDS image)
+constexpr int NSUB = 2;  // sub-slabs per slab: one barrier per NSUB * KC rows
 constexpr int NT = 512;  // threads per workgroup
 
 template <bool BF16>
@@ -58,7 +60,7 @@ struct SyrkArgs {
   double *H;
   int64_t ldh;
   int T;          // lower tiles
-  int NS;         // slabs per tile
+  int NS;         // slabs (NSUB * KC rows) per tile
   int head;       // tiles 0 .. head - 1: one unit each (whole K), added to H directly
   int Tt;         // tiles head .. T - 1: NC units each (K in chunks of CK slabs)
   int NC, CK;
@@ -157,7 +159,8 @@ __device__ inline void half_slab_mfma(const Frags &f, doublex4 (&acc)[FI][FJ]) {
 // workgroup's barrier or on LDS.
 template <bool BF16>
 __global__ __launch_bounds__(NT, 4) void syrk16_kernel(SyrkArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short S[2][2][BT * KC];  // [stage][strip]
+  // [stage][sub-slab][strip]
+  __shared__ __attribute__((aligned(16))) unsigned short S[2][NSUB][2][BT * KC];
   __shared__ unsigned s_unit;
   const int g = blockIdx.x;
   if (a.stamps && threadIdx.x == 0) {
@@ -192,25 +195,41 @@ __global__ __launch_bounds__(NT, 4) void syrk16_kernel(SyrkArgs a) {
     for (int i = 0; i < FI; ++i)
 #pragma unroll
       for (int j = 0; j < FJ; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+    // slab s = NSUB sub-slabs of KC rows; the next slab's sub-slab b goes
+    // from registers to the other stage right after this slab's sub-slab b
+    // has been consumed, and its global loads for sub-slab b + 1 follow (one
+    // sub-slab of registers in flight, a sub-slab of MFMAs to cover them)
+    const int64_t R0 = int64_t(NSUB) * KC;
     Stage st;
-    st.load(a, tm, tn, int64_t(s0) * KC);
-    st.store(S[0][0], S[0][1]);
-    if (s0 + 1 < s1) st.load(a, tm, tn, int64_t(s0 + 1) * KC);
-    __syncthreads();
-    int cur = 0;
-    for (int s = s0; s < s1; ++s) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        Frags f;
-        f.read(S[cur][0], S[cur][1], h);
-        half_slab_mfma<BF16>(f, acc);
-      }
-      if (s + 1 < s1) {
-        st.store(S[cur ^ 1][0], S[cur ^ 1][1]);
-        if (s + 2 < s1) st.load(a, tm, tn, int64_t(s + 2) * KC);
+    for (int b = 0; b < NSUB; ++b) {
+      st.load(a, tm, tn, int64_t(s0) * R0 + b * KC);
+      st.store(S[0][b][0], S[0][b][1]);
+    }
+    if (s0 + 1 < s1) st.load(a, tm, tn, int64_t(s0 + 1) * R0);
+    __syncthreads();
+    // slabs in pairs, so the stage of each is a compile-time index (LDS
+    // addresses become immediates instead of registers)
+    auto slab = [&]<int CUR>(std::integral_constant<int, CUR>, int s) __attribute__((always_inline)) {
+#pragma unroll
+      for (int b = 0; b < NSUB; ++b) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          Frags f;
+          f.read(S[CUR][b][0], S[CUR][b][1], h);
+          half_slab_mfma<BF16>(f, acc);
+        }
+        if (s + 1 < s1) {
+          st.store(S[CUR ^ 1][b][0], S[CUR ^ 1][b][1]);
+          if (b + 1 < NSUB) st.load(a, tm, tn, int64_t(s + 1) * R0 + (b + 1) * KC);
+          else if (s + 2 < s1) st.load(a, tm, tn, int64_t(s + 2) * R0);
+        }
       }
       __syncthreads();
-      cur ^= 1;
+    };
+    for (int s = s0; s < s1; s += 2) {
+      slab(std::integral_constant<int, 0>{}, s);
+      if (s + 1 < s1) slab(std::integral_constant<int, 1>{}, s + 1);
     }
     if (slot < 0) {  // H += acc on the tile, mirrored
 #pragma unroll
@@ -318,7 +337,7 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   a.ldh = ldh;
   const int nt = cdiv(n, BT);
   a.T = nt * (nt + 1) / 2;
-  a.NS = cdiv(rows, KC);
+  a.NS = cdiv(rows, NSUB * KC);
   const int G = resident_groups();
   a.Tt = std::min(a.T, G);
   a.head = a.T - a.Tt;

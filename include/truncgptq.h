@@ -51,9 +51,9 @@ int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n,
 /* The same update with a caller workspace (tg_syrk_workspace_size bytes, a
  * device constant independent of n and rows): fp16 / bf16 X with n and ldx
  * multiples of 8 and a 16-byte aligned X take the dedicated 16-bit SYRK
- * (syrk.hip: X kept 16-bit in LDS, stream-K over the lower 128 x 128 tiles,
- * partial tiles summed in a fixed order -- deterministic for a given
- * device); other inputs fall back to tg_syrk_accum. */
+ * (syrk.hip: X kept 16-bit in LDS, lower 128 x 128 tiles handed out by an
+ * atomic queue over a static decomposition whose partial tiles are summed in
+ * a fixed order -- deterministic); other inputs fall back to tg_syrk_accum. */
 size_t tg_syrk_workspace_size(int n);
 int tg_syrk_accum_ws(void *stream, const void *X, int x_dtype, int64_t rows, int n, int64_t ldx,
                      double *H, int ldh, void *ws, size_t ws_bytes);
@@ -65,7 +65,9 @@ int tg_syrk_accum_ws(void *stream, const void *X, int x_dtype, int64_t rows, int
 int tg_scale_f64(void *stream, const double *H, int64_t count, double inv_n, double *out);
 
 /* FP64 MFMA GEMM used by every dense stage (exported for tests / reuse):
- * C = alpha op(A) op(B) + beta C, row-major, op(A) M x K, op(B) K x N. */
+ * C = alpha op(A) op(B) + beta C, row-major, op(A) M x K, op(B) K x N.
+ * Hand-written kernels only (gemm64.hip: 8-wave 128 x 128 tiles for large
+ * products, 64 x 64 tiles otherwise); no vendor BLAS is linked. */
 int tg_dgemm(void *stream, int transA, int transB, int M, int N, int K, double alpha,
              const double *A, int lda, const double *B, int ldb, double beta, double *C, int ldc);
 

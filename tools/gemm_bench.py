@@ -1,4 +1,5 @@
-"""FP64 GEMM shapes of the solver: tg_dgemm vs torch (hipBLASLt) (development tool)."""
+"""FP64 GEMM shapes of the solver: tg_dgemm (8-wave, 8-wave without the XCD tile order,
+4-wave) vs torch (hipBLASLt / Tensile) (development tool)."""
 import os
 import sys
 
@@ -34,7 +35,7 @@ for name, ta, tb, M, N, K, beta in cases:
     opB = B.T if tb else B
     def ref():
         torch.addmm(C, opA, opB, beta=beta, out=C) if beta else torch.mm(opA, opB, out=C)
-    for fn, lab in ((ours, "own8"), (ours, "own8-2d"), (ours, "rocblas"), (ref, "torch")):
+    for fn, lab in ((ours, "own8"), (ours, "own8-2d"), (ours, "own"), (ref, "torch")):
         os.environ["TG_GEMM_IMPL"] = lab.split("-")[0]
         os.environ["TG_GEMM_SWZ"] = "0" if lab.endswith("-2d") else "1"
         for _ in range(3):
