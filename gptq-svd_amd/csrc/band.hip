@@ -930,9 +930,14 @@ __global__ __launch_bounds__(256) void w_update_kernel(const double *__restrict_
 // with the tile's old values already in flight: the K = 96 kernel above
 // waits out an L2 round trip per 16-deep slab.  Two workgroups per CU.
 constexpr int WT = 64, WK = 2 * SB_B, WP = 4;
+// NP (Y, W) pairs: A22 -= sum_p Y_p W_p^T + W_p Y_p^T (NP = 2: two panels'
+// updates deferred into one pass over A22, K = 128 staged 64 at a time).
+struct YW2 {
+  const double *Y[2], *W[2];  // m x 32 each, leading dimension SB_B
+};
+template <int NP>
 __global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A, int64_t lda, int m,
-                                                         const double *__restrict__ Y,
-                                                         const double *__restrict__ W) {
+                                                         YW2 yw) {
   __shared__ double Aop[WK][WT + WP];
   __shared__ double Bop[WK][WT + WP];
   const int b = blockIdx.x;
@@ -954,50 +959,55 @@ __global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A,
         const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
         old[i][j][r] = A[int64_t(gi) * lda + gj];
       }
-  {
-    // thread: row tid / 4 of the tile, 8 consecutive k (two 16-B loads) of
-    // each of Y_r, W_r, W_c, Y_c
-    const int rl = tid >> 2, k0 = (tid & 3) * 8;
-    const int gr = min(tm + rl, m - 1), gc = min(tn + rl, m - 1);
-    const bool okr = tm + rl < m, okc = tn + rl < m;
-    double2 v[4][4];
-    const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
-                            W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
-#pragma unroll
-    for (int o = 0; o < 4; ++o)
-#pragma unroll
-      for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int k = k0 + 2 * h;
-      Aop[k][rl] = okr ? v[0][h].x : 0.0;
-      Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
-      Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
-      Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
-      Bop[k][rl] = okc ? v[2][h].x : 0.0;
-      Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
-      Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
-      Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
-    }
-  }
-  __syncthreads();
   doublex4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int kq = 0; kq < WK; kq += 4) {
-    double af[2], bf[2];
+  for (int pp = 0; pp < NP; ++pp) {
+    if (pp > 0) __syncthreads();  // the previous pair's operand images are consumed
+    const double *Y = yw.Y[pp], *W = yw.W[pp];
+    {
+      // thread: row tid / 4 of the tile, 8 consecutive k (two 16-B loads) of
+      // each of Y_r, W_r, W_c, Y_c
+      const int rl = tid >> 2, k0 = (tid & 3) * 8;
+      const int gr = min(tm + rl, m - 1), gc = min(tn + rl, m - 1);
+      const bool okr = tm + rl < m, okc = tn + rl < m;
+      double2 v[4][4];
+      const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
+                              W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
 #pragma unroll
-    for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+      for (int o = 0; o < 4; ++o)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+        for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int h = 0; h < 4; ++h) {
+        const int k = k0 + 2 * h;
+        Aop[k][rl] = okr ? v[0][h].x : 0.0;
+        Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
+        Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
+        Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
+        Bop[k][rl] = okc ? v[2][h].x : 0.0;
+        Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
+        Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
+        Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
+      }
+    }
+    __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    for (int kq = 0; kq < WK; kq += 4) {
+      double af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
   }
   __syncthreads();  // operand images dead: Aop becomes the mirror tile
   double(*Tt)[WT + 1] = reinterpret_cast<double(*)[WT + 1]>(&Aop[0][0]);
@@ -1024,6 +1034,166 @@ __global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A,
       if (tn + lc < m && tm + lr < m) A[int64_t(tn + lc) * lda + tm + lr] = Tt[lr][lc];
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Panel pairs (single-level plans): the two-sided update of panel a is
+// deferred and merged with panel b's (the next 32 columns) into one rank-128
+// pass over the trailing matrix.
+//  1. after W_a: panel b's columns (every row of A22_a, the 32 columns at its
+//     left edge, lower part + mirror) get panel a's update now (they are
+//     panel b's QR input and its band diagonal block);
+//  2. panel b's X is formed from the NOT yet updated trailing matrix,
+//     X_raw = A_cur YT_b, and corrected:  X_b = X_raw - Y_a' P - W_a' Q,
+//     P = W_a'^T YT_b, Q = Y_a'^T YT_b (a' = panel a's rows below panel b's
+//     columns); M_b = M_raw - T_b^T (E1 P + E2 Q), E1 = Y_b^T Y_a',
+//     E2 = Y_b^T W_a';
+//  3. one syr2k over A22_b with (Y_a', W_a') and (Y_b, W_b).
+// Per pair the trailing matrix is streamed 3x (two X passes, one update of
+// 1.5x the bytes) instead of 4x.
+// ---------------------------------------------------------------------------
+// 1: A22[i][j] -= sum_l Y[i][l] W[j][l] + W[i][l] Y[j][l] for j < 32,
+// i >= j, mirrored to A22[j][i]; 32 rows x 32 columns per workgroup.
+__global__ __launch_bounds__(256) void panel_upd_kernel(double *__restrict__ A, int64_t lda, int m,
+                                                        const double *__restrict__ Y,
+                                                        const double *__restrict__ W) {
+  __shared__ double yc[SB_B][SB_B + 1], wc[SB_B][SB_B + 1];  // rows 0..31: the columns' factors
+  __shared__ double yr[SB_B][SB_B + 1], wr[SB_B][SB_B + 1];  // this block's 32 rows
+  const int tid = threadIdx.x, i0 = blockIdx.x * SB_B;
+  for (int e = tid; e < SB_B * SB_B; e += 256) {
+    const int r = e >> 5, c = e & 31;
+    yc[r][c] = Y[r * SB_B + c];
+    wc[r][c] = W[r * SB_B + c];
+    const int gi = min(i0 + r, m - 1);
+    yr[r][c] = Y[int64_t(gi) * SB_B + c];
+    wr[r][c] = W[int64_t(gi) * SB_B + c];
+  }
+  __syncthreads();
+  const int j = tid & 31;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int il = (tid >> 5) + 8 * q, i = i0 + il;
+    if (i >= m || i < j) continue;
+    double v = 0.0;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) v = fma(yr[il][l], wc[j][l], v);
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) v = fma(wr[il][l], yc[j][l], v);
+    const double a = A[int64_t(i) * lda + j] - v;
+    A[int64_t(i) * lda + j] = a;
+    if (i != j) A[int64_t(j) * lda + i] = a;
+  }
+}
+
+// 2a: per block of PR rows r of panel b's trailing rows (Ya = Y_a', Wa =
+// W_a', Yb = Y_b, YTb = YT_b, m rows each, ld 32): partial sums of the four
+// 32 x 32 products P = Wa^T YTb, Q = Ya^T YTb, E1 = Yb^T Ya, E2 = Yb^T Wa,
+// to part[blk * 4096 + {0, 1024, 2048, 3072} + 32 l + c].
+constexpr int PR = 128;
+__global__ __launch_bounds__(256) void pair_part_kernel(const double *__restrict__ Ya,
+                                                        const double *__restrict__ Wa,
+                                                        const double *__restrict__ Yb,
+                                                        const double *__restrict__ YTb, int m,
+                                                        double *__restrict__ part) {
+  __shared__ double sa[32][SB_B + 1], sw[32][SB_B + 1], sb[32][SB_B + 1], st[32][SB_B + 1];
+  const int tid = threadIdx.x, r0 = blockIdx.x * PR;
+  // thread: 16 outputs = product pr (tid >> 6), row l (tid & 31), columns c0 .. c0 + 15
+  const int pr = tid >> 6, l = tid & 31, c0 = ((tid >> 5) & 1) * 16;
+  double acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+  for (int rb = r0; rb < min(m, r0 + PR); rb += 32) {
+    __syncthreads();
+    for (int e = tid; e < 32 * SB_B; e += 256) {
+      const int r = e >> 5, c = e & 31, gr = rb + r;
+      const bool ok = gr < m;
+      const int64_t o = int64_t(ok ? gr : 0) * SB_B + c;
+      sa[r][c] = ok ? Ya[o] : 0.0;
+      sw[r][c] = ok ? Wa[o] : 0.0;
+      sb[r][c] = ok ? Yb[o] : 0.0;
+      st[r][c] = ok ? YTb[o] : 0.0;
+    }
+    __syncthreads();
+    // left factor column l, right factor columns c0..: sum over the 32 rows
+    const double(*L)[SB_B + 1] = pr == 0 ? sw : pr == 1 ? sa : sb;
+    const double(*R)[SB_B + 1] = pr <= 1 ? st : pr == 2 ? sa : sw;
+    for (int r = 0; r < 32; ++r) {
+      const double a = L[r][l];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) acc[c] = fma(a, R[r][c0 + c], acc[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) part[size_t(blockIdx.x) * 4096 + pr * 1024 + l * 32 + c0 + c] = acc[c];
+}
+
+// 2b: one workgroup: the four products summed over the blocks in block order
+// -> PQ[0..2047] = {P, Q}; M -= T^T (E1 P + E2 Q) in place.
+__global__ __launch_bounds__(1024) void pair_fin_kernel(const double *__restrict__ part, int nblk,
+                                                        const double *__restrict__ T,
+                                                        double *__restrict__ M,
+                                                        double *__restrict__ PQ) {
+  __shared__ double S[4][SB_B][SB_B + 1], D[SB_B][SB_B + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 4096; e += 1024) {
+    double v = 0.0;
+    for (int z = 0; z < nblk; ++z) v += part[size_t(z) * 4096 + e];
+    S[e >> 10][(e >> 5) & 31][e & 31] = v;
+    if (e < 2048) PQ[e] = v;
+  }
+  __syncthreads();
+  {  // D = E1 P + E2 Q
+    const int a = tid >> 5, c = tid & 31;
+    double v = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < SB_B; ++k) v = fma(S[2][a][k], S[0][k][c], v);
+#pragma unroll 8
+    for (int k = 0; k < SB_B; ++k) v = fma(S[3][a][k], S[1][k][c], v);
+    D[a][c] = v;
+  }
+  __syncthreads();
+  {  // M -= T^T D (T upper triangular: column a of T has rows k <= a)
+    const int a = tid >> 5, c = tid & 31;
+    double v = 0.0;
+    for (int k = 0; k <= a; ++k) v = fma(T[k * SB_B + a], D[k][c], v);
+    M[a * SB_B + c] -= v;
+  }
+}
+
+// 2c: W_b = X_raw - Ya P - Wa Q - 1/2 Yb M_b in place over X (as
+// w_update_kernel, two more 32-term products).
+__global__ __launch_bounds__(256) void w_update2_kernel(const double *__restrict__ Yb,
+                                                        double *__restrict__ X, int m,
+                                                        const double *__restrict__ M,
+                                                        const double *__restrict__ Ya,
+                                                        const double *__restrict__ Wa,
+                                                        const double *__restrict__ PQ) {
+  __shared__ double2 Ms[SB_B][SB_B / 2], Ps[SB_B][SB_B / 2], Qs[SB_B][SB_B / 2];
+  const int tid = threadIdx.x;
+  const int r = blockIdx.x * WU_R + (tid >> 4), c2 = tid & 15;
+  const int rc = min(r, m - 1);
+  for (int e = tid; e < SB_B * SB_B / 2; e += 256) {
+    Ms[e >> 4][e & 15] = reinterpret_cast<const double2 *>(M)[e];
+    Ps[e >> 4][e & 15] = reinterpret_cast<const double2 *>(PQ)[e];
+    Qs[e >> 4][e & 15] = reinterpret_cast<const double2 *>(PQ + 1024)[e];
+  }
+  const double2 x = reinterpret_cast<const double2 *>(X + int64_t(rc) * SB_B)[c2];
+  __syncthreads();
+  double v0 = 0.0, v1 = 0.0, u0 = 0.0, u1 = 0.0;
+  for (int h = 0; h < SB_B; ++h) {
+    const double yb = Yb[int64_t(rc) * SB_B + h], ya = Ya[int64_t(rc) * SB_B + h],
+                 wa = Wa[int64_t(rc) * SB_B + h];
+    const double2 mm = Ms[h][c2], pp = Ps[h][c2], qq = Qs[h][c2];
+    v0 = fma(yb, mm.x, v0);
+    v1 = fma(yb, mm.y, v1);
+    u0 = fma(ya, pp.x, u0);
+    u1 = fma(ya, pp.y, u1);
+    u0 = fma(wa, qq.x, u0);
+    u1 = fma(wa, qq.y, u1);
+  }
+  if (r < m)
+    reinterpret_cast<double2 *>(X + int64_t(r) * SB_B)[c2] =
+        make_double2((x.x - u0) - 0.5 * v0, (x.y - u1) - 0.5 * v1);
 }
 
 // dst[s][:] = src[map(s)][:]
@@ -1159,11 +1329,42 @@ static hipError_t side_stream(SideStream *&out) {
 // a whole CU's LDS and wait for the trailing update to drain; the same on
 // CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
 // triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
+// X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
+static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const double *YT,
+                            const double *Yp, const double *Tp, double *X, const SbBufs &b) {
+  const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
+  const int nbc = fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
+  const int G = cdiv(m, XR * nbc);
+  XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
+  if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
+  else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
+  return hipGetLastError();
+}
+
+// Panel pairs (see panel_upd_kernel) with TG_SB_PAIR=1 (read per call), for
+// panels whose partner has at least PAIR_MIN trailing rows; the workspace's
+// X holds n x ncmax*32 doubles, so two m x 32 slabs fit once n >= 2 SB_C.
+// Measured at n = 12,288 (rocprofv3): the merged rank-128
+// update saves 20 ms of the 62 ms of rank-64 updates, but the corrections'
+// cross-row reductions (pair_part 27 us + the one-workgroup pair_fin 66 us
+// per pair, latency-bound) cost as much; at n = 4096 the pairs are 2.7 ms
+// slower.  Off by default until the reductions ride on the X / M kernel's.
+constexpr int PAIR_MIN = 256;
+
+// One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
+// (Measured and removed in round 3's clean-up, DESIGN.md §5: a look-ahead
+// with the next panel's QR on a side stream, +5 ms -- the QR's workgroups need
+// a whole CU's LDS and wait for the trailing update to drain; the same on
+// CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
+// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
   TG_CHK(hipMemsetAsync(b.xm_tick, 0, sizeof(unsigned) * xm_tick_words(n), st));
   const int np = int(pl.panels.size());
+  const char *pe = getenv("TG_SB_PAIR");
+  const bool pairs = (pe && pe[0] == '1') && pl.ncmax >= 2;
+  double *Xa = b.X, *Xb = b.X + size_t(n) * SB_B;
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
     const int m = P.m, r0 = P.r0;
@@ -1171,23 +1372,45 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
     TG_CHK(panel_qr(st, A, lda, P.p, P.r0, P.m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    // X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
-    {
-      const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
-      const int nbc = fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
-      const int G = cdiv(m, XR * nbc);
-      XmArgs xa{A22, int64_t(lda), m, b.YT, Yp, Tp, b.X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
-      if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
-      else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
-      TG_CHK(hipGetLastError());
-    }
-    // W = X - Y M / 2 in place, then A22 -= Y W^T + W Y^T
-    hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, b.X, m, b.M);
+    TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b));
+    // W = X - Y M / 2 in place
+    hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
     TG_CHK(hipGetLastError());
-    const int nt = cdiv(m, WT);
-    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
-    hipLaunchKernelGGL(syr2k_w_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                       int64_t(lda), m, Yp, b.X);
+    const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= PAIR_MIN;
+    if (!pair) {  // A22 -= Y W^T + W Y^T
+      const int nt = cdiv(m, WT);
+      auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
+      hipLaunchKernelGGL(syr2k_w_kernel<1>, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
+                         int64_t(lda), m, YW2{{Yp, nullptr}, {Xa, nullptr}});
+      prof_end(st, tok);
+      TG_CHK(hipGetLastError());
+      continue;
+    }
+    // panel b = pi + 1: its columns get panel a's update now
+    hipLaunchKernelGGL(panel_upd_kernel, dim3(cdiv(m, SB_B)), dim3(256), 0, st, A22,
+                       int64_t(lda), m, Yp, Xa);
+    TG_CHK(hipGetLastError());
+    ++pi;
+    const SbPanel &Q = pl.panels[pi];
+    const int mb = Q.m;
+    double *A22b = A + int64_t(Q.r0) * lda + Q.r0;
+    double *Yb = b.Y + Q.L[0].yoff, *Tb = b.T + Q.L[0].toff;
+    const double *Ya = Yp + SB_B * SB_B, *Wa = Xa + SB_B * SB_B;  // panel a's rows >= Q.r0
+    TG_CHK(panel_qr(st, A, lda, Q.p, Q.r0, Q.m, Yb, b.YT, Tb, b.pq_part, b.pq_bc,
+                    b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
+    TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
+    const int nblk = cdiv(mb, PR);
+    hipLaunchKernelGGL(pair_part_kernel, dim3(nblk), dim3(256), 0, st, Ya, Wa, Yb, b.YT, mb, b.U);
+    TG_CHK(hipGetLastError());
+    hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, st, b.U, nblk, Tb, b.M, b.G);
+    TG_CHK(hipGetLastError());
+    hipLaunchKernelGGL(w_update2_kernel, dim3(cdiv(mb, WU_R)), dim3(256), 0, st, Yb, Xb, mb, b.M,
+                       Ya, Wa, b.G);
+    TG_CHK(hipGetLastError());
+    const int nt = cdiv(mb, WT);
+    auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(mb) * mb, 128.0 * double(mb) * mb);
+    hipLaunchKernelGGL(syr2k_w_kernel<2>, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22b,
+                       int64_t(lda), mb, YW2{{Ya, Yb}, {Wa, Xb}});
     prof_end(st, tok);
     TG_CHK(hipGetLastError());
   }

@@ -307,7 +307,7 @@ int resident_groups() {
 
 namespace tg {
 
-constexpr int NCMAX = 4;  // chunks per tail tile
+constexpr int NCMAX = 4;  // chunks per tail tile (G tail tiles)
 
 // Layout: partial tiles (G tail tiles x NCMAX chunks), the queue head, the
 // TG_SYRK_STAMPS clocks (3 words per workgroup).
@@ -323,9 +323,12 @@ bool syrk16_supported(const void *X, int n, int64_t ldx) {
 // Decomposition (static, so H does not depend on which workgroup ran what):
 // the last min(T, G) tiles are cut into NCMAX chunks of K, every other tile
 // is one unit; units are handed out by an atomic queue, so a workgroup that
-// runs faster (the older of the two on a CU wins the issue arbitration: their
-// times differ by up to 1.8x, TG_SYRK_STAMPS) simply takes more of them, and
-// the last round is made of quarter tiles.
+// runs faster (the older of the two on a CU wins the issue arbitration: with
+// equal static shares their times differed by up to 1.8x, TG_SYRK_STAMPS)
+// simply takes more of them, and the last round is made of quarter tiles.
+// (Eighth tiles over the last G / 2 tiles measured slower at n = 4096, 24.8
+// against 19.8 ms: the whole tiles then handed to the slower workgroups of
+// the first round finish last.)
 hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n, int64_t ldx,
                   double *H, int64_t ldh, void *ws) {
   SyrkArgs a{};

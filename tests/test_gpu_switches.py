@@ -1,9 +1,9 @@
 """Every path-selecting developer switch left in the library, on the GPU:
 each alternative path must reproduce the default path on the same Hessian
 (perm identical, U / R_x to 1e-10, the quantised weights bit-identical).
-n = 2048 (rank 1536): large enough that the GEMMs take the rocBLAS branch
-(TG_NO_ROCBLAS covers the in-house FP64 GEMM in its place) and both spectral
-paths exist.  The switches are read per call."""
+n = 2048 (rank 1536): large enough that the GEMMs take the 128-tile kernels
+(TG_GEMM_IMPL=own selects the 4-wave one, TG_GEMM_TILE forces a tile) and
+both spectral paths exist.  The switches are read per call."""
 import numpy as np
 import pytest
 import torch
@@ -44,9 +44,12 @@ def rel(a, b):
     {"TG_INVIT_REG": "1"},
     {"TG_BT_MULTI": "1"},
     {"TG_URX_TWOCHOL": "1"},
-    {"TG_NO_ROCBLAS": "1"},
-    {"TG_NO_ROCBLAS": "1", "TG_GEMM_TILE": "128"},
-    {"TG_NO_ROCBLAS": "1", "TG_GEMM_TILE": "12864"},
+    {"TG_GEMM_IMPL": "own"},
+    {"TG_GEMM_TILE": "128"},
+    {"TG_GEMM_TILE": "12864"},
+    {"TG_GEMM_TILE": "64"},
+    {"TG_GEMM_SWZ": "0", "TG_GEMM_TILE": "128"},
+    {"TG_SB_PAIR": "1"},
     {"TG_XM_NBC": "2"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},

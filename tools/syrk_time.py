@@ -45,7 +45,7 @@ if __import__("os").environ.get("TG_SYRK_STAMPS"):
         acc.add_batch(X)
         acc.add_batch(X)
         torch.cuda.synchronize()
-        G = (acc._ws.numel() // 8 - 64) // (4 * 128 * 128 + 3)
+        G = (acc._ws.numel() // 8 - 64) // (4 * 128 * 128 + 3)  # G x 4 partial tiles
         off = (G * 4 * 128 * 128 + 64) * 8
         st = acc._ws[off:off + 24 * G].view(torch.int64).cpu().numpy().reshape(G, 3)
         t0 = st[:, 0].min()
