@@ -1036,6 +1036,130 @@ __global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A,
   }
 }
 
+// Persistent form of syr2k_w_kernel<1> (the default): two workgroups per CU
+// loop over the lower tiles; while a tile's operands are staged, multiplied
+// and written back, the NEXT tile's old values are already loading (issued
+// after this tile's operand loads, so waiting for those leaves them in
+// flight).  The one-tile-per-workgroup form left the memory pipe idle
+// through every workgroup's MFMA, epilogue and dispatch: 3.7 TB/s on the
+// HBM-resident trailing matrices of n >= 12,288.
+__device__ __forceinline__ void syr2k_tile(int b, int &tm, int &tn) {
+  int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= b) ++I;
+  while (I * (I + 1) / 2 > b) --I;
+  tm = I * WT;
+  tn = (b - I * (I + 1) / 2) * WT;
+}
+__global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A, int64_t lda,
+                                                          int m, const double *__restrict__ Y,
+                                                          const double *__restrict__ W,
+                                                          int ntiles) {
+  __shared__ double Aop[WK][WT + WP];
+  __shared__ double Bop[WK][WT + WP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int b = blockIdx.x;
+  if (b >= ntiles) return;
+  auto load_old = [&](int tb, double (&o)[2][2][4]) __attribute__((always_inline)) {
+    int tm, tn;
+    syr2k_tile(tb, tm, tn);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = min(tm + wm * 32 + i * 16 + (lane >> 4) + 4 * r, m - 1);
+          const int gj = min(tn + wn * 32 + j * 16 + (lane & 15), m - 1);
+          o[i][j][r] = A[int64_t(gi) * lda + gj];
+        }
+  };
+  double old[2][2][4], nold[2][2][4];
+  load_old(b, old);
+  for (; b < ntiles; b += gridDim.x) {
+    int tm, tn;
+    syr2k_tile(b, tm, tn);
+    __syncthreads();  // the previous tile's mirror reads of Aop are done
+    const int rl = tid >> 2, k0 = (tid & 3) * 8;
+    const int gr = min(tm + rl, m - 1), gc = min(tn + rl, m - 1);
+    const bool okr = tm + rl < m, okc = tn + rl < m;
+    double2 v[4][4];
+    {
+      const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
+                              W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int bn = b + int(gridDim.x);
+    if (bn < ntiles) load_old(bn, nold);  // in flight through this tile
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int k = k0 + 2 * h;
+      Aop[k][rl] = okr ? v[0][h].x : 0.0;
+      Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
+      Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
+      Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
+      Bop[k][rl] = okc ? v[2][h].x : 0.0;
+      Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
+      Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
+      Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
+    }
+    __syncthreads();
+    doublex4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kq = 0; kq < WK; kq += 4) {
+      double af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // operand images dead: Aop becomes the mirror tile
+    double(*Tt)[WT + 1] = reinterpret_cast<double(*)[WT + 1]>(&Aop[0][0]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int li = wm * 32 + i * 16 + (lane >> 4) + 4 * r, lj = wn * 32 + j * 16 + (lane & 15);
+          const int gi = tm + li, gj = tn + lj;
+          if (gi < m && gj < m && gi >= gj) {
+            const double val = old[i][j][r] - acc[i][j][r];
+            A[int64_t(gi) * lda + gj] = val;
+            if (tm != tn) Tt[li][lj] = val;
+            else if (gi != gj) A[int64_t(gj) * lda + gi] = val;
+          }
+        }
+    if (tm != tn) {  // uniform per workgroup
+      __syncthreads();
+      for (int idx = tid; idx < WT * WT; idx += 256) {
+        const int lc = idx >> 6, lr = idx & 63;  // row tn + lc, column tm + lr
+        if (tn + lc < m && tm + lr < m) A[int64_t(tn + lc) * lda + tm + lr] = Tt[lr][lc];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[i][j][r] = nold[i][j][r];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Panel pairs (single-level plans): the two-sided update of panel a is
 // deferred and merged with panel b's (the next 32 columns) into one rank-128
@@ -1364,6 +1488,11 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   const int np = int(pl.panels.size());
   const char *pe = getenv("TG_SB_PAIR");
   const bool pairs = (pe && pe[0] == '1') && pl.ncmax >= 2;
+  // TG_SYR2K_PERSIST=0: one tile per workgroup (development switch, per call)
+  const char *ps = getenv("TG_SYR2K_PERSIST");
+  const bool persist = !(ps && ps[0] == '0');
+  const XcdInfo xi = xcd_info();
+  const int ncu = std::max(1, xi.xcds * xi.cus_per_xcd);
   double *Xa = b.X, *Xb = b.X + size_t(n) * SB_B;
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
@@ -1378,10 +1507,14 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     TG_CHK(hipGetLastError());
     const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= PAIR_MIN;
     if (!pair) {  // A22 -= Y W^T + W Y^T
-      const int nt = cdiv(m, WT);
+      const int nt = cdiv(m, WT), tiles = nt * (nt + 1) / 2;
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
-      hipLaunchKernelGGL(syr2k_w_kernel<1>, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22,
-                         int64_t(lda), m, YW2{{Yp, nullptr}, {Xa, nullptr}});
+      if (persist)
+        hipLaunchKernelGGL(syr2k_wp_kernel, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st, A22,
+                           int64_t(lda), m, Yp, Xa, tiles);
+      else
+        hipLaunchKernelGGL(syr2k_w_kernel<1>, dim3(tiles), dim3(256), 0, st, A22, int64_t(lda), m,
+                           YW2{{Yp, nullptr}, {Xa, nullptr}});
       prof_end(st, tok);
       TG_CHK(hipGetLastError());
       continue;

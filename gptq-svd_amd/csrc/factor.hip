@@ -1163,6 +1163,130 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
   }
 }
 
+// Persistent form of syrk_compact_kernel (the default): two workgroups per
+// CU loop over the tiles of the leading (n - ps2)^2 block (its size read on
+// the device); the next tile's gathered old values are loaded while this
+// tile is multiplied and written (its row / column indices one step earlier
+// still), so the memory pipe does not idle through each workgroup's MFMA,
+// epilogue and dispatch.  Same arithmetic per entry as syrk_compact_kernel.
+__global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
+                                                                const double *__restrict__ Hc,
+                                                                double *__restrict__ Hn) {
+  __shared__ double li[PB][64], lj[PB][64];
+  __shared__ double tt[64][65];
+  const int tid = threadIdx.x;
+  const int ps2 = w.sstate[0], tn = max(w.sstate[1], 0);
+  const int nc = n - ps2;
+  if (nc <= 0) return;
+  const int ntile = tg::cdiv(nc, 64), tiles = ntile * (ntile + 1) / 2;
+  const int lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  auto tile_ij = [&](int b, int &i0, int &j0) __attribute__((always_inline)) {
+    int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= b) ++I;
+    while (I * (I + 1) / 2 > b) --I;
+    i0 = 64 * I;
+    j0 = 64 * (b - I * (I + 1) / 2);
+  };
+  // this thread's gathered rows (ib, q) and columns (jb) of a tile
+  auto load_idx = [&](int b, int (&ro)[2][4], int (&co)[2]) __attribute__((always_inline)) {
+    int i0, j0;
+    tile_ij(b, i0, j0);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ro[ib][q] = w.oidx[tn + min(i0 + wm * 32 + ib * 16 + lk + 4 * q, nc - 1)];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) co[jb] = w.oidx[tn + min(j0 + wn * 32 + jb * 16 + lr, nc - 1)];
+  };
+  auto load_old = [&](const int (&ro)[2][4], const int (&co)[2], double (&o)[2][2][4])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[ib][jb][q] = Hc[size_t(ro[ib][q]) * n + co[jb]];
+  };
+  int b = blockIdx.x;
+  if (b >= tiles) return;
+  int ro[2][4], co[2];
+  double old[2][2][4], nold[2][2][4];
+  load_idx(b, ro, co);
+  load_old(ro, co, old);
+  const int G = int(gridDim.x);
+  if (b + G < tiles) load_idx(b + G, ro, co);
+  for (; b < tiles; b += G) {
+    int i0, j0;
+    tile_ij(b, i0, j0);
+    __syncthreads();  // the previous tile's reads of li, lj, tt are done
+    double lv[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + u * 256, l = e >> 6, c = e & 63;
+      lv[u][0] = w.LT[size_t(l) * n + min(i0 + c, nc - 1)];
+      lv[u][1] = w.LT[size_t(l) * n + min(j0 + c, nc - 1)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = b + G < tiles;
+    if (more) load_old(ro, co, nold);  // in flight through this tile
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + u * 256, l = e >> 6, c = e & 63;
+      li[l][c] = lv[u][0];
+      lj[l][c] = lv[u][1];
+    }
+    __syncthreads();
+    if (b + 2 * G < tiles) load_idx(b + 2 * G, ro, co);
+    doublex4 acc[2][2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[ib][jb][q] = old[ib][jb][q];
+#pragma unroll
+    for (int kq = 0; kq < PB; kq += 4) {
+      double af[2], bf[2];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) af[ib] = -li[kq + lk][wm * 32 + ib * 16 + lr];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) bf[jb] = lj[kq + lk][wn * 32 + jb * 16 + lr];
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[ib], bf[jb], acc[ib][jb], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = wm * 32 + ib * 16 + lk + 4 * q, cl = wn * 32 + jb * 16 + lr;
+          const int gi = i0 + rl, gj = j0 + cl;
+          if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
+          tt[cl][rl] = acc[ib][jb][q];
+        }
+    if (i0 != j0) {  // uniform: mirror rows j0 .. j0 + 63, columns i0 .. i0 + 63
+      __syncthreads();
+      for (int e = tid; e < 64 * 64; e += 256) {
+        const int rr = e >> 6, cc = e & 63;
+        const int gi = j0 + rr, gj = i0 + cc;
+        if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = tt[rr][cc];
+      }
+    }
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[ib][jb][q] = nold[ib][jb][q];
+  }
+}
+
 // dsc = diag(Hk), perm = pos = identity, no pivot chosen yet.
 __global__ __launch_bounds__(256) void piv_init2_kernel(int n, PivWs w) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
@@ -1743,12 +1867,21 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   if (lds > 48 * 1024)
     TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  // TG_SYR2K_PERSIST=0: one tile per workgroup (development switch, per call)
+  const char *ps = getenv("TG_SYR2K_PERSIST");
+  const bool persist = !(ps && ps[0] == '0');
+  const tg::XcdInfo xi = tg::xcd_info();
+  const int ncu = std::max(1, xi.xcds * xi.cus_per_xcd);
   // compacted Schur complements alternate between the two buffers
   const double *hc = w.Hk;
   double *hn = w.Hk2;
   auto schur_compact = [&](int rows) -> hipError_t {
     const int nt = tg::cdiv(rows, 64);
-    hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc, hn);
+    if (persist)
+      hipLaunchKernelGGL(syrk_compact_p_kernel, dim3(std::min(nt * (nt + 1) / 2, 2 * ncu)),
+                         dim3(256), 0, st, n, w, hc, hn);
+    else
+      hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc, hn);
     const hipError_t e = hipGetLastError();
     double *t = const_cast<double *>(hc);
     hc = hn;
