@@ -130,6 +130,73 @@ def test_token_sharded_harness_matches_single():
         assert np.array_equal(r0["W"][name], W1[name]), name
 
 
+def test_early_stop_matches_full_layer_passes():
+    """A calibration pass that stops at the group's first linear (forward
+    pre-hook, harness.quantize_model(early_stop=True)) accumulates the same
+    H, hence the same weights, as running the whole layer (the reference,
+    quantize.py:139-148, discards the output)."""
+    import gptq_svd_amd.harness as harness
+    gen = torch.Generator().manual_seed(4)
+    ids = [torch.randint(0, 256, (1, 16), generator=gen) for _ in range(5)]
+    out = []
+    for early in (True, False):
+        hs = []
+        _patch(harness, hs)
+        model = tiny_opt(5)
+        harness.quantize_model(model, ids, mode="eigh", w_bits=4, group_size=64, sym=False,
+                               eps=1e-3, threshold_method="energy", batch_size=2, device="cpu",
+                               early_stop=early)
+        out.append((hs, {n: p.detach().clone() for n, p in model.named_parameters()}))
+    (h1, w1), (h2, w2) = out
+    assert len(h1) == len(h2) == 8
+    for a, b in zip(h1, h2):
+        assert torch.equal(a, b)
+    for n in w1:
+        assert torch.equal(w1[n], w2[n]), n
+
+
+def _factor_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from gptq_svd_amd.harness import check_factor_agrees, quantize_model
+        R = torch.arange(12, dtype=torch.float64).reshape(3, 4)
+        perm = torch.tensor([2, 0, 3, 1])
+        check_factor_agrees(R, perm)  # identical on both ranks: passes
+        res = {}
+        R2 = R.clone()
+        if rank == 1:
+            R2[1, 2] += 1e-13  # one rank's factor differs in the last bits
+        try:
+            check_factor_agrees(R2, perm)
+            res["mismatch"] = "no error"
+        except RuntimeError as e:
+            res["mismatch"] = "RuntimeError" if "disagree" in str(e) else str(e)
+        # fewer calibration sequences than ranks: every rank raises before a collective
+        try:
+            quantize_model(torch.nn.Linear(2, 2), [torch.zeros(1, 4, dtype=torch.long)],
+                           device="cpu")
+            res["few"] = "no error"
+        except ValueError as e:
+            res["few"] = "ValueError" if "fewer calibration sequences" in str(e) else str(e)
+        out[rank] = res
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_factor_agreement_and_short_calibration_raise_on_every_rank():
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_factor_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in (0, 1):
+        assert out[r]["mismatch"] == "RuntimeError", out[r]
+        assert out[r]["few"] == "ValueError", out[r]
+
+
 def test_allreduce_hessian_single_process_is_noop():
     from gptq_svd_amd.harness import allreduce_hessian
 
