@@ -768,19 +768,32 @@ __device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e)
   return s;
 }
 
+// NBC = 2 (m >= XM_WIDE, the HBM-resident trailing matrices): two
+// workgroups per CU -- 6 K steps in flight per wave (<= 128 registers) and
+// the Y / X rows of the block staged in the reduction buffer once it is free
+// (<= 80 KB of LDS), so one workgroup's reductions and ramp-up overlap the
+// other's stream; at 1 per CU the stream paused through both.
 template <int NBC>
-__global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
+constexpr int xm_depth() { return NBC == 2 ? 6 : XDA; }
+template <int NBC>
+__global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g) {
   constexpr int RB = XR * NBC;                // rows of X per workgroup
+  constexpr int DA = xm_depth<NBC>();
   __shared__ double red[XW][RB][SB_B + 1];   // the last workgroup reuses it for C, T
-  __shared__ double xs[RB][SB_B + 1], ys[RB][SB_B + 1];
+  static_assert(XW >= 2, "xs and ys alias red[0] and red[1]");
+  double(*xs)[SB_B + 1] = red[0];
+  double(*ys)[SB_B + 1] = red[1];
   __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform K loop
   const int r0 = blockIdx.x * RB;
   const int G = int(gridDim.x), NG = (G + XG - 1) / XG;
-  for (int e = tid; e < RB * SB_B; e += 64 * XW) {
-    const int rr = e >> 5, c = e & 31, row = r0 + rr;
-    ys[rr][c] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
+  constexpr int YPT = RB * SB_B / (64 * XW);  // Y values per thread
+  double yv[YPT];
+#pragma unroll
+  for (int u = 0; u < YPT; ++u) {
+    const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31, row = r0 + rr;
+    yv[u] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
   }
   // wave w takes the K steps w, w + XW, ... (4 rows of A22 each)
   const int KS = 4 * XW, kb = 4 * wid;
@@ -799,22 +812,22 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
     for (int i = 0; i < 2; ++i) acc[c][i] = doublex4{0.0, 0.0, 0.0, 0.0};
   if (kb < g.m) {
     const int nit = (g.m - kb + KS - 1) / KS;
-    XmStep<NBC> f[XDA];
+    XmStep<NBC> f[DA];
 #pragma unroll
-    for (int u = 0; u < XDA; ++u) xm_load<NBC>(g, colc, kb + KS * u, f[u]);
+    for (int u = 0; u < DA; ++u) xm_load<NBC>(g, colc, kb + KS * u, f[u]);
     // (the compiler drains vmcnt to 0 at the loop header -- the slots are
     // loop-carried -- and waits only for the slot in use inside the body;
     // unrolling 4 or 8 rounds per iteration measured no faster)
-    for (int it = 0; it < nit; it += XDA) {
+    for (int it = 0; it < nit; it += DA) {
 #pragma unroll
-      for (int u = 0; u < XDA; ++u) {
+      for (int u = 0; u < DA; ++u) {
         // scheduling barriers keep the issue order (MFMAs on step it + u,
-        // then the load of step it + u + XDA into the freed slot): the
+        // then the load of step it + u + DA into the freed slot): the
         // machine scheduler otherwise sinks prefetches next to their uses
         const int k0 = kb + KS * (it + u);
         xm_mma<NBC>(f[u], cok, k0, acc, g.m);
         __builtin_amdgcn_sched_barrier(0);
-        xm_load<NBC>(g, colc, k0 + KS * XDA, f[u]);
+        xm_load<NBC>(g, colc, k0 + KS * DA, f[u]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -828,13 +841,22 @@ __global__ __launch_bounds__(64 * XW) void xm_kernel(XmArgs g) {
       for (int q = 0; q < 4; ++q)
         red[wid][16 * c + (lane & 15)][16 * i + (lane >> 4) + 4 * q] = acc[c][i][q];
   __syncthreads();
-  for (int e = tid; e < RB * SB_B; e += 64 * XW) {
-    const int rr = e >> 5, c = e & 31;
+  double xv[YPT];
+#pragma unroll
+  for (int u = 0; u < YPT; ++u) {
+    const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31;
     double x = 0.0;
 #pragma unroll
     for (int w = 0; w < XW; ++w) x += red[w][rr][c];
     if (r0 + rr < g.m) g.X[int64_t(r0 + rr) * SB_B + c] = x;
-    xs[rr][c] = r0 + rr < g.m ? x : 0.0;
+    xv[u] = r0 + rr < g.m ? x : 0.0;
+  }
+  __syncthreads();  // red is free: its first two slices take the block's X and Y rows
+#pragma unroll
+  for (int u = 0; u < YPT; ++u) {
+    const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31;
+    xs[rr][c] = xv[u];
+    ys[rr][c] = yv[u];
   }
   __syncthreads();
   // this block's Y_zᵀ X_z, write-through, then the group ticket
