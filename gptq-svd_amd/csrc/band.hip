@@ -1274,10 +1274,10 @@ __global__ __launch_bounds__(256) void pair_part_kernel(const double *__restrict
 }
 
 // 2b: one workgroup: the four products summed over the blocks in block order
-// -> PQ[0..2047] = {P, Q}; M -= T^T (E1 P + E2 Q) in place.
+// -> PQ[0..2047] = {P, Q}, PQ[2048..3071] = T^T (E1 P + E2 Q) (subtracted
+// from M_raw by w_update2_kernel).
 __global__ __launch_bounds__(1024) void pair_fin_kernel(const double *__restrict__ part, int nblk,
                                                         const double *__restrict__ T,
-                                                        double *__restrict__ M,
                                                         double *__restrict__ PQ) {
   __shared__ double S[4][SB_B][SB_B + 1], D[SB_B][SB_B + 1];
   const int tid = threadIdx.x;
@@ -1298,11 +1298,11 @@ __global__ __launch_bounds__(1024) void pair_fin_kernel(const double *__restrict
     D[a][c] = v;
   }
   __syncthreads();
-  {  // M -= T^T D (T upper triangular: column a of T has rows k <= a)
+  {  // T^T D (T upper triangular: column a of T has rows k <= a)
     const int a = tid >> 5, c = tid & 31;
     double v = 0.0;
     for (int k = 0; k <= a; ++k) v = fma(T[k * SB_B + a], D[k][c], v);
-    M[a * SB_B + c] -= v;
+    PQ[2048 + a * SB_B + c] = v;
   }
 }
 
@@ -1319,7 +1319,9 @@ __global__ __launch_bounds__(256) void w_update2_kernel(const double *__restrict
   const int r = blockIdx.x * WU_R + (tid >> 4), c2 = tid & 15;
   const int rc = min(r, m - 1);
   for (int e = tid; e < SB_B * SB_B / 2; e += 256) {
-    Ms[e >> 4][e & 15] = reinterpret_cast<const double2 *>(M)[e];
+    const double2 mr = reinterpret_cast<const double2 *>(M)[e];
+    const double2 td = reinterpret_cast<const double2 *>(PQ + 2048)[e];
+    Ms[e >> 4][e & 15] = make_double2(mr.x - td.x, mr.y - td.y);  // M_b = M_raw - T^T D
     Ps[e >> 4][e & 15] = reinterpret_cast<const double2 *>(PQ)[e];
     Qs[e >> 4][e & 15] = reinterpret_cast<const double2 *>(PQ + 1024)[e];
   }
@@ -1515,6 +1517,8 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   const bool persist = !(ps && ps[0] == '0');
   const XcdInfo xi = xcd_info();
   const int ncu = std::max(1, xi.xcds * xi.cus_per_xcd);
+  SideStream *ss = nullptr;
+  if (pairs) TG_CHK(side_stream(ss));
   double *Xa = b.X, *Xb = b.X + size_t(n) * SB_B;
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
@@ -1553,12 +1557,19 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     const double *Ya = Yp + SB_B * SB_B, *Wa = Xa + SB_B * SB_B;  // panel a's rows >= Q.r0
     TG_CHK(panel_qr(st, A, lda, Q.p, Q.r0, Q.m, Yb, b.YT, Tb, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
+    // the corrections' products depend only on panel b's QR and panel a's
+    // Y / W: a side stream forms them while X_raw streams the matrix
     const int nblk = cdiv(mb, PR);
-    hipLaunchKernelGGL(pair_part_kernel, dim3(nblk), dim3(256), 0, st, Ya, Wa, Yb, b.YT, mb, b.U);
+    TG_CHK(hipEventRecord(ss->ev0[0], st));
+    TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[0], 0));
+    hipLaunchKernelGGL(pair_part_kernel, dim3(nblk), dim3(256), 0, ss->s, Ya, Wa, Yb, b.YT, mb,
+                       b.Gr);
     TG_CHK(hipGetLastError());
-    hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, st, b.U, nblk, Tb, b.M, b.G);
+    hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, ss->s, b.Gr, nblk, Tb, b.G);
     TG_CHK(hipGetLastError());
+    TG_CHK(hipEventRecord(ss->ev1[0], ss->s));
+    TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
+    TG_CHK(hipStreamWaitEvent(st, ss->ev1[0], 0));
     hipLaunchKernelGGL(w_update2_kernel, dim3(cdiv(mb, WU_R)), dim3(256), 0, st, Yb, Xb, mb, b.M,
                        Ya, Wa, b.G);
     TG_CHK(hipGetLastError());
