@@ -51,6 +51,7 @@ def rel(a, b):
     {"TG_GEMM_SWZ": "0", "TG_GEMM_TILE": "128"},
     {"TG_SB_PAIR": "1"},
     {"TG_SYR2K_PERSIST": "0"},
+    {"TG_BULGE_MULTI": "1"},
     {"TG_XM_NBC": "2"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},

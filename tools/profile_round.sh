@@ -1,29 +1,41 @@
 #!/bin/bash
 # Round profile: kernel trace + stats over bench.py, then one PMC pass per
 # counter (FETCH_SIZE, WRITE_SIZE) on the bulge chase and the two streaming
-# band-reduction kernels (X/M and the rank-64 update), then the per-class traffic JSON, then the default
-# bench line (with the CPU baseline).  Every GPU step has its own limit and
+# band-reduction kernels (X/M and the rank-64 update) at n = 4096, the same
+# two passes over one n = 12,288 solve (band update, X/M and the pivot
+# order's Schur updates: HBM-resident there), then the per-class traffic
+# JSONs, then the default bench line.  Every GPU step has its own limit and
 # the steps are chained, so the first failure ends the script.
-# usage: tools/profile_round.sh OUTDIR [KERNEL_REGEX]
+# usage: tools/profile_round.sh OUTDIR
 set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/${1:-gpurun_out/prof}
-KRE=${2:-bulge_lds_kernel|syr2k_w_kernel|xm_kernel}
+KRE="bulge_lds_kernel|syr2k_w|xm_kernel"
+LRE="syr2k_w|xm_kernel|syrk_compact"
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-large-n > "$OUT/trace_bench.log" 2>&1
+  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-large-n --no-e2e > "$OUT/trace_bench.log" 2>&1
 echo "trace done"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "$KRE" -f csv -d "$OUT/pmc_$C" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-syrk --no-large-n > "$OUT/pmc_$C.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-syrk --no-large-n --no-e2e > "$OUT/pmc_$C.log" 2>&1
   echo "pmc $C done"
 done
-STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | sort | sed -n 1p)
-FC=$(find "$OUT/pmc_FETCH_SIZE" -name '*counter_collection.csv' | sort | sed -n 1p)
-WC=$(find "$OUT/pmc_WRITE_SIZE" -name '*counter_collection.csv' | sort | sed -n 1p)
-python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$FC" "$WC" "$STATS" \
-  bulge_chase=bulge_lds_kernel band_update=syr2k_w_kernel band_xm=xm_kernel
-timeout -k 10 600 python3 bench.py > "$OUT/bench.log" 2>&1
-tail -1 "$OUT/bench.log"
+N=12288 ROWS=2 REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace12k" -o run -- \
+  python3 tools/solve_time.py > "$OUT/trace12k.log" 2>&1
+for C in FETCH_SIZE WRITE_SIZE; do
+  N=12288 ROWS=2 REPS=1 timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "$LRE" -f csv -d "$OUT/pmc12k_$C" -o run -- \
+    python3 tools/solve_time.py > "$OUT/pmc12k_$C.log" 2>&1
+  echo "pmc12k $C done"
+done
+first() { find "$1" -name "$2" | sort | sed -n 1p; }
+python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$(first $OUT/pmc_FETCH_SIZE '*counter_collection.csv')" \
+  "$(first $OUT/pmc_WRITE_SIZE '*counter_collection.csv')" "$(first $OUT/trace '*kernel_stats.csv')" \
+  bulge_chase=bulge_lds_kernel band_update=syr2k_w band_xm=xm_kernel
+python3 tools/pmc_traffic.py "$OUT/pmc_traffic_n12288.json" "$(first $OUT/pmc12k_FETCH_SIZE '*counter_collection.csv')" \
+  "$(first $OUT/pmc12k_WRITE_SIZE '*counter_collection.csv')" "$(first $OUT/trace12k '*kernel_stats.csv')" \
+  band_update=syr2k_w band_xm=xm_kernel pivot_schur=syrk_compact
+timeout -k 10 900 python3 bench.py > "$OUT/bench.log" 2>&1
+tail -c 3000 "$OUT/bench.log"
