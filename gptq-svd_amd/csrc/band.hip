@@ -709,6 +709,7 @@ struct XmArgs {
   const double *YT, *Y, *T;
   double *X, *part, *gpart, *M;
   unsigned *tick;
+  int asm_loads;  // K loop with the hand-written loads and waits (TG_XM_ASM, default 1)
 };
 // The product is formed transposed, Xᵀ[:, j-block] = YTᵀ · A22[:, j-block]
 // (A22 symmetric): the MFMA B operand is then 4 rows x 16 consecutive
@@ -738,6 +739,50 @@ __device__ __forceinline__ void xm_load(const XmArgs &g, const int (&col)[NBC], 
   for (int c = 0; c < NBC; ++c) f.b[c] = g.A[int64_t(k) * g.lda + col[c]];
   f.a[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
   f.a[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
+}
+// The same loads as inline asm, with the waits written out (TG_XM_ASM, the
+// default): with the compiler's loads the K loop's back edge carried DA
+// steps of pending loads and the compiler waited for ALL of them at the loop
+// header (s_waitcnt vmcnt(0) once per DA steps), so each wave had between 0
+// and DA steps in flight.  Here step u's slot waits only for its own loads
+// (vmcnt = the loads of the DA - 1 younger steps), so DA - 1 steps stay in
+// flight across the back edge.  The waits tie the slot's registers ("+v"), so
+// nothing that reads them is scheduled above the wait, and the loop exit
+// drains every slot before the registers are reused.
+__device__ __forceinline__ double xm_gload(const double *p) {
+  double v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+template <int NBC>
+__device__ __forceinline__ void xm_load_asm(const XmArgs &g, const int (&col)[NBC], int k0,
+                                            XmStep<NBC> &f) {
+  const int lane = threadIdx.x & 63;
+  const int k = min(k0 + (lane >> 4), g.m - 1);
+#pragma unroll
+  for (int c = 0; c < NBC; ++c) f.b[c] = xm_gload(g.A + int64_t(k) * g.lda + col[c]);
+  const double *yt = g.YT + int64_t(k) * SB_B + (lane & 15);
+  f.a[0] = xm_gload(yt);
+  f.a[1] = xm_gload(yt + 16);
+}
+// wait until step slot f's loads are in: the DA - 1 younger steps' loads
+// (NBC + 2 each) may stay outstanding
+template <int NBC, int DA>
+__device__ __forceinline__ void xm_wait_slot(XmStep<NBC> &f) {
+  static_assert((DA - 1) * (NBC + 2) == 20 || (DA - 1) * (NBC + 2) == 21, "xm wait count");
+  if constexpr (NBC == 2) {
+    asm volatile("s_waitcnt vmcnt(20)" : "+v"(f.b[0]), "+v"(f.b[1]), "+v"(f.a[0]), "+v"(f.a[1]));
+  } else {
+    asm volatile("s_waitcnt vmcnt(21)" : "+v"(f.b[0]), "+v"(f.a[0]), "+v"(f.a[1]));
+  }
+}
+template <int NBC>
+__device__ __forceinline__ void xm_drain_slot(XmStep<NBC> &f) {
+  if constexpr (NBC == 2) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.b[1]), "+v"(f.a[0]), "+v"(f.a[1]));
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.a[0]), "+v"(f.a[1]));
+  }
 }
 template <int NBC>
 __device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[NBC], int k0,
@@ -810,7 +855,23 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
   for (int c = 0; c < NBC; ++c)
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[c][i] = doublex4{0.0, 0.0, 0.0, 0.0};
-  if (kb < g.m) {
+  if (kb < g.m && g.asm_loads) {
+    const int nit = (g.m - kb + KS - 1) / KS;
+    XmStep<NBC> f[DA];
+#pragma unroll
+    for (int u = 0; u < DA; ++u) xm_load_asm<NBC>(g, colc, kb + KS * u, f[u]);
+    for (int it = 0; it < nit; it += DA) {
+#pragma unroll
+      for (int u = 0; u < DA; ++u) {
+        const int k0 = kb + KS * (it + u);
+        xm_wait_slot<NBC, DA>(f[u]);
+        xm_mma<NBC>(f[u], cok, k0, acc, g.m);
+        xm_load_asm<NBC>(g, colc, k0 + KS * DA, f[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DA; ++u) xm_drain_slot<NBC>(f[u]);
+  } else if (kb < g.m) {
     const int nit = (g.m - kb + KS - 1) / KS;
     XmStep<NBC> f[DA];
 #pragma unroll
@@ -1483,7 +1544,10 @@ static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const d
   const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
   const int nbc = fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
   const int G = cdiv(m, XR * nbc);
-  XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick};
+  const char *xs = getenv("TG_XM_ASM");  // development switch: 0 = compiler-scheduled loads
+  const int asm_loads = !(xs && xs[0] == '0');
+  XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick,
+            asm_loads};
   if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
   else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
   return hipGetLastError();

@@ -52,6 +52,8 @@ def rel(a, b):
     {"TG_SB_PAIR": "1"},
     {"TG_SYR2K_PERSIST": "0"},
     {"TG_BULGE_MULTI": "1"},
+    {"TG_XM_ASM": "0"},
+    {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
