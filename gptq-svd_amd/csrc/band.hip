@@ -1553,15 +1553,17 @@ static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const d
   return hipGetLastError();
 }
 
-// Panel pairs (see panel_upd_kernel) with TG_SB_PAIR=1 (read per call), for
-// panels whose partner has at least PAIR_MIN trailing rows; the workspace's
-// X holds n x ncmax*32 doubles, so two m x 32 slabs fit once n >= 2 SB_C.
-// Measured at n = 12,288 (rocprofv3): the merged rank-128
-// update saves 20 ms of the 62 ms of rank-64 updates, but the corrections'
-// cross-row reductions (pair_part 27 us + the one-workgroup pair_fin 66 us
-// per pair, latency-bound) cost as much; at n = 4096 the pairs are 2.7 ms
-// slower.  Off by default until the reductions ride on the X / M kernel's.
-constexpr int PAIR_MIN = 256;
+// Panel pairs (see panel_upd_kernel) for panels whose partner has at least
+// PAIR_MIN trailing rows (TG_SB_PAIR=1: every panel with a partner of >= 256
+// rows, 0: none; read per call); the workspace's X holds n x ncmax*32
+// doubles, so two m x 32 slabs fit once n >= 2 SB_C.  The merged rank-128
+// update streams the HBM-resident trailing matrix once per two panels; the
+// pair's correction products run on a side stream beside X_raw.  Measured
+// (tools/solve_time.py): n = 12,288 509.5 vs 521.8 ms, n = 28,672 3.18 vs
+// 3.47 s, but n = 4096 64.6 vs 61.4 ms (MALL-resident trailing matrices: the
+// corrections' reductions cost more than the pass they save), hence the
+// 6144-row default.
+constexpr int PAIR_MIN_ALL = 256, PAIR_MIN = 6144;
 
 // One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
 // (Measured and removed in round 3's clean-up, DESIGN.md §5: a look-ahead
@@ -1575,7 +1577,8 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   TG_CHK(hipMemsetAsync(b.xm_tick, 0, sizeof(unsigned) * xm_tick_words(n), st));
   const int np = int(pl.panels.size());
   const char *pe = getenv("TG_SB_PAIR");
-  const bool pairs = (pe && pe[0] == '1') && pl.ncmax >= 2;
+  const bool pairs = !(pe && pe[0] == '0') && pl.ncmax >= 2;
+  const int pair_min = (pe && pe[0] == '1') ? PAIR_MIN_ALL : PAIR_MIN;
   // TG_SYR2K_PERSIST=0: one tile per workgroup (development switch, per call)
   const char *ps = getenv("TG_SYR2K_PERSIST");
   const bool persist = !(ps && ps[0] == '0');
@@ -1595,7 +1598,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     // W = X - Y M / 2 in place
     hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
     TG_CHK(hipGetLastError());
-    const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= PAIR_MIN;
+    const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= pair_min;
     if (!pair) {  // A22 -= Y W^T + W Y^T
       const int nt = cdiv(m, WT), tiles = nt * (nt + 1) / 2;
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);

@@ -103,9 +103,10 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // compiler could break it: the vmcnt wait is an asm with a memory clobber
 // before the progress store, and the column loads are issued after the poll
 // returns (they depend on it through the wave barrier).
-// Past n = 8192 the workers of EVERY XCD take groups (bulge_multi_xcd; the
-// MX form of the kernel): band stores become write-through and the progress
-// store `sc1`, so the hand-off above holds across L2s.
+// With TG_BULGE_MULTI=1 the workers of EVERY XCD take groups (the MX form
+// of the kernel): band stores become write-through and the progress store
+// `sc1`, so the hand-off above holds across L2s (measured slower, kept as a
+// tested switch).
 // Workers take sweep groups from a queue in increasing order (dependencies
 // point only to lower groups, so any number of resident workers is safe).
 // Waits are bounded (spin.h): the first wait past the timeout sets the stall
@@ -733,13 +734,17 @@ namespace tg {
 
 int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 
-// Workers on every XCD once the sweep groups in flight outnumber one XCD's
-// CUs: a group trails its producer by 2 + LAG (G_SW - 1) steps and runs
-// ~n / b of them, so ~n / (b (2 + LAG (G_SW - 1))) groups overlap (32 at
-// n = 4096, 96 at 12,288).  TG_BULGE_MULTI=0 / 1 forces one XCD / all XCDs.
+// Workers on every XCD (TG_BULGE_MULTI=1, read per call; default one XCD).
+// The sweep groups in flight outnumber one XCD's CUs past n ~ 4096 (a group
+// trails its producer by 2 + LAG (G_SW - 1) steps and runs ~n / b of them:
+// ~96 overlap at n = 12,288), but with the band handed across L2s every
+// step's write-back and load go to memory and the chain slows more than the
+// extra CUs give back: 112 vs 83 ms at n = 12,288, 449 vs 378 ms at 28,672
+// (tools/solve_time.py, TG_BULGE_STATS=1), 22.0 ms either way at 4096.
 bool bulge_multi_xcd(int n) {
-  if (const char *v = getenv("TG_BULGE_MULTI")) return atoi(v) != 0;
-  return n >= 8192;
+  (void)n;
+  const char *v = getenv("TG_BULGE_MULTI");
+  return v && atoi(v) != 0;
 }
 
 // progress word per sweep group + control words + 64 dummy words

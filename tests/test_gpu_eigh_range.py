@@ -108,8 +108,8 @@ def test_orthogonality_n4096(kind, first, count):
 
 @pytest.mark.parametrize("n", [2048, 9000])
 def test_bulge_every_xcd_matches_one_xcd(n, monkeypatch):
-    """The band -> tridiagonal chase with workers on every XCD (the default
-    past n = 8192, TG_BULGE_MULTI=1 below it) hands band columns across L2s:
+    """The band -> tridiagonal chase with workers on every XCD
+    (TG_BULGE_MULTI=1) hands band columns across L2s:
     its eigenvalues must equal the one-XCD chase's bit for bit, twice in a
     row (a stale column read would show as a difference), and satisfy
     trace / Frobenius identities of H to 1e-12."""
@@ -133,3 +133,31 @@ def test_bulge_every_xcd_matches_one_xcd(n, monkeypatch):
     assert abs(one.sum() - np.trace(Hh)) <= 1e-12 * abs(np.trace(Hh))
     fro = float((Hh * Hh).sum())
     assert abs(float((one * one).sum()) - fro) <= 1e-12 * fro
+
+
+def test_panel_pairs_large_n(monkeypatch):
+    """n = 9000: the default band reduction pairs the panels with >= 6144
+    trailing rows (merged rank-128 updates, corrections on a side stream);
+    its eigenvalues match the unpaired reduction's (TG_SB_PAIR=0) to
+    1e-12 ||H|| and repeat bit for bit."""
+    from gptq_svd_amd import _lib as lib
+    n = 9000
+    H = torch.from_numpy(_wishart(n, 4)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def values(pair):
+        if pair is None:
+            monkeypatch.delenv("TG_SB_PAIR", raising=False)
+        else:
+            monkeypatch.setenv("TG_SB_PAIR", pair)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        torch.cuda.synchronize()
+        return w.cpu().numpy()
+
+    paired, plain = values(None), values("0")
+    assert np.array_equal(values(None), paired)
+    nrm = np.abs(plain).max()
+    assert np.abs(paired - plain).max() <= 1e-12 * nrm
