@@ -94,8 +94,10 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   take(b.R[1], w * SB_B);
   take(b.Gr, w * n);
   // X partials: one m x 32 slab per 256-row block of A22 (TSQR path); the
-  // single path's X / M partials (n / 16 + n / 256 blocks of 1024) fit too
-  take(b.U, std::max(w * n, (size_t(n) / 16 + size_t(n) / 256 + 2) * 1024));
+  // single path's X / M partials (n / 16 + n / 256 blocks of 1024; with the
+  // panel-pair products n / 32 + n / 1024 blocks of 5 x 1024) fit too
+  take(b.U, std::max({w * n, (size_t(n) / 16 + size_t(n) / 256 + 2) * 1024,
+                      (size_t(n) / 32 + size_t(n) / 1024 + 2) * 5 * 1024}));
   take(b.Xs, w * w);
   take(b.Zg, w * kmax);
   take(b.P, w * kmax);

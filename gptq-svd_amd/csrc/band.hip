@@ -710,7 +710,16 @@ struct XmArgs {
   double *X, *part, *gpart, *M;
   unsigned *tick;
   int asm_loads;  // K loop with the hand-written loads and waits (TG_XM_ASM, default 1)
+  // panel pairs (NBC = 2 only): panel a's deferred factors Ya = Y_a', Wa =
+  // W_a' (rows of this panel's A22, ld 32) -> the corrections' products
+  // P = Wa^T YT, Q = Ya^T YT, E1 = Y^T Ya, E2 = Y^T Wa ride on the block
+  // partials and the last arriver writes PQ = {P, Q, T^T (E1 P + E2 Q)}
+  // (what pair_part_kernel + pair_fin_kernel form otherwise); null: none
+  const double *Ya, *Wa;
+  double *PQ;
 };
+// doubles of one block's partials: Y^T X, + the four pair products
+__host__ __device__ inline int xm_np(const XmArgs &g) { return g.Ya ? 5 : 1; }
 // The product is formed transposed, Xᵀ[:, j-block] = YTᵀ · A22[:, j-block]
 // (A22 symmetric): the MFMA B operand is then 4 rows x 16 consecutive
 // columns of A22, so lane l reads A22[k + l/16][j0 + l%16] and every load
@@ -798,14 +807,15 @@ __device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[N
 }
 // sum over z in [z0, z1) of p[z * 1024 + e], in z order, with the L1-
 // bypassing loads of a batch all in flight before the first add
-__device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e) {
+__device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e,
+                                         int stride = 1024) {
   constexpr int NB = 8;
   double s = 0.0;
   for (int zb = z0; zb < z1; zb += NB) {
     double v[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u)
-      v[u] = tg::load_partial(&p[size_t(min(zb + u, z1 - 1)) * 1024 + e]);
+      v[u] = tg::load_partial(&p[size_t(min(zb + u, z1 - 1)) * stride + e]);
 #pragma unroll
     for (int u = 0; u < NB; ++u)
       if (zb + u < z1) s += v[u];
@@ -919,15 +929,45 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
     xs[rr][c] = xv[u];
     ys[rr][c] = yv[u];
   }
+  // panel pairs: the block's rows of Ya, Wa and YT in the next three slices
+  const bool pp = NBC == 2 && g.Ya != nullptr;  // uniform
+  const int NP = pp ? 5 : 1;
+  if constexpr (NBC == 2) {
+    if (pp) {
+#pragma unroll
+      for (int u = 0; u < YPT; ++u) {
+        const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31, row = r0 + rr;
+        const bool ok = row < g.m;
+        const int64_t o = int64_t(ok ? row : 0) * SB_B + c;
+        red[2][rr][c] = ok ? g.Ya[o] : 0.0;
+        red[3][rr][c] = ok ? g.Wa[o] : 0.0;
+        red[4][rr][c] = ok ? g.YT[o] : 0.0;
+      }
+    }
+  }
   __syncthreads();
-  // this block's Y_zᵀ X_z, write-through, then the group ticket
+  // this block's Y_zᵀ X_z (and the pair products), write-through, then the group ticket
+  double *mypart = g.part + size_t(blockIdx.x) * NP * 1024;
   for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
     const int a = e >> 5, c = e & 31;
     double p = 0.0;
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr) p = fma(ys[rr][a], xs[rr][c], p);
-    __hip_atomic_store(&g.part[size_t(blockIdx.x) * 1024 + e], p, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&mypart[e], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if constexpr (NBC == 2) {
+    if (pp) {
+      // k = 0: P = Wa^T YT, 1: Q = Ya^T YT, 2: E1 = Y^T Ya, 3: E2 = Y^T Wa
+      for (int e = tid; e < 4 * SB_B * SB_B; e += 64 * XW) {
+        const int k = e >> 10, a = (e >> 5) & 31, c = e & 31;
+        const double(*L)[SB_B + 1] = k == 0 ? red[3] : k == 1 ? red[2] : ys;
+        const double(*R)[SB_B + 1] = k <= 1 ? red[4] : k == 2 ? red[2] : red[3];
+        double p = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) p = fma(L[rr][a], R[rr][c], p);
+        __hip_atomic_store(&mypart[1024 + e], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -937,17 +977,22 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
              unsigned(z1 - z0 - 1);
   __syncthreads();
   if (!s_last) return;
-  double *Cs = &red[0][0][0], *Ts = Cs + SB_B * SB_B;
+  // Cs = C (Y^T X), then the pair sums P, Q, E1, E2 (pp); Ts = T
+  double *Cs = &red[0][0][0], *Ts = Cs + 5 * SB_B * SB_B;
   static_assert(XW * XR * (SB_B + 1) >= 2 * SB_B * SB_B, "C and T fit in red");
-  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
-    const double s = xm_sum(g.part, z0, z1, e);
+  static_assert(NBC == 1 || XW * XR * NBC * (SB_B + 1) >= 6 * SB_B * SB_B,
+                "C, the pair sums and T fit in red");
+  if (!pp) Ts = Cs + SB_B * SB_B;
+  const int ne = NP * SB_B * SB_B;
+  for (int e = tid; e < ne; e += 64 * XW) {
+    const double s = xm_sum(g.part, z0, z1, e, NP * 1024);
     if (NG == 1)
       Cs[e] = s;  // one group: its last arriver forms M (no second hand-off)
     else
-      __hip_atomic_store(&g.gpart[size_t(grp) * 1024 + e], s, __ATOMIC_RELAXED,
+      __hip_atomic_store(&g.gpart[size_t(grp) * NP * 1024 + e], s, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    Ts[e] = g.T[e];
   }
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW) Ts[e] = g.T[e];
   if (NG > 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -958,7 +1003,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
     }
     __syncthreads();
     if (!s_last) return;
-    for (int e = tid; e < SB_B * SB_B; e += 64 * XW) Cs[e] = xm_sum(g.gpart, 0, NG, e);
+    for (int e = tid; e < ne; e += 64 * XW) Cs[e] = xm_sum(g.gpart, 0, NG, e, NP * 1024);
   }
   __syncthreads();
   for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
@@ -966,6 +1011,29 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
     double v = 0.0;
     for (int k = 0; k <= a; ++k) v = fma(Ts[k * SB_B + a], Cs[k * SB_B + c], v);
     g.M[e] = v;
+  }
+  if (pp) {
+    // PQ[0 .. 2047] = {P, Q}; D = E1 P + E2 Q into C's slot (M is out);
+    // PQ[2048 ..] = T^T D
+    const double *Ps = Cs + 1024, *Qs = Cs + 2048, *E1 = Cs + 3072, *E2 = Cs + 4096;
+    for (int e = tid; e < 2048; e += 64 * XW) g.PQ[e] = Cs[1024 + e];
+    __syncthreads();
+    for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+      const int a = e >> 5, c = e & 31;
+      double v = 0.0;
+#pragma unroll 8
+      for (int k = 0; k < SB_B; ++k) v = fma(E1[a * SB_B + k], Ps[k * SB_B + c], v);
+#pragma unroll 8
+      for (int k = 0; k < SB_B; ++k) v = fma(E2[a * SB_B + k], Qs[k * SB_B + c], v);
+      Cs[e] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
+      const int a = e >> 5, c = e & 31;
+      double v = 0.0;
+      for (int k = 0; k <= a; ++k) v = fma(Ts[k * SB_B + a], Cs[k * SB_B + c], v);
+      g.PQ[2048 + e] = v;
+    }
   }
   if (tid == 0) {
     g.tick[grp] = 0u;
@@ -1539,15 +1607,22 @@ static hipError_t side_stream(SideStream *&out) {
 // CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
 // triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
 // X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
-static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const double *YT,
-                            const double *Yp, const double *Tp, double *X, const SbBufs &b) {
+static int xm_nbc(int m) {
   const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
-  const int nbc = fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
-  const int G = cdiv(m, XR * nbc);
+  return fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
+}
+// Ya / Wa (panel pairs, NBC = 2 only): also form the pair products into PQ
+static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const double *YT,
+                            const double *Yp, const double *Tp, double *X, const SbBufs &b,
+                            const double *Ya = nullptr, const double *Wa = nullptr,
+                            double *PQ = nullptr) {
+  const int nbc = xm_nbc(m);
+  if (Ya && nbc != 2) return hipErrorInvalidValue;
+  const int G = cdiv(m, XR * nbc), np = Ya ? 5 : 1;
   const char *xs = getenv("TG_XM_ASM");  // development switch: 0 = compiler-scheduled loads
   const int asm_loads = !(xs && xs[0] == '0');
-  XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * 1024, b.M, b.xm_tick,
-            asm_loads};
+  XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * np * 1024, b.M,
+            b.xm_tick, asm_loads, Ya, Wa, PQ};
   if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
   else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
   return hipGetLastError();
@@ -1585,7 +1660,10 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   const XcdInfo xi = xcd_info();
   const int ncu = std::max(1, xi.xcds * xi.cus_per_xcd);
   SideStream *ss = nullptr;
-  if (pairs) TG_CHK(side_stream(ss));
+  // TG_SB_PAIR_SIDE=1: the pair products by pair_part / pair_fin on a side
+  // stream even where the X / M kernel can form them (development switch)
+  const char *psd = getenv("TG_SB_PAIR_SIDE");
+  const bool pair_side = psd && psd[0] == '1';
   double *Xa = b.X, *Xb = b.X + size_t(n) * SB_B;
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
@@ -1624,19 +1702,25 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     const double *Ya = Yp + SB_B * SB_B, *Wa = Xa + SB_B * SB_B;  // panel a's rows >= Q.r0
     TG_CHK(panel_qr(st, A, lda, Q.p, Q.r0, Q.m, Yb, b.YT, Tb, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    // the corrections' products depend only on panel b's QR and panel a's
-    // Y / W: a side stream forms them while X_raw streams the matrix
-    const int nblk = cdiv(mb, PR);
-    TG_CHK(hipEventRecord(ss->ev0[0], st));
-    TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[0], 0));
-    hipLaunchKernelGGL(pair_part_kernel, dim3(nblk), dim3(256), 0, ss->s, Ya, Wa, Yb, b.YT, mb,
-                       b.Gr);
-    TG_CHK(hipGetLastError());
-    hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, ss->s, b.Gr, nblk, Tb, b.G);
-    TG_CHK(hipGetLastError());
-    TG_CHK(hipEventRecord(ss->ev1[0], ss->s));
-    TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
-    TG_CHK(hipStreamWaitEvent(st, ss->ev1[0], 0));
+    if (xm_nbc(mb) == 2 && !pair_side) {
+      // X_raw, M_raw and the corrections' products in one launch
+      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b, Ya, Wa, b.G));
+    } else {
+      // the corrections' products depend only on panel b's QR and panel a's
+      // Y / W: a side stream forms them while X_raw streams the matrix
+      const int nblk = cdiv(mb, PR);
+      if (!ss) TG_CHK(side_stream(ss));
+      TG_CHK(hipEventRecord(ss->ev0[0], st));
+      TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[0], 0));
+      hipLaunchKernelGGL(pair_part_kernel, dim3(nblk), dim3(256), 0, ss->s, Ya, Wa, Yb, b.YT, mb,
+                         b.Gr);
+      TG_CHK(hipGetLastError());
+      hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, ss->s, b.Gr, nblk, Tb, b.G);
+      TG_CHK(hipGetLastError());
+      TG_CHK(hipEventRecord(ss->ev1[0], ss->s));
+      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
+      TG_CHK(hipStreamWaitEvent(st, ss->ev1[0], 0));
+    }
     hipLaunchKernelGGL(w_update2_kernel, dim3(cdiv(mb, WU_R)), dim3(256), 0, st, Yb, Xb, mb, b.M,
                        Ya, Wa, b.G);
     TG_CHK(hipGetLastError());

@@ -51,6 +51,8 @@ def rel(a, b):
     {"TG_GEMM_SWZ": "0", "TG_GEMM_TILE": "128"},
     {"TG_SB_PAIR": "1"},
     {"TG_SB_PAIR": "0"},
+    {"TG_SB_PAIR": "1", "TG_XM_NBC": "2"},
+    {"TG_SB_PAIR": "1", "TG_XM_NBC": "2", "TG_SB_PAIR_SIDE": "1"},
     {"TG_SYR2K_PERSIST": "0"},
     {"TG_BULGE_MULTI": "1"},
     {"TG_XM_ASM": "0"},
