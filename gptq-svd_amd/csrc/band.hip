@@ -1187,7 +1187,7 @@ __global__ __launch_bounds__(256, 2) void syr2k_w_kernel(double *__restrict__ A,
   }
 }
 
-// Persistent form of syr2k_w_kernel<1> (the default): two workgroups per CU
+// Persistent form of syr2k_w_kernel<NP> (the default): two workgroups per CU
 // loop over the lower tiles; while a tile's operands are staged, multiplied
 // and written back, the NEXT tile's old values are already loading (issued
 // after this tile's operand loads, so waiting for those leaves them in
@@ -1201,10 +1201,9 @@ __device__ __forceinline__ void syr2k_tile(int b, int &tm, int &tn) {
   tm = I * WT;
   tn = (b - I * (I + 1) / 2) * WT;
 }
+template <int NP>
 __global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A, int64_t lda,
-                                                          int m, const double *__restrict__ Y,
-                                                          const double *__restrict__ W,
-                                                          int ntiles) {
+                                                          int m, YW2 yw, int ntiles) {
   __shared__ double Aop[WK][WT + WP];
   __shared__ double Bop[WK][WT + WP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1230,53 +1229,60 @@ __global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A
   for (; b < ntiles; b += gridDim.x) {
     int tm, tn;
     syr2k_tile(b, tm, tn);
-    __syncthreads();  // the previous tile's mirror reads of Aop are done
     const int rl = tid >> 2, k0 = (tid & 3) * 8;
     const int gr = min(tm + rl, m - 1), gc = min(tn + rl, m - 1);
     const bool okr = tm + rl < m, okc = tn + rl < m;
-    double2 v[4][4];
-    {
-      const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
-                              W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
-#pragma unroll
-      for (int o = 0; o < 4; ++o)
-#pragma unroll
-        for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int bn = b + int(gridDim.x);
-    if (bn < ntiles) load_old(bn, nold);  // in flight through this tile
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int k = k0 + 2 * h;
-      Aop[k][rl] = okr ? v[0][h].x : 0.0;
-      Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
-      Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
-      Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
-      Bop[k][rl] = okc ? v[2][h].x : 0.0;
-      Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
-      Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
-      Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
-    }
-    __syncthreads();
     doublex4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int kq = 0; kq < WK; kq += 4) {
-      double af[2], bf[2];
+    for (int pp = 0; pp < NP; ++pp) {
+      // the previous tile's mirror reads / the previous pair's MFMA reads of Aop are done
+      __syncthreads();
+      const double *Y = yw.Y[pp], *W = yw.W[pp];
+      double2 v[4][4];
+      {
+        const double *src[4] = {Y + int64_t(gr) * SB_B + k0, W + int64_t(gr) * SB_B + k0,
+                                W + int64_t(gc) * SB_B + k0, Y + int64_t(gc) * SB_B + k0};
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+        for (int o = 0; o < 4; ++o)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+          for (int h = 0; h < 4; ++h) v[o][h] = reinterpret_cast<const double2 *>(src[o])[h];
+      }
+      if (pp == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int bn = b + int(gridDim.x);
+        if (bn < ntiles) load_old(bn, nold);  // in flight through this tile
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int h = 0; h < 4; ++h) {
+        const int k = k0 + 2 * h;
+        Aop[k][rl] = okr ? v[0][h].x : 0.0;
+        Aop[k + 1][rl] = okr ? v[0][h].y : 0.0;
+        Aop[SB_B + k][rl] = okr ? v[1][h].x : 0.0;
+        Aop[SB_B + k + 1][rl] = okr ? v[1][h].y : 0.0;
+        Bop[k][rl] = okc ? v[2][h].x : 0.0;
+        Bop[k + 1][rl] = okc ? v[2][h].y : 0.0;
+        Bop[SB_B + k][rl] = okc ? v[3][h].x : 0.0;
+        Bop[SB_B + k + 1][rl] = okc ? v[3][h].y : 0.0;
+      }
+      __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+      for (int kq = 0; kq < WK; kq += 4) {
+        double af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = Aop[kq + (lane >> 4)][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = Bop[kq + (lane >> 4)][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();  // operand images dead: Aop becomes the mirror tile
     double(*Tt)[WT + 1] = reinterpret_cast<double(*)[WT + 1]>(&Aop[0][0]);
@@ -1681,8 +1687,8 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
       const int nt = cdiv(m, WT), tiles = nt * (nt + 1) / 2;
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
       if (persist)
-        hipLaunchKernelGGL(syr2k_wp_kernel, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st, A22,
-                           int64_t(lda), m, Yp, Xa, tiles);
+        hipLaunchKernelGGL(syr2k_wp_kernel<1>, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st,
+                           A22, int64_t(lda), m, YW2{{Yp, nullptr}, {Xa, nullptr}}, tiles);
       else
         hipLaunchKernelGGL(syr2k_w_kernel<1>, dim3(tiles), dim3(256), 0, st, A22, int64_t(lda), m,
                            YW2{{Yp, nullptr}, {Xa, nullptr}});
@@ -1726,8 +1732,13 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     TG_CHK(hipGetLastError());
     const int nt = cdiv(mb, WT);
     auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(mb) * mb, 128.0 * double(mb) * mb);
-    hipLaunchKernelGGL(syr2k_w_kernel<2>, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, A22b,
-                       int64_t(lda), mb, YW2{{Ya, Yb}, {Wa, Xb}});
+    const int tiles = nt * (nt + 1) / 2;
+    if (persist)
+      hipLaunchKernelGGL(syr2k_wp_kernel<2>, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st,
+                         A22b, int64_t(lda), mb, YW2{{Ya, Yb}, {Wa, Xb}}, tiles);
+    else
+      hipLaunchKernelGGL(syr2k_w_kernel<2>, dim3(tiles), dim3(256), 0, st, A22b, int64_t(lda), mb,
+                         YW2{{Ya, Yb}, {Wa, Xb}});
     prof_end(st, tok);
     TG_CHK(hipGetLastError());
   }
