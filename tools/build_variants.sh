@@ -25,7 +25,7 @@ i=0
 for V in "$@"; do
   TAG=v$i
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$PK/variants/lib_${UNIT}_$TAG.so" \
-    $OTHERS "$PK/build/var/${UNIT}_$TAG.o" -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
+    $OTHERS "$PK/build/var/${UNIT}_$TAG.o"
   echo "$PK/variants/lib_${UNIT}_$TAG.so: $V"
   i=$((i+1))
 done
