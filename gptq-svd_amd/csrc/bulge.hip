@@ -447,6 +447,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
                                                        unsigned long long timeout) {
 #if TG_BULGE_STATS
   uint64_t sw = 0, stk = 0, sbar = 0, nsteps = 0;
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ double R[RING][LDB];
   __shared__ WaveScratch wsc[NCW];
@@ -703,6 +704,9 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
     atomicAdd(stats + 2, (unsigned long long)stk);
     atomicAdd(stats + 3, (unsigned long long)sbar);
     atomicAdd(stats + 6, (unsigned long long)nsteps);
+    // shader clock over the launch: s_memtime cycles per 100 MHz tick
+    atomicAdd(stats + 4, (unsigned long long)(__builtin_amdgcn_s_memtime() - clk0));
+    atomicAdd(stats + 5, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rt0));
   }
 #endif
 }
@@ -840,6 +844,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
         fprintf(stderr,
                 "  workers %.0f, steps/worker %.0f; per step (us): wait %.2f task %.2f bar %.2f\n",
                 W, S / W, h[1] / 100.0 / S, h[2] / 100.0 / S, h[3] / 100.0 / S);
+        if (h[5]) fprintf(stderr, "  shader clock %.2f GHz\n", 0.1 * double(h[4]) / double(h[5]));
         fprintf(stderr, "  per-wave busy per step (us):");
         for (int w = 0; w < NCW + 2; ++w) fprintf(stderr, " w%d %.2f", w, h[8 + w] / 100.0 / S);
         fprintf(stderr, "\n");

@@ -1607,9 +1607,11 @@ __global__ __launch_bounds__(256) void trinv_diag_kernel(const double *__restric
 // go out as two batched GEMMs, which skip the zero triangles of Y11 and Y22
 // (half their flops); a pair whose second block is the ragged tail gets two
 // plain GEMMs.  T holds >= n*n/4 doubles.
+// bmax: stop before merging blocks of bmax rows (the diagonal bmax x bmax
+// blocks of Y are then the inverses of U's, the rest untouched).
 hipError_t trinv_offdiag(hipStream_t st, const double *U, int ldu, double *Y, int ldy, int n,
-                         double *T) {
-  for (int b = NU; b < n; b *= 2) {
+                         double *T, int bmax = 1 << 30) {
+  for (int b = NU; b < n && b < bmax; b *= 2) {
     const int nblk = tg::cdiv(n, b), npair = nblk / 2;
     const bool ragged = npair > 0 && 2 * npair * b > n;
     const int nfull = ragged ? npair - 1 : npair;
@@ -2192,6 +2194,36 @@ extern "C" size_t tg_ufactor_rx_workspace_size(int n, int k) {
   return s.off + 256;
 }
 
+// C = R11^-1 B for the upper-triangular R11 (k x k, ld ldr; its strict lower
+// triangle zero) and B (k x m, ld ldr): back substitution by TB-row blocks
+// from the bottom, block i = Dinv_i (Cw_i) then Cw[0:p] -= R11[0:p, i] C_i;
+// Dinv (ld ldd) holds the inverses of the TB x TB diagonal blocks.
+// Cw: k x m scratch (ld m); C: k x m (ld m).  k^2 m flops against the
+// explicit R11^-1's k^3 / 3 (the near-full-rank layers' m = n - k is tiny).
+constexpr int TB = 256;
+static int trsm_upper_blocks(hipStream_t st, const double *R, int ldr, int k, const double *B,
+                             int m, const double *Dinv, int ldd, double *Cw, double *C) {
+  TG_HIP(hipMemcpy2DAsync(Cw, sizeof(double) * m, B, sizeof(double) * ldr, sizeof(double) * m, k,
+                          hipMemcpyDeviceToDevice, st));
+  for (int bi = tg::cdiv(k, TB) - 1; bi >= 0; --bi) {
+    const int p = bi * TB, pb = std::min(TB, k - p);
+    TG_HIP(tg::dgemm(st, false, false, pb, m, pb, 1.0, Dinv + size_t(p) * ldd + p, ldd,
+                     Cw + size_t(p) * m, m, 0.0, C + size_t(p) * m, m));
+    if (p > 0)
+      TG_HIP(tg::dgemm(st, false, false, p, m, pb, -1.0, R + p, ldr, C + size_t(p) * m, m, 1.0, Cw,
+                       m));
+  }
+  return 0;
+}
+
+// The small-m form of the U factor (below): m * 16 <= k by default;
+// TG_URX_SMALLM=0 / 1 forces the explicit-inverse form / this one.
+static bool urx_small_m(int k, int m) {
+  const char *e = getenv("TG_URX_SMALLM");
+  if (e) return e[0] == '1';
+  return int64_t(m) * 16 <= int64_t(k);
+}
+
 extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U,
                               int ldu, void *ws, size_t ws_bytes) {
   TG_ARG(Rx, 2, "null Rx");
@@ -2213,18 +2245,42 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
     const int m = n - k;
     const dim3 gk(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k);
     double *Yr = Y, *C = Bm, *ZT = S, *Nm = A;  // C: k x m (ld m)
+    const bool small_m = urx_small_m(k, m);
     TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
     hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, Rx, ldr, k, Yr,
                        k);
     TG_LAUNCHED();
-    TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));                 // Yr = R11^-1
-    TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr, sizeof(double) * k,
-                            k, hipMemcpyDeviceToDevice, st));         // Z^T = R11 (+ ...)
-    if (m > 0) {
-      TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
-      TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));  // + R12 C^T
+    auto form_zt = [&]() -> int {  // Z^T = R11 + R12 C^T
+      TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr,
+                              sizeof(double) * k, k, hipMemcpyDeviceToDevice, st));
+      if (m > 0)
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));
+      return 0;
+    };
+    if (small_m) {
+      // C = R11^-1 R12 by block back substitution (no explicit inverse), and
+      // N = Z Z^T = (R11 + R12 C^T)^T (R11 + R12 C^T) as
+      //   R11^T R11 + V C^T + C V^T,  V = R11^T R12 + C (R12^T R12) / 2,
+      // the first term a triangular SYRK (a third of the square's flops)
+      if (m > 0) {
+        TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));          // 256-block inverses
+        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C)) return e;
+        double *V = ZT, *G = Rq;  // k x m and m x m (ld m)
+        TG_HIP(tg::dgemm(st, true, false, k, m, k, 1.0, Rx, ldr, Rx + k, ldr, 0.0, V, m));
+        TG_HIP(tg::dgemm(st, true, false, m, m, k, 1.0, Rx + k, ldr, Rx + k, ldr, 0.0, G, m));
+        TG_HIP(tg::dgemm(st, false, false, k, m, m, 0.5, C, m, G, m, 1.0, V, m));
+      }
+      TG_HIP(tg::dsyrk_tn_upper(st, k, 1.0, Rx, ldr, 0.0, Nm, k));     // R11^T R11
+      if (m > 0) {
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, ZT, m, C, m, 1.0, Nm, k));  // + V C^T
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, C, m, ZT, m, 1.0, Nm, k));  // + C V^T
+      }
+    } else {
+      TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));               // Yr = R11^-1
+      if (m > 0) TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
+      if (const int e = form_zt()) return e;
+      TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
     }
-    TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));           // N = Z Z^T
     hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, Rq);  // N' = J N J
     TG_LAUNCHED();
     TG_HIP(chol_upper_rows(st, Rq, k, k, k, Wb, info));               // N' = R^T R
@@ -2236,6 +2292,9 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
       // R is the R factor of Yq = J Z^T J (Yq^T Yq = N'): CholeskyQR passes on Yq
       double *Yq = Nm;
       TG_HIP(zero_lower(st, Rq, k, k));
+      if (small_m) {  // ZT held V
+        if (const int e = form_zt()) return e;
+      }
       hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, ZT, k, Yq);
       TG_LAUNCHED();
       const int e = refine_factor(st, Yq, k, k, Rq, rw, Wb, info, h);

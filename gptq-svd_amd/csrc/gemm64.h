@@ -27,6 +27,9 @@ hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, d
 // Symmetric rank-K updates (lower tiles computed, mirrored to the upper triangle).
 hipError_t dsyrk_tn(hipStream_t st, int n, int K, double alpha, const double *X, int64_t ldx,
                     double beta, double *C, int64_t ldc);  // C = a X^T X + b C, X: K x n
+// C = a X^T X + b C for an upper-triangular X (n x n, strict lower triangle zero)
+hipError_t dsyrk_tn_upper(hipStream_t st, int n, double alpha, const double *X, int64_t ldx,
+                          double beta, double *C, int64_t ldc);
 hipError_t dsyrk_tn_lower(hipStream_t st, int n, int K, double alpha, const double *X,
                           int64_t ldx, double beta, double *C,
                           int64_t ldc);  // lower tiles of C only, no mirror

@@ -342,12 +342,15 @@ __global__ __launch_bounds__(G8_NT, 4) void dgemm8_kernel(int M, int N, int K, d
   __shared__ __attribute__((aligned(16))) double Bs[2][G8_KC][G8_P];
   int tm, tn;
   if (SYRK) {
-    const int b = blockIdx.x;
+    // swz = 1 in SYRK mode: op(A) = X^T with X upper triangular (K x M), so
+    // the lower tile (tm, tn) only sums k < tn + 128; heaviest tiles first
+    const int b = swz ? int(gridDim.x) - 1 - int(blockIdx.x) : int(blockIdx.x);
     int I = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
     while ((I + 1) * (I + 2) / 2 <= b) ++I;
     while (I * (I + 1) / 2 > b) --I;
     tm = I * G8_T;
     tn = (b - I * (I + 1) / 2) * G8_T;
+    if (swz) K = min(K, tn + G8_T);
   } else if (swz) {
     const int tmn = tg::cdiv(M, G8_T), tnn = tg::cdiv(N, G8_T), nb = tmn * tnn;
     const int per = tg::cdiv(nb, 8);
@@ -668,6 +671,20 @@ hipError_t sum_partials(hipStream_t st, const double *P, int nz, int M, int N, d
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, P, nz, zs, M, N, alpha,
                      beta, C, ldc);
   return hipGetLastError();
+}
+
+// C = alpha * X^T X + beta * C for an UPPER TRIANGULAR X (n x n, ld ldx;
+// its strict lower triangle must hold zeros): lower tiles, mirrored, each
+// summing only the rows above its column block (a third of the flops).
+hipError_t dsyrk_tn_upper(hipStream_t st, int n, double alpha, const double *X, int64_t ldx,
+                          double beta, double *C, int64_t ldc) {
+  if (n <= 0) return hipSuccess;
+  const int n128 = cdiv(n, 128);
+  if (gemm_impl() != 2 || C == X) return dsyrk_tn(st, n, n, alpha, X, ldx, beta, C, ldc);
+  const dim3 grid(n128 * (n128 + 1) / 2);
+  const bool v = vec_ok(X, ldx);
+  return launch8_v<true, false, true>(st, grid, v, v, n, n, n, alpha, X, ldx, X, ldx, beta, C,
+                                      ldc, 1);
 }
 
 // C = alpha * X^T X + beta * C on lower tiles, mirrored (X is K x n, ld ldx).

@@ -59,6 +59,7 @@ def rel(a, b):
     {"TG_XM_ASM": "0"},
     {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
+    {"TG_URX_SMALLM": "1"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
     {"TG_ORTH_MGS": "1"},
@@ -77,3 +78,27 @@ def test_switch_matches_default(problem, path, switches, monkeypatch):
     assert rel(got["R_x"], ref["R_x"]) <= 1e-10
     mism = float(np.mean(got["Wq"] != ref["Wq"]))
     assert mism <= 1e-5, mism  # U agrees to ~1e-15: at most a rounding-tie flip
+
+
+def test_small_m_u_factor_near_full_rank(monkeypatch):
+    """A near-full-rank H (rows 2n, the real layers' case: k = n - m with m
+    tiny) takes the small-m U factor by default (C = R11^-1 R12 by block back
+    substitution, N = R11^T R11 by a triangular SYRK + a rank-2m term); U
+    matches the explicit-inverse form (TG_URX_SMALLM=0) to 1e-10, perm and R_x
+    identical."""
+    import gptq_svd_amd.gptq_utils as g
+    torch.manual_seed(7)
+    n = 2048
+    acc = g.HessianAccumulator(n, DEV)
+    acc.add_batch(torch.randn(2 * n, n).half().to(DEV))
+    H = acc.get_hessian()
+    W = torch.randn(128, n, device=DEV)
+    monkeypatch.setenv("TG_SPECTRAL_PATH", "complement")
+    got = solve(g, H, W)
+    k = got["R_x"].shape[0]
+    assert (n - k) * 16 <= k, k
+    monkeypatch.setenv("TG_URX_SMALLM", "0")
+    ref = solve(g, H, W)
+    assert np.array_equal(got["perm"], ref["perm"])
+    assert rel(got["R_x"], ref["R_x"]) == 0.0
+    assert rel(got["U"], ref["U"]) <= 1e-10
