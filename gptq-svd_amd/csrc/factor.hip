@@ -576,6 +576,13 @@ __device__ inline unsigned long long dkey(double d) {
   return d > 0.0 ? static_cast<unsigned long long>(__double_as_longlong(d)) : 0ull;
 }
 
+// The compacted H_k buffers keep only their lower triangle (the Schur update
+// writes no mirror): entry (a, b) is read at (max, min).  The first panel's
+// H_k is the full matrix, for which that is the same entry.
+__device__ __forceinline__ size_t hk_at(int a, int b, int n) {
+  return size_t(max(a, b)) * n + min(a, b);
+}
+
 constexpr int STH = 512;        // threads of piv_sel_kernel (8 waves)
 constexpr int CPT = SEL / STH;  // candidates per thread
 
@@ -947,7 +954,7 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
     double hv[CPT];
 #pragma unroll
     for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
-      hv[u] = Hc[size_t(opiv) * n + oc[u]];  // unconditional; masked below
+      hv[u] = Hc[hk_at(opiv, oc[u], n)];  // unconditional; masked below
 #pragma unroll
     for (int u = 0; u < CPT; ++u)
       if (rc[u] == piv) {
@@ -1046,7 +1053,7 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
   const int r = w.perm[xc], oi = w.oidx[xc - ps];
   double hv[PB];
 #pragma unroll
-  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? Hc[size_t(poi[i]) * n + oi] : 0.0;
+  for (int i = 0; i < PB; ++i) hv[i] = i < tn ? Hc[hk_at(poi[i], oi, n)] : 0.0;
   double d = w.dsc[r];
   double lr[PB];
   bool done = false;
@@ -1087,12 +1094,16 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 // Next panel's compacted H_k: Hn[i][j] = Hc[oidx[tn + i]][oidx[tn + j]]
-// - sum_l LT[l][i] LT[l][j] for i, j < n - ps2 (ps2 = steps done after the
-// panel, tn its steps), 64 x 64 lower tiles mirrored through LDS.  The grid
-// covers the whole n x n lower triangle; tiles past the block exit.
+// - sum_l LT[l][i] LT[l][j] for n - ps2 > i >= j (ps2 = steps done after the
+// panel, tn its steps) on 64 x 64 lower tiles: the lower triangle only (8
+// bytes per entry of the block read and written instead of 12 with the
+// mirror; every reader takes (max, min), hk_at).  The entries are the values
+// the mirrored form wrote, bit for bit (a diagonal tile's (a, b) and (b, a)
+// are the same products summed in the same order).  The grid covers the
+// whole n x n lower triangle; tiles past the block exit.
 __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
                                                            const double *__restrict__ Hc,
-                                                           double *__restrict__ Hn) {
+                                                           double *__restrict__ Hn, int mirror) {
   __shared__ double li[PB][64], lj[PB][64];
   __shared__ double tt[64][65];
   __shared__ int orow[64], ocol[64];
@@ -1128,7 +1139,7 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        acc[ib][jb][q] = Hc[size_t(orow[wm * 32 + ib * 16 + lk + 4 * q]) * n + ocol[wn * 32 + jb * 16 + lr]];
+        acc[ib][jb][q] = Hc[hk_at(orow[wm * 32 + ib * 16 + lk + 4 * q], ocol[wn * 32 + jb * 16 + lr], n)];
 #pragma unroll
   for (int kq = 0; kq < PB; kq += 4) {
     double af[2], bf[2];
@@ -1150,10 +1161,10 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
       for (int q = 0; q < 4; ++q) {
         const int rl = wm * 32 + ib * 16 + lk + 4 * q, cl = wn * 32 + jb * 16 + lr;
         const int gi = i0 + rl, gj = j0 + cl;
-        if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
+        if (gi < nc && gj < nc && (mirror || gi >= gj)) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
         tt[cl][rl] = acc[ib][jb][q];
       }
-  if (I == J) return;  // uniform
+  if (I == J || !mirror) return;  // uniform
   __syncthreads();
   // mirror: rows j0 .. j0 + 63 of the block, columns i0 .. i0 + 63, row-contiguous
   for (int e = tid; e < 64 * 64; e += 256) {
@@ -1171,7 +1182,8 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
 // epilogue and dispatch.  Same arithmetic per entry as syrk_compact_kernel.
 __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
                                                                 const double *__restrict__ Hc,
-                                                                double *__restrict__ Hn) {
+                                                                double *__restrict__ Hn,
+                                                                int mirror) {
   __shared__ double li[PB][64], lj[PB][64];
   __shared__ double tt[64][65];
   const int tid = threadIdx.x;
@@ -1206,7 +1218,7 @@ __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[ib][jb][q] = Hc[size_t(ro[ib][q]) * n + co[jb]];
+        for (int q = 0; q < 4; ++q) o[ib][jb][q] = Hc[hk_at(ro[ib][q], co[jb], n)];
   };
   int b = blockIdx.x;
   if (b >= tiles) return;
@@ -1267,10 +1279,10 @@ __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
         for (int q = 0; q < 4; ++q) {
           const int rl = wm * 32 + ib * 16 + lk + 4 * q, cl = wn * 32 + jb * 16 + lr;
           const int gi = i0 + rl, gj = j0 + cl;
-          if (gi < nc && gj < nc) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
+          if (gi < nc && gj < nc && (mirror || gi >= gj)) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
           tt[cl][rl] = acc[ib][jb][q];
         }
-    if (i0 != j0) {  // uniform: mirror rows j0 .. j0 + 63, columns i0 .. i0 + 63
+    if (i0 != j0 && mirror) {  // uniform: mirror rows j0 .. j0 + 63, columns i0 .. i0 + 63
       __syncthreads();
       for (int e = tid; e < 64 * 64; e += 256) {
         const int rr = e >> 6, cc = e & 63;
@@ -1872,6 +1884,10 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   // TG_SYR2K_PERSIST=0: one tile per workgroup (development switch, per call)
   const char *ps = getenv("TG_SYR2K_PERSIST");
   const bool persist = !(ps && ps[0] == '0');
+  // TG_SCHUR_MIRROR=1: the Schur updates also write the upper triangle
+  // (development switch; the readers take (max, min) either way)
+  const char *sm = getenv("TG_SCHUR_MIRROR");
+  const int mirror = (sm && sm[0] == '1') ? 1 : 0;
   const tg::XcdInfo xi = tg::xcd_info();
   const int ncu = std::max(1, xi.xcds * xi.cus_per_xcd);
   // compacted Schur complements alternate between the two buffers
@@ -1881,9 +1897,10 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
     const int nt = tg::cdiv(rows, 64);
     if (persist)
       hipLaunchKernelGGL(syrk_compact_p_kernel, dim3(std::min(nt * (nt + 1) / 2, 2 * ncu)),
-                         dim3(256), 0, st, n, w, hc, hn);
+                         dim3(256), 0, st, n, w, hc, hn, mirror);
     else
-      hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc, hn);
+      hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc,
+                         hn, mirror);
     const hipError_t e = hipGetLastError();
     double *t = const_cast<double *>(hc);
     hc = hn;
