@@ -103,10 +103,11 @@ __device__ inline int ntasks(int n, int j) { return (j <= n - 3) ? (n - 3 - j) /
 // compiler could break it: the vmcnt wait is an asm with a memory clobber
 // before the progress store, and the column loads are issued after the poll
 // returns (they depend on it through the wave barrier).
-// With TG_BULGE_MULTI=1 the workers of EVERY XCD take groups (the MX form
-// of the kernel): band stores become write-through and the progress store
-// `sc1`, so the hand-off above holds across L2s (measured slower, kept as a
-// tested switch).
+// (A form with the workers of every XCD -- write-through band stores, `sc1`
+// progress words -- gave bit-identical eigenvalues but was slower: 112 vs
+// 83 ms at n = 12,288, 449 vs 378 ms at 28,672, every step's transfers going
+// to memory instead of the XCD's L2; its template also cost the one-XCD
+// kernel 1 ms at n = 4096 through a different schedule, so it was removed.)
 // Workers take sweep groups from a queue in increasing order (dependencies
 // point only to lower groups, so any number of resident workers is safe).
 // Waits are bounded (spin.h): the first wait past the timeout sets the stall
@@ -398,15 +399,12 @@ __device__ __forceinline__ unsigned *lane0_or_dummy(unsigned *real, unsigned *du
   return wlane == 0 ? real : dummy + wlane;
 }
 
-template <bool MX>
 __device__ __forceinline__ void publish(unsigned *p, unsigned v) {
 #if TG_BULGE_FLAG_L2
-  if constexpr (!MX) {
-    __hip_atomic_store((tg::spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
-  }
-#endif
+  __hip_atomic_store((tg::spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
   tg::ctl_store(p, v);
+#endif
 }
 
 #if TG_BULGE_STATS
@@ -431,14 +429,7 @@ __device__ __forceinline__ void publish(unsigned *p, unsigned v) {
 #define HB(ph)
 #endif
 
-// ctl[0] = chosen XCD + 1, ctl[1] = group queue, ctl[2] = stall word.
-// MX (every XCD's CUs work; large n, where one XCD's 32 CUs, not the chain of
-// hand-offs, bound the launch): the band crosses XCDs, so every store of it is
-// write-through (`sc1`: the line leaves the storing XCD's L2 and no L2 keeps
-// a stale copy), every storing wave drains (`vmcnt(0)`) before the progress
-// word is stored `sc1`, and every load of it is an `sc1` load after the poll
-// (MI355X_MICROARCH.md, visibility: the first row of the sc1 hand-off table).
-template <bool MX>
+// ctl[0] = chosen XCD + 1, ctl[1] = group queue, ctl[2] = stall word
 __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, int n,
                                                        double *__restrict__ V2, int smax,
                                                        unsigned *__restrict__ prog,
@@ -461,17 +452,13 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   unsigned *stall = ctl + 2;
   unsigned *dummy = ctl + 4;  // 64 words: the lanes 1-63 targets of lane-0 operations
   if (tid == 0) {
-    if constexpr (MX) {
-      sh_G = 0;
-    } else {
-      unsigned x;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-      unsigned expect = 0;
-      __hip_atomic_compare_exchange_strong(ctl, &expect, x + 1, __ATOMIC_RELAXED,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned chosen = expect == 0 ? x + 1 : expect;
-      sh_G = (chosen == x + 1) ? 0 : -1;
-    }
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned expect = 0;
+    __hip_atomic_compare_exchange_strong(ctl, &expect, x + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned chosen = expect == 0 ? x + 1 : expect;
+    sh_G = (chosen == x + 1) ? 0 : -1;
     sh_dead = 0;
     sh_wdone[0] = sh_wdone[1] = 0;
   }
@@ -482,7 +469,6 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
   const int bytes = n * LDB * int(sizeof(double));
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(B, 0, bytes, 0x00020000);
   constexpr int SC1 = 16;                 // cache policy bit of the L1-bypassing loads
-  constexpr int WST = MX ? SC1 : 0;       // band stores: write-through across XCDs
   constexpr int NTC = LDB / 2;            // 16-B chunks per column
   constexpr int PFN = SB_B * NTC / BT + 1;  // chunks per thread of a whole-workgroup load
   // halves of each step's write-back (NH) and load (NHL), 1 KB blocks by parity
@@ -577,14 +563,14 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
             const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
             const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                   (c * LDB + 2 * h) * 8, 0, WST);
+                                                   (c * LDB + 2 * h) * 8, 0, 0);
           }
         }
       };
       auto wb_finish = [&](int half) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (NH == 1) {
-          publish<MX>(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
+          publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
         } else {
           // each half marks its word, then reads the other's: LDS serves one
           // CU's requests in order, so the later of the two sees both marks
@@ -594,7 +580,7 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           const unsigned o = __hip_atomic_load(&sh_wdone[half ^ 1], __ATOMIC_SEQ_CST,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
           if (__builtin_amdgcn_readfirstlane(o) >= nstep + 1)
-            publish<MX>(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
+            publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(t));
         }
       };
       // the load as two parts (issue after the poll; LDS writes once the data is in)
@@ -689,13 +675,13 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
           const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
           const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                 (c * LDB + 2 * h) * 8, 0, WST);
+                                                 (c * LDB + 2 * h) * 8, 0, 0);
         }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (wid == 0) publish<MX>(lane0_or_dummy(prog + G, dummy, wlane), unsigned(total + 1));
+    if (wid == 0) publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(total + 1));
   }
 #if TG_BULGE_STATS
   if (stats && tid == 0) {
@@ -737,19 +723,6 @@ __global__ void extract_tri_kernel(const double *__restrict__ Bst, int n,
 namespace tg {
 
 int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
-
-// Workers on every XCD (TG_BULGE_MULTI=1, read per call; default one XCD).
-// The sweep groups in flight outnumber one XCD's CUs past n ~ 4096 (a group
-// trails its producer by 2 + LAG (G_SW - 1) steps and runs ~n / b of them:
-// ~96 overlap at n = 12,288), but with the band handed across L2s every
-// step's write-back and load go to memory and the chain slows more than the
-// extra CUs give back: 112 vs 83 ms at n = 12,288, 449 vs 378 ms at 28,672
-// (tools/solve_time.py, TG_BULGE_STATS=1), 22.0 ms either way at 4096.
-bool bulge_multi_xcd(int n) {
-  (void)n;
-  const char *v = getenv("TG_BULGE_MULTI");
-  return v && atoi(v) != 0;
-}
 
 // progress word per sweep group + control words + 64 dummy words
 size_t sb2st_prog_words(int n) { return size_t(cdiv(std::max(1, n - 2), G_SW)) + 4 + 64; }
@@ -800,12 +773,9 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     // one workgroup per CU (the ring fills the LDS): the elected XCD's share
     // of the grid is its CUs, the other XCDs' workgroups exit at once
     const XcdInfo xi = xcd_info();
-    if (bulge_multi_xcd(n))
-      hipLaunchKernelGGL(bulge_lds_kernel<true>, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st,
-                         Bst, n, V2, sb_smax(n), prog, ctl, stats, timeout);
-    else
-      hipLaunchKernelGGL(bulge_lds_kernel<false>, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st,
-                         Bst, n, V2, sb_smax(n), prog, ctl, stats, timeout);
+    hipLaunchKernelGGL(bulge_lds_kernel, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st, Bst, n,
+                       V2, sb_smax(n),
+                       prog, ctl, stats, timeout);
     tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;

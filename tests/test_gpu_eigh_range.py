@@ -106,35 +106,6 @@ def test_orthogonality_n4096(kind, first, count):
     assert orth <= 1e-9
 
 
-@pytest.mark.parametrize("n", [2048, 9000])
-def test_bulge_every_xcd_matches_one_xcd(n, monkeypatch):
-    """The band -> tridiagonal chase with workers on every XCD
-    (TG_BULGE_MULTI=1) hands band columns across L2s:
-    its eigenvalues must equal the one-XCD chase's bit for bit, twice in a
-    row (a stale column read would show as a difference), and satisfy
-    trace / Frobenius identities of H to 1e-12."""
-    from gptq_svd_amd import _lib as lib
-    H = torch.from_numpy(_wishart(n, 3)).to(DEV)
-    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
-
-    def values(multi):
-        monkeypatch.setenv("TG_BULGE_MULTI", multi)
-        A = H.clone()
-        w = torch.empty(n, dtype=torch.float64, device=DEV)
-        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
-                 ws.numel())
-        torch.cuda.synchronize()
-        return w.cpu().numpy()
-
-    one = values("0")
-    for _ in range(2):
-        assert np.array_equal(values("1"), one)
-    Hh = H.cpu().numpy()
-    assert abs(one.sum() - np.trace(Hh)) <= 1e-12 * abs(np.trace(Hh))
-    fro = float((Hh * Hh).sum())
-    assert abs(float((one * one).sum()) - fro) <= 1e-12 * fro
-
-
 def test_panel_pairs_large_n(monkeypatch):
     """n = 9000: the default band reduction pairs the panels with >= 6144
     trailing rows (merged rank-128 updates, corrections on a side stream);

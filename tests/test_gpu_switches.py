@@ -55,7 +55,6 @@ def rel(a, b):
     {"TG_SB_PAIR": "1", "TG_XM_NBC": "2", "TG_SB_PAIR_SIDE": "1"},
     {"TG_SYR2K_PERSIST": "0"},
     {"TG_SYR2K_PERSIST": "0", "TG_SB_PAIR": "1"},
-    {"TG_BULGE_MULTI": "1"},
     {"TG_XM_ASM": "0"},
     {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
