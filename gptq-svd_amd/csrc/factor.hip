@@ -1057,22 +1057,21 @@ __global__ __launch_bounds__(256) void piv_fill_kernel(int n, int k, PivWs w,
   double d = w.dsc[r];
   double lr[PB];
   bool done = false;
+  // branch-free (selects, no exec-mask regions around each step, so the
+  // broadcast LDS reads of row i of the pivots' L are not serialised behind
+  // per-step waits): an inactive step (past the panel's steps, or after this
+  // row was pivoted) keeps lr = 0 and d, and its fma terms with lr = 0 leave
+  // the later sums unchanged -- the same values as the branchy loop
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
-    lr[i] = 0.0;
-    if (i >= tn || done) continue;
-    if (prow[i] == r) {
-      lr[i] = lpp[i][i];
-      done = true;
-      continue;
-    }
     double v = hv[i];
 #pragma unroll
-    for (int l = 0; l < PB; ++l)
-      if (l < i) v = fma(-lr[l], lpp[i][l], v);
+    for (int l = 0; l < i; ++l) v = fma(-lr[l], lpp[i][l], v);
     const double lv = v * pinv[i];
-    lr[i] = lv;
-    d = fma(-lv, lv, d);
+    const bool act = (i < tn) & !done, isp = prow[i] == r;
+    lr[i] = act ? (isp ? lpp[i][i] : lv) : 0.0;
+    d = (act & !isp) ? fma(-lv, lv, d) : d;
+    done = done | (act & isp);
   }
   if (valid) w.dsc[r] = d;
 #pragma unroll

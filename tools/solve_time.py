@@ -16,8 +16,10 @@ rows = int(float(os.environ.get("ROWS", "0.75")) * n)  # calibration rows (x n)
 dev = torch.device("cuda")
 torch.manual_seed(1)
 acc = g.HessianAccumulator(n, dev)
+xf32 = os.environ.get("XF32") == "1"  # fp32 rows: the generic (not the 16-bit) SYRK
 for r0 in range(0, rows, 16384):
-    acc.add_batch(torch.randn(min(16384, rows - r0), n, device=dev).half())
+    x = torch.randn(min(16384, rows - r0), n, device=dev).half()
+    acc.add_batch(x.float() if xf32 else x)
 H = acc.get_hessian()
 del acc
 W = torch.randn(4096, n, device=dev)
