@@ -21,6 +21,16 @@ struct Arena {
     off += count * sizeof(T);
     return p;
   }
+  // absolute alignment (the buffer's address, not its offset): A - 1 bytes
+  // of slack per call in the Sizer's count
+  template <class T>
+  T *take_aligned(size_t count, size_t A) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    off = ((b + off + A - 1) & ~uintptr_t(A - 1)) - b;
+    T *p = reinterpret_cast<T *>(base + off);
+    off += count * sizeof(T);
+    return p;
+  }
   bool ok() const { return off <= cap; }
 };
 
@@ -31,6 +41,10 @@ struct Sizer {
   void take(size_t count) {
     off = (off + 255) & ~size_t(255);
     off += count * sizeof(T);
+  }
+  template <class T>
+  void take_aligned(size_t count, size_t A) {
+    off += A - 1 + count * sizeof(T);
   }
 };
 

@@ -79,11 +79,18 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
     if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take<T>(cnt);
     else ar.template take<T>(cnt);
   };
+  // the two compacted H_k buffers on 2 MB boundaries (their rows are
+  // gathered by the candidate steps and the fill kernel)
+  auto take2m = [&](double *&dst, size_t cnt) {
+    constexpr size_t AL = size_t(2) << 20;
+    if constexpr (std::is_same_v<A, tg::Arena>) dst = ar.template take_aligned<double>(cnt, AL);
+    else ar.template take_aligned<double>(cnt, AL);
+  };
   take(q.B, size_t(k) * n);
   take(q.pp, size_t(2) * PGMAX * PPS);
   take(q.bc, PPS);
   take(q.flag, 16);
-  take(q.Hk, size_t(n) * n);
+  take2m(q.Hk, size_t(n) * n);
   take(q.dsc, n);
   take(q.L, size_t(n) * k);
   take(q.LT, size_t(PB) * n);
@@ -95,7 +102,7 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.prow, PB);
   take(q.pinv, PB);
   take(q.Lpp, PB * PB);
-  take(q.Hk2, compact_pivot(n) ? size_t(n) * n : size_t(1));
+  take2m(q.Hk2, compact_pivot(n) ? size_t(n) * n : size_t(1));
   take(q.oidx, n);
 }
 
