@@ -640,7 +640,10 @@ __device__ inline void block_argmax_sel(double &v, int &p, int &r, int &o, doubl
   const bool hold = v == m;
   const unsigned long long b = __ballot(hold);
   int L = __ffsll(static_cast<long long>(b)) - 1;
-  if (__popcll(b) > 1) {  // tie on v: smallest position among the holders (uniform branch)
+  // tie on v: smallest position among the holders (uniform branch).  A wave
+  // whose candidates are all exhausted (every lane at -inf) skips it: its
+  // record cannot win unless every wave's is -inf, and then the panel ends
+  if (__popcll(b) > 1 && m != -INFINITY) {
     int pp = hold ? p : INT_MAX;
     pp = wave_min_stage<0>(pp);
     pp = wave_min_stage<1>(pp);
