@@ -220,8 +220,8 @@ def large_n(g, args, device):
         a2.n, a2.m = n, 4096
         W = torch.randn(a2.m, n, device=device)
         # one warm-up solve at every width: a cold call also pays the caching
-        # allocator's first hipMalloc of each workspace (at n = 28,672 the
-        # U factor's 16 GB alone measured +0.47 s)
+        # allocator's first hipMalloc of each workspace (two cold n = 28,672
+        # calls on identical U-factor code timed that phase at 0.77 and 1.24 s)
         phases(g, H, W, a2)
         ph, k = phases(g, H, W, a2)
         ent = dict(rank_k=k, path=phases.path, solve_ms=round(sum(ph.values()), 3), phases_ms=ph)
