@@ -56,6 +56,10 @@ struct BtArgs {
   unsigned *cnt;          // [0] step counter, [1] timeout flag (zeroed per call)
   unsigned long long timeout;
   int wexp;               // XCD form: workers wanted (= workgroups per XCD)
+  // Q2 as a wavefront (TG_BT_Q2_WAVE, default 1): colflag[G2] = blocks of
+  // sweep group G2 applied (zeroed per call, ~0u once the group is done)
+  unsigned *colflag;
+  int q2_wave;
 };
 
 struct SmQ2 {
@@ -534,7 +538,7 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
   __syncthreads();
 }
 
-template <int NCB>
+template <int NCB, bool Q2W>
 __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
   __shared__ BtShared sm;
   __shared__ int sh_w[2];
@@ -605,10 +609,43 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
     return false;
   };
   Q2Pre p2;
+  if constexpr (Q2W) if (a.nlev2 > 0) {
+    // Q2 as a wavefront instead of level by level: block (G2, s) needs the
+    // blocks of the later sweep group G2 + 1 up to step s (the rows it
+    // shares: (G2 + 1, s - 1) and (G2 + 1, s); everything else it overlaps
+    // precedes those), and its own group's step s - 1.  So each wave takes
+    // whole sweep groups, G2 descending, steps ascending, waits only for
+    // colflag[G2 + 1] >= s + 1 and publishes colflag[G2] after its Z stores
+    // drained -- point-to-point hand-offs in the one XCD's L2 (the level
+    // form paid a grid barrier per level: 255 levels at n = 4096).  Same
+    // blocks, same arithmetic, same order on every row: bit-identical Z.
+    const int NW = W * BW, gw = me * BW + wid;
+    unsigned *stall = a.cnt + 1;
+    const int lane = threadIdx.x & 63;
+    for (int c = gw; c < a.ng2; c += NW) {
+      const int G2 = a.ng2 - 1 - c, nb = ntasks(a.n, G2 * QB);
+      if (nb > 0) q2_fetch(a, G2, 0, p2);
+      for (int s = 0; s < nb; ++s) {
+        if (G2 + 1 < a.ng2) tg::spin_geq(a.colflag + G2 + 1, unsigned(s + 1), stall, a.timeout);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // Z loads stay below the poll
+        q2_block<NCB>(a, rz, G2, s, p2, sm.q2.Vs[wid], sm.q2.Ts[wid]);
+        if (s + 1 < nb) q2_fetch(a, G2, s + 1, p2);  // read-only reflectors: no wait needed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Z stores drained
+        if (lane == 0)
+          __hip_atomic_store((gu32 *)(a.colflag + G2), unsigned(s + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0)
+        __hip_atomic_store((gu32 *)(a.colflag + G2), ~0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    grid_barrier(a, unsigned(W) * ++step);  // every group done before Q1
+  }
   int nG2 = 0, ns = 0;
-  bool have = a.nlev2 > 0 && q2_first(0, nG2, ns);
+  const int nlev2 = Q2W ? 0 : a.nlev2;
+  bool have = nlev2 > 0 && q2_first(0, nG2, ns);
   if (have) q2_fetch(a, nG2, ns, p2);
-  for (int L = 0; L < a.nlev2; ++L) {
+  for (int L = 0; L < nlev2; ++L) {
     BT_T(t0)
     const int s_lo = max(0, L - (a.ng2 - 1)), s_hi = min(a.smax - 1, L);
     bool first = true;
@@ -620,7 +657,7 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
       q2_block<NCB>(a, rz, G2, s, p2, sm.q2.Vs[wid], sm.q2.Ts[wid]);
     }
     // next level's first block: its reflectors load across the barrier
-    if (L + 1 < a.nlev2 && q2_first(L + 1, nG2, ns)) q2_fetch(a, nG2, ns, p2);
+    if (L + 1 < nlev2 && q2_first(L + 1, nG2, ns)) q2_fetch(a, nG2, ns, p2);
     BT_T(t1)
     grid_barrier(a, unsigned(W) * ++step);
     BT_T(t2)
@@ -700,8 +737,12 @@ static size_t few_ops_bytes(const SbPlan &pl) {
 static int few_nsub(const SbPlan &pl) {
   return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) : 0;
 }
-size_t sb_apply_few_scratch(const SbPlan &pl) {
-  return few_ops_bytes(pl) + size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double);
+static size_t few_part_bytes(const SbPlan &pl) {
+  return size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double);
+}
+// + one progress word per Q2 sweep group (n / 32 + 1), 16-byte padded
+size_t sb_apply_few_scratch(const SbPlan &pl, int n) {
+  return few_ops_bytes(pl) + few_part_bytes(pl) + ((size_t(n / QB + 1) * 4 + 15) & ~size_t(15));
 }
 
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
@@ -740,6 +781,16 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.part = reinterpret_cast<double *>(static_cast<char *>(dev) + few_ops_bytes(pl));
   a.cnt = cnt;
   a.timeout = spin_timeout_ticks("TG_BT_TIMEOUT_TICKS");
+  a.colflag = reinterpret_cast<unsigned *>(static_cast<char *>(dev) + few_ops_bytes(pl) +
+                                           few_part_bytes(pl));
+  {
+    const char *qw = getenv("TG_BT_Q2_WAVE");  // development switch, read per call
+    a.q2_wave = (qw && qw[0] == '0') ? 0 : 1;
+  }
+  if (a.q2_wave && a.ng2 > 0) {
+    e = hipMemsetAsync(a.colflag, 0, ((size_t(a.ng2) * 4 + 15) & ~size_t(15)), st);
+    if (e != hipSuccess) return e;
+  }
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
   int W = std::min(256, std::max(std::max(std::max(1, cdiv(a.smax, BW)), pl.ncmax), few_nsub(pl)));
   // the workers (one CU each: BtShared fills the LDS) must all be resident:
@@ -750,10 +801,17 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.wexp = W;
   auto tok = prof_begin(st, PROF_Q2, 0.0, 0.0);
   const int grid = TG_BT_XCD ? xi.xcds * W : W;  // XCD form: W land on each XCD
-  if (k <= 16)
-    hipLaunchKernelGGL(bt_few_kernel<1>, dim3(grid), dim3(64 * BW), 0, st, a);
-  else
-    hipLaunchKernelGGL(bt_few_kernel<2>, dim3(grid), dim3(64 * BW), 0, st, a);
+  if (a.q2_wave) {
+    if (k <= 16)
+      hipLaunchKernelGGL((bt_few_kernel<1, true>), dim3(grid), dim3(64 * BW), 0, st, a);
+    else
+      hipLaunchKernelGGL((bt_few_kernel<2, true>), dim3(grid), dim3(64 * BW), 0, st, a);
+  } else {
+    if (k <= 16)
+      hipLaunchKernelGGL((bt_few_kernel<1, false>), dim3(grid), dim3(64 * BW), 0, st, a);
+    else
+      hipLaunchKernelGGL((bt_few_kernel<2, false>), dim3(grid), dim3(64 * BW), 0, st, a);
+  }
   prof_end(st, tok);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   unsigned h[24] = {0};

@@ -140,7 +140,7 @@ hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, double *T2);
 // Z (n x k row-major, k <= 32) <- Q1 Q2 Z in one persistent launch (backtr.hip);
 // T2 must hold the Q2 T factors; dev: sb_apply_few_scratch bytes of device
 // scratch.  Syncs the stream (reads the barrier timeout flag).
-size_t sb_apply_few_scratch(const SbPlan &pl);
+size_t sb_apply_few_scratch(const SbPlan &pl, int n);
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                         const SbBufs &b, void *dev, bool *timed_out);
 // Z (n x k row-major) <- Q1 Z.

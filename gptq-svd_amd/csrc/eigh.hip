@@ -1706,7 +1706,7 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   if (ts) {
     // few vectors (the complement path's request): one persistent launch
     const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
-    if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl) <= sizeof(double) * size_t(n) * tg::SB_B) {
+    if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl, n) <= sizeof(double) * size_t(n) * tg::SB_B) {
       TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.T2));
       bool tmo = false;
       TG_HIP(tg::sb_apply_few(st, n, w.Z, k, pl, sb, sb.X, &tmo));

@@ -132,3 +132,30 @@ def test_panel_pairs_large_n(monkeypatch):
     assert np.array_equal(values(None), paired)
     nrm = np.abs(plain).max()
     assert np.abs(paired - plain).max() <= 1e-12 * nrm
+
+
+@pytest.mark.parametrize("n,count", [(4096, 14), (2048, 32)])
+def test_q2_wavefront_bit_identical(n, count, monkeypatch):
+    """The few-vector back-transform's Q2 part as a wavefront of sweep
+    groups (point-to-point progress words, the default) gives the level-by-
+    level form's eigenvectors bit for bit (same blocks, same arithmetic,
+    same order on every row), twice in a row."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 9)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def vectors(wave):
+        monkeypatch.setenv("TG_BT_Q2_WAVE", wave)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - count, count,
+                 lib.ptr(V), n, lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    ref = vectors("0")
+    for _ in range(2):
+        assert np.array_equal(vectors("1"), ref)
