@@ -56,7 +56,7 @@ struct BtArgs {
   unsigned *cnt;          // [0] step counter, [1] timeout flag (zeroed per call)
   unsigned long long timeout;
   int wexp;               // XCD form: workers wanted (= workgroups per XCD)
-  // Q2 as a wavefront (TG_BT_Q2_WAVE, default 1): colflag[G2] = blocks of
+  // Q2 as a wavefront (TG_BT_Q2_WAVE=1): colflag[G2] = blocks of
   // sweep group G2 applied (zeroed per call, ~0u once the group is done)
   unsigned *colflag;
   int q2_wave;
@@ -785,7 +785,7 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
                                            few_part_bytes(pl));
   {
     const char *qw = getenv("TG_BT_Q2_WAVE");  // development switch, read per call
-    a.q2_wave = (qw && qw[0] == '0') ? 0 : 1;
+    a.q2_wave = (qw && qw[0] == '1') ? 1 : 0;
   }
   if (a.q2_wave && a.ng2 > 0) {
     e = hipMemsetAsync(a.colflag, 0, ((size_t(a.ng2) * 4 + 15) & ~size_t(15)), st);

@@ -137,7 +137,7 @@ def test_panel_pairs_large_n(monkeypatch):
 @pytest.mark.parametrize("n,count", [(4096, 14), (2048, 32)])
 def test_q2_wavefront_bit_identical(n, count, monkeypatch):
     """The few-vector back-transform's Q2 part as a wavefront of sweep
-    groups (point-to-point progress words, the default) gives the level-by-
+    groups (point-to-point progress words, TG_BT_Q2_WAVE=1) gives the level-by-
     level form's eigenvectors bit for bit (same blocks, same arithmetic,
     same order on every row), twice in a row."""
     from gptq_svd_amd import _lib as lib
