@@ -78,7 +78,10 @@ def parse():
                    help="skip the n = 8192 / 12288 / 14336 / 28672 solve timings in the extras")
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the end-to-end Qwen3-8B-shaped quantize wall-clock")
-    p.add_argument("--e2e-layers", type=int, default=36)
+    p.add_argument("--e2e-layers", type=int, default=36, help="layers of the Qwen3-8B-shaped run")
+    p.add_argument("--e2e-only", default="",
+                   help="comma list of e2e_qwen3_8b_shape, e2e_llama3_8b_shape, "
+                        "layer_llama3_70b_shape (default: all three)")
     p.add_argument("--e2e-samples", type=int, default=128)
     return p.parse_args()
 
@@ -248,39 +251,62 @@ QWEN3_8B = dict(vocab_size=151936, hidden_size=4096, intermediate_size=12288,
                 num_hidden_layers=36, num_attention_heads=32, num_key_value_heads=8, head_dim=128,
                 max_position_embeddings=40960, rope_theta=1000000.0, rms_norm_eps=1e-6,
                 tie_word_embeddings=False)
+# Meta-Llama-3-8B / -70B config.json dimensions (BASELINE configs[2], [4])
+LLAMA3_8B = dict(vocab_size=128256, hidden_size=4096, intermediate_size=14336,
+                 num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                 max_position_embeddings=8192, rope_theta=500000.0, rms_norm_eps=1e-5,
+                 tie_word_embeddings=False)
+LLAMA3_70B = dict(LLAMA3_8B, hidden_size=8192, intermediate_size=28672, num_hidden_layers=80,
+                  num_attention_heads=64)
+MODEL_SHAPES = {"qwen3_8b": ("qwen3", QWEN3_8B), "llama3_8b": ("llama", LLAMA3_8B),
+                "llama3_70b": ("llama", LLAMA3_70B)}
 
 
-def e2e_qwen3_shape(args, device):
-    """The second half of BASELINE.json's metric: end-to-end quantize
-    wall-clock of a Qwen3-8B-shaped model (the reference's `metrics.total_time`,
-    quantize.py:101, :257-260 -- 1522-1534 s on A100).  No
-    weights exist in this image, so the model is random-init (fp16, N(0, 0.02)
-    linears, unit norms) with Qwen3-8B's exact `Qwen3Config` dimensions, fed
-    128 random 2048-token sequences (the reference's n_samples x seq_len) in
-    batches of 32 (run_benchmark.py:111-127): every stage runs at production
-    shape -- calibration forwards, SYRK at N = 262,144 for n = 4096 and
-    12,288, four solves and seven gptq_fwrd per layer, the re-forward.
-    Settings: eigh, 4-bit asym g128, eps 1e-4 energy (BASELINE configs[3]'s
-    solver path; the rank k depends on the random activations).  Timing only:
-    the weights are random, so no PPL."""
-    from transformers import Qwen3Config, Qwen3ForCausalLM
-    from gptq_svd_amd import harness
-    cfg = Qwen3Config(**dict(QWEN3_8B, num_hidden_layers=args.e2e_layers))
+def random_causal_lm(shape: str, layers: int, device, seed: int = 0):
+    """A random-init fp16 model with the named model's exact config
+    dimensions (no weights exist in this image): N(0, 0.02) matrices, unit
+    norm weights, built on the meta device and materialised on `device`."""
+    from transformers import LlamaConfig, LlamaForCausalLM, Qwen3Config, Qwen3ForCausalLM
+    arch, dims = MODEL_SHAPES[shape]
+    Cfg, Model = (Qwen3Config, Qwen3ForCausalLM) if arch == "qwen3" else (LlamaConfig,
+                                                                           LlamaForCausalLM)
+    cfg = Cfg(**dict(dims, num_hidden_layers=layers))
     cfg._attn_implementation = "sdpa"
-    t0 = time.perf_counter()
     with torch.device("meta"):
-        model = Qwen3ForCausalLM(cfg)
+        model = Model(cfg)
     model = model.to(dtype=torch.float16).to_empty(device=device)
-    gen = torch.Generator(device=device).manual_seed(0)
+    gen = torch.Generator(device=device).manual_seed(seed)
     with torch.no_grad():
-        for name, p in model.named_parameters():
+        for _, p in model.named_parameters():
             if p.dim() == 2:
                 p.normal_(0.0, 0.02, generator=gen)
             else:
                 p.fill_(1.0)
         model.model.rotary_emb = type(model.model.rotary_emb)(config=cfg, device=device)
     model.eval()
-    ids = torch.randint(0, cfg.vocab_size, (args.e2e_samples, 2048), generator=gen,
+    return model, gen
+
+
+E2E_NOTE = ("random-init weights with the named model's dimensions and random token ids: a "
+            "timing of every stage at production shape, not the reference's workload -- no "
+            "PPL; the ranks k come out near n (random activations) where real models keep "
+            "fewer; calibration forwards stop at each group's first linear (the reference "
+            "runs the whole layer, quantize.py:139-148); the model stays resident in HBM "
+            "(the reference moves each layer CPU<->GPU, quantize.py:101, :250) and no "
+            "per-batch cleanup()/synchronize (quantize.py:28-35, :148)")
+
+
+def e2e_model_shape(shape: str, args, device, layers: int, samples: int,
+                    reference_total: str = None):
+    """End-to-end quantize wall-clock of a random-init model with a real
+    model's shape (the reference's `metrics.total_time`, quantize.py:101,
+    :257-260): 2048-token random sequences in batches of 32
+    (run_benchmark.py:111-127), eigh 4-bit asym g128, eps 1e-4 energy.
+    Per-stage device time from harness.StageClock."""
+    from gptq_svd_amd import harness
+    t0 = time.perf_counter()
+    model, gen = random_causal_lm(shape, layers, device)
+    ids = torch.randint(0, model.config.vocab_size, (samples, 2048), generator=gen,
                         device=device).cpu()
     ids = [ids[i:i + 1] for i in range(ids.shape[0])]
     torch.cuda.synchronize()
@@ -308,12 +334,35 @@ def e2e_qwen3_shape(args, device):
     med = {nm: int(sorted(v)[len(v) // 2]) for nm, v in ranks.items()}
     del model
     torch.cuda.empty_cache()
-    return dict(total_s=round(res["total_time"], 2), layers=args.e2e_layers,
-                samples=args.e2e_samples, seq_len=2048, batch_size=32,
-                stages_s=stages, stage_counts=dict(sorted(clock.counts.items())),
-                median_rank=med, model_init_s=round(t_init, 2),
-                reference_total_s="1522-1534 (A100 40GB, real weights, 36 layers)",
-                note="random-init weights with Qwen3-8B's dimensions: timing only, no PPL")
+    out = dict(total_s=round(res["total_time"], 2), layers=layers, samples=samples, seq_len=2048,
+               batch_size=32, stages_s=stages, stage_counts=dict(sorted(clock.counts.items())),
+               median_rank=med, model_init_s=round(t_init, 2))
+    if reference_total:
+        out["reference_total_s"] = reference_total
+    out["note"] = E2E_NOTE
+    return out
+
+
+def e2e_extras(args, device):
+    """BASELINE's model-level configs on one MI355X: the Qwen3-8B-shaped
+    (configs[3]'s model; the reference's 1522-1534 s run) and Llama-3-8B-shaped
+    (configs[2]) full-model quantize, and one Llama-3-70B-shaped layer
+    (configs[4]'s layer: hidden 8192, intermediate 28,672) with its stage
+    times -- the measured per-layer inputs of DESIGN.md §6's 8-GPU bound."""
+    out = {}
+    runs = [("e2e_qwen3_8b_shape", "qwen3_8b", args.e2e_layers,
+             "1522-1534 (A100 40GB, real weights, 36 layers)"),
+            ("e2e_llama3_8b_shape", "llama3_8b", 32, None),
+            ("layer_llama3_70b_shape", "llama3_70b", 1, None)]
+    for key, shape, layers, ref in runs:
+        if args.e2e_only and key not in args.e2e_only.split(","):
+            continue
+        try:
+            out[key] = e2e_model_shape(shape, args, device, layers, args.e2e_samples, ref)
+        except Exception as exc:  # the solver line stands without it
+            out[key] = dict(error=f"{type(exc).__name__}: {exc}")
+        torch.cuda.empty_cache()
+    return out
 
 
 def ar1_solve(g, args, device):
@@ -568,10 +617,7 @@ def run(args):
         if not args.no_large_n and (args.n, args.m) == (4096, 4096):
             extra["large_n"] = large_n(g, args, device)
         if not args.no_e2e and world == 1:
-            try:
-                extra["e2e_qwen3_8b_shape"] = e2e_qwen3_shape(args, device)
-            except Exception as exc:  # the solver line stands without it
-                extra["e2e_qwen3_8b_shape"] = dict(error=f"{type(exc).__name__}: {exc}")
+            extra.update(e2e_extras(args, device))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(H, W, args)

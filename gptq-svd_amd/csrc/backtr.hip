@@ -627,7 +627,14 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
       if (nb > 0) q2_fetch(a, G2, 0, p2);
       for (int s = 0; s < nb; ++s) {
         if (G2 + 1 < a.ng2) tg::spin_geq(a.colflag + G2 + 1, unsigned(s + 1), stall, a.timeout);
+#if TG_BT_XCD
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // Z loads stay below the poll
+#else
+        // placement-independent build: Z is read through L1 (load_z), so the
+        // producer's rows need an agent-scope acquire (its stores are
+        // write-through, store_sc1)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
         q2_block<NCB>(a, rz, G2, s, p2, sm.q2.Vs[wid], sm.q2.Ts[wid]);
         if (s + 1 < nb) q2_fetch(a, G2, s + 1, p2);  // read-only reflectors: no wait needed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Z stores drained

@@ -74,7 +74,7 @@ ProfTok prof_begin(hipStream_t st, int id, double bytes, double flops);
 void prof_end(hipStream_t st, ProfTok tok);
 
 // 16-bit Hessian SYRK (syrk.hip)
-size_t syrk16_workspace_size();
+size_t syrk16_workspace_size(int n);
 bool syrk16_supported(const void *X, int n, int64_t ldx);
 hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n, int64_t ldx,
                   double *H, int64_t ldh, void *ws);

@@ -1581,12 +1581,18 @@ __global__ __launch_bounds__(256) void diag_mean_kernel(const double *__restrict
 __global__ void flip_damp_kernel(const double *__restrict__ H, int64_t ldh, int n,
                                  const int64_t *__restrict__ perm, double damp,
                                  const double *__restrict__ mean, double *__restrict__ A) {
+  // Entry (i, j) of A = J H_p J is H_p[n-1-i][n-1-j]; it is always read from
+  // H_p's LOWER triangle (row n-1-min(i,j) >= column n-1-max(i,j)), the only
+  // triangle the reference's torch.linalg.cholesky(H_damped) reads
+  // (gptq_utils.py:152), so an H that is not bit-symmetric factors the same
+  // way.  A itself is then exactly symmetric, whichever triangle
+  // chol_upper_rows' panels and strip SYRKs read.
   const int i = blockIdx.y;
-  const int64_t pi = perm ? perm[n - 1 - i] : n - 1 - i;
   const double dm = damp * mean[0];
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const int64_t pj = perm ? perm[n - 1 - j] : n - 1 - j;
-    double v = H[pi * ldh + pj];
+    const int r = n - 1 - min(i, j), c = n - 1 - max(i, j);
+    const int64_t pr = perm ? perm[r] : r, pc = perm ? perm[c] : c;
+    double v = H[pr * ldh + pc];
     if (i == j) v += dm;
     A[int64_t(i) * n + j] = v;
   }

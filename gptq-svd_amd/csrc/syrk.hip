@@ -309,11 +309,16 @@ namespace tg {
 
 constexpr int NCMAX = 4;  // chunks per tail tile (G tail tiles)
 
-// Layout: partial tiles (G tail tiles x NCMAX chunks), the queue head, the
+// tail tiles cut into chunks: the last min(T, G) of the T lower tiles
+static int syrk16_tail_tiles(int n) {
+  const int nt = cdiv(n, BT);
+  return std::min(nt * (nt + 1) / 2, resident_groups());
+}
+// Layout: partial tiles (Tt tail tiles x NCMAX chunks), the queue head, the
 // TG_SYRK_STAMPS clocks (3 words per workgroup).
-size_t syrk16_workspace_size() {
+size_t syrk16_workspace_size(int n) {
   const size_t G = resident_groups();
-  return sizeof(double) * (G * NCMAX * BT * BT + 64 + 3 * G);
+  return sizeof(double) * (size_t(syrk16_tail_tiles(n)) * NCMAX * BT * BT + 64 + 3 * G);
 }
 
 bool syrk16_supported(const void *X, int n, int64_t ldx) {
@@ -342,13 +347,13 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   a.T = nt * (nt + 1) / 2;
   a.NS = cdiv(rows, NSUB * KC);
   const int G = resident_groups();
-  a.Tt = std::min(a.T, G);
+  a.Tt = syrk16_tail_tiles(n);
   a.head = a.T - a.Tt;
   a.NC = std::min(NCMAX, a.NS);
   a.CK = cdiv(a.NS, a.NC);
   a.U = a.head + a.Tt * a.NC;
   a.piece = static_cast<double *>(ws);
-  double *tail = a.piece + int64_t(G) * NCMAX * BT * BT;
+  double *tail = a.piece + int64_t(a.Tt) * NCMAX * BT * BT;
   a.next = reinterpret_cast<unsigned *>(tail);
   // development switch (read per call): per-workgroup start / end clocks and
   // XCD, for tools/syrk_time.py
@@ -368,8 +373,7 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
 }  // namespace tg
 
 extern "C" size_t tg_syrk_workspace_size(int n) {
-  (void)n;
-  return tg::syrk16_workspace_size();
+  return n > 0 ? tg::syrk16_workspace_size(n) : 0;
 }
 
 extern "C" int tg_syrk_accum_ws(void *stream, const void *X, int x_dtype, int64_t rows, int n,
@@ -385,7 +389,7 @@ extern "C" int tg_syrk_accum_ws(void *stream, const void *X, int x_dtype, int64_
   const bool b16 = x_dtype == TG_F16 || x_dtype == TG_BF16;
   if (!b16 || !tg::syrk16_supported(X, n, ldx) || rows > INT32_MAX)
     return tg_syrk_accum(stream, X, x_dtype, rows, n, ldx, H, ldh);
-  TG_ARG(ws && ws_bytes >= tg::syrk16_workspace_size(), 9, "workspace too small");
+  TG_ARG(ws && ws_bytes >= tg::syrk16_workspace_size(n), 9, "workspace too small");
   TG_HIP(tg::syrk16((hipStream_t)stream, X, x_dtype == TG_BF16, rows, n, ldx, H, ldh, ws));
   return 0;
 }

@@ -59,10 +59,20 @@ class HessianAccumulator:
             raise RuntimeError(f"add_batch: expected {self.H.shape[0]} features, got {n}")
         if rows:
             with torch.cuda.device(self.H.device):
-                if self._ws is None:  # the 16-bit SYRK's partial-tile scratch
+                # the 16-bit SYRK's partial-tile scratch, only for inputs that
+                # take it (fp16 / bf16, n and the row stride multiples of 8,
+                # 16-byte aligned); everything else runs the generic path
+                b16 = (x.dtype in (torch.float16, torch.bfloat16) and n % 8 == 0
+                       and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+                if b16 and self._ws is None:
                     self._ws = workspace(_lib.lib.tg_syrk_workspace_size(n), self.H.device)
-                call("tg_syrk_accum_ws", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
-                     x.stride(0), ptr(self.H), self.H.shape[0], ptr(self._ws), self._ws.numel())
+                if b16:
+                    call("tg_syrk_accum_ws", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
+                         x.stride(0), ptr(self.H), self.H.shape[0], ptr(self._ws),
+                         self._ws.numel())
+                else:
+                    call("tg_syrk_accum", stream(), ptr(x), _lib.DTYPES[x.dtype], rows, n,
+                         x.stride(0), ptr(self.H), self.H.shape[0])
         self.n_samples += rows
 
     def get_hessian(self):                                    # gptq_utils.py:225-228

@@ -39,10 +39,11 @@ What differs, deliberately:
   fingerprint reduction before any row is quantised); each linear's rows
   are quantised by their owning rank (``dist.shard_rows``; rows are
   independent given U and perm) and all-gathered, so every rank writes the
-  same dequantised weight.  The reference places a 70B model's layers
-  across 8 GPUs and runs them one after another (quantize.py:238-249); here
-  each GPU holds the whole model (288 GB) and the ranks split the
-  calibration forward passes, the H accumulation and the quantisation.
+  same dequantised weight.  The reference has no multi-GPU mode: it loads
+  the model on one device (model_utils.py:45, ``device_map=device``) and
+  moves one layer at a time to it (quantize.py:101, :250).  Here each GPU
+  holds the whole model (288 GB) and the ranks split the calibration forward
+  passes, the H accumulation and the quantisation.
 """
 from __future__ import annotations
 
@@ -58,7 +59,7 @@ from .gptq_utils import (HessianAccumulator, Quantizer, gptq_fwrd, log_quantizat
                          pack_quantized, process_hessian, process_hessian_alt)
 
 __all__ = ["get_layers", "get_sequenced_groups", "capture_initial_inputs", "quantize_model",
-           "adaptive_eps", "StageClock", "check_factor_agrees"]
+           "adaptive_eps", "StageClock", "check_factor_agrees", "run_and_record"]
 
 
 def get_layers(model: nn.Module) -> nn.ModuleList:
@@ -238,14 +239,21 @@ def check_factor_agrees(R: torch.Tensor, perm: torch.Tensor, pg=None) -> None:
     Rd = R.to(torch.float64)
     fp = torch.stack([torch.tensor(float(R.shape[0]), dtype=torch.float64, device=R.device),
                       (perm.to(torch.float64) * pos).sum(), Rd.sum(), (Rd * Rd).sum()])
-    lo, hi = fp.clone(), fp.clone()
+    # compared as bit patterns: a NaN or Inf in a (shared) factor must not read
+    # as a disagreement between ranks (NaN != NaN as floats)
+    bits = fp.view(torch.int64)
+    lo, hi = bits.clone(), bits.clone()
     if fp.is_cuda and dist.get_backend(pg) == "gloo":
         lo, hi = lo.cpu(), hi.cpu()
     dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=pg)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=pg)
     if not torch.equal(lo, hi):
         raise RuntimeError("ranks disagree on the factorisation of the shared Hessian "
-                           f"(fingerprint min {lo.tolist()} max {hi.tolist()})")
+                           f"(fingerprint min {lo.view(torch.float64).tolist()} "
+                           f"max {hi.view(torch.float64).tolist()})")
+    if not bool(torch.isfinite(fp).all()):
+        raise RuntimeError("the shared factorisation is not finite on every rank "
+                           f"(fingerprint {fp.tolist()}): check the layer's Hessian")
 
 
 def quantize_linear_sharded(W: torch.Tensor, R: torch.Tensor, perm: torch.Tensor,
@@ -284,7 +292,8 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
                    damp_percent: float = 0.01, use_adaptive_eps: bool = False,
                    batch_size: int = 8, device="cuda", block_size: int = 1024,
                    pack: bool = False, offload: bool = False, pg=None, early_stop: bool = True,
-                   clock: Optional[StageClock] = None) -> Dict[str, Any]:
+                   clock: Optional[StageClock] = None, save_path: Optional[str] = None,
+                   run_config: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
     """Quantise every sequenced linear of `model` in place (layer by layer).
 
     mode "eigh" = TruncGPTQ (process_hessian_alt + gptq_fwrd(use_triton=True));
@@ -299,10 +308,23 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     skipped (the reference runs the whole layer and discards the output,
     quantize.py:139-148, so H is the same).  `clock`: a StageClock that
     receives per-stage device times.
+    `save_path`: write the run's ``quantization.log`` and ``results.json`` there
+    in the reference's schema (``runlog.py``; rank 0 only in multi-GPU mode);
+    `run_config` adds to / overrides the ``config`` block (e.g. model_id,
+    n_samples, seq_len).  ``quantized_ppl`` is added by ``runlog.RunLog.finish``
+    when the caller evaluates afterwards (see ``run_and_record``).
     Returns {"layer_stats": [...], "total_time": s, "packed": {name: tensors}}.
     """
     if mode not in ("eigh", "gptq"):
         raise ValueError(f"mode must be 'eigh' or 'gptq', got {mode!r}")
+    if save_path is not None:
+        res = run_and_record(model, input_ids_list, save_path, run_config, mode=mode,
+                             w_bits=w_bits, group_size=group_size, sym=sym, eps=eps,
+                             threshold_method=threshold_method, actorder=actorder,
+                             damp_percent=damp_percent, use_adaptive_eps=use_adaptive_eps,
+                             batch_size=batch_size, device=device, block_size=block_size,
+                             pack=pack, offload=offload, pg=pg, early_stop=early_stop, clock=clock)
+        return res
     t_start = time.time()
     world, rank = _world(pg)
     if world > 1:
@@ -424,3 +446,45 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     return {"layer_stats": stats, "total_time": time.time() - t_start, "packed": packed}
+
+
+def run_and_record(model: nn.Module, input_ids_list: Sequence[torch.Tensor], save_path: str,
+                   run_config: Optional[Dict[str, Any]] = None, evaluate=None,
+                   **kw) -> Dict[str, Any]:
+    """``quantize_model`` with the reference's run records (quantize.py:48-66,
+    :254-284): ``<save_path>/quantization.log`` receives every log line of the
+    run in the reference's format and ``<save_path>/results.json`` the config,
+    the per-module ``layer_stats`` and the metrics.  ``evaluate`` (optional):
+    a callable ``model -> ppl`` run after quantisation (e.g.
+    ``evaluate.evaluate_perplexity`` bound to a tokenizer); its value becomes
+    ``metrics.quantized_ppl`` as at quantize.py:281.  In multi-GPU mode only
+    rank 0 writes the files; every rank runs the same quantisation."""
+    from . import runlog
+    input_ids_list = list(input_ids_list)
+    world, rank = _world(kw.get("pg"))
+    cfg = runlog.reference_config(
+        device=str(kw.get("device", "cuda")), n_samples=len(list(input_ids_list)),
+        seq_len=int(input_ids_list[0].shape[-1]) if len(input_ids_list) else 0,
+        batch_size=kw.get("batch_size", 8), w_bits=kw.get("w_bits", 4),
+        group_size=kw.get("group_size", -1), sym=bool(kw.get("sym", False)),
+        eps=kw.get("eps", 1e-2), mode=kw.get("mode", "eigh"),
+        threshold_method=kw.get("threshold_method", "mean_trimmed"),
+        actorder=bool(kw.get("actorder", False)), damp_percent=kw.get("damp_percent", 0.01),
+        adaptive_eps=bool(kw.get("use_adaptive_eps", False)), save_path=save_path, no_save=True)
+    mid = getattr(getattr(model, "config", None), "_name_or_path", None)
+    if mid:
+        cfg["model_id"] = mid
+    cfg.update(run_config or {})
+    if rank != 0:
+        res = quantize_model(model, input_ids_list, **kw)
+        if evaluate is not None:
+            evaluate(model)
+        return res
+    with runlog.RunLog(save_path, cfg) as rl:
+        res = quantize_model(model, input_ids_list, **kw)
+        ppl = None
+        if evaluate is not None:
+            runlog.substep("Running final evaluation...")
+            ppl = float(evaluate(model))
+        rl.finish(res["layer_stats"], res["total_time"], ppl)
+    return res

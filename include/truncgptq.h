@@ -48,8 +48,8 @@ enum tg_rank_rule { TG_RULE_NONE = 0, TG_RULE_ENERGY = 1, TG_RULE_MEAN_TRIMMED =
 int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n, int64_t ldx,
                   double *H, int ldh);
 
-/* The same update with a caller workspace (tg_syrk_workspace_size bytes, a
- * device constant independent of n and rows): fp16 / bf16 X with n and ldx
+/* The same update with a caller workspace (tg_syrk_workspace_size(n) bytes,
+ * independent of rows; up to ~256 MiB at n >= 2944): fp16 / bf16 X with n and ldx
  * multiples of 8 and a 16-byte aligned X take the dedicated 16-bit SYRK
  * (syrk.hip: X kept 16-bit in LDS, lower 128 x 128 tiles handed out by an
  * atomic queue over a static decomposition whose partial tiles are summed in

@@ -175,6 +175,14 @@ def _factor_worker(rank, world, port, out):
             res["mismatch"] = "no error"
         except RuntimeError as e:
             res["mismatch"] = "RuntimeError" if "disagree" in str(e) else str(e)
+        # identical non-finite factors: reported as non-finite, not as a disagreement
+        R3 = R.clone()
+        R3[0, 0] = float("nan")
+        try:
+            check_factor_agrees(R3, perm)
+            res["nan"] = "no error"
+        except RuntimeError as e:
+            res["nan"] = "not finite" if "not finite" in str(e) else str(e)
         # fewer calibration sequences than ranks: every rank raises before a collective
         try:
             quantize_model(torch.nn.Linear(2, 2), [torch.zeros(1, 4, dtype=torch.long)],
@@ -194,6 +202,7 @@ def test_factor_agreement_and_short_calibration_raise_on_every_rank():
     mp.spawn(_factor_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in (0, 1):
         assert out[r]["mismatch"] == "RuntimeError", out[r]
+        assert out[r]["nan"] == "not finite", out[r]
         assert out[r]["few"] == "ValueError", out[r]
 
 

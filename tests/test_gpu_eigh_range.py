@@ -159,3 +159,34 @@ def test_q2_wavefront_bit_identical(n, count, monkeypatch):
     ref = vectors("0")
     for _ in range(2):
         assert np.array_equal(vectors("1"), ref)
+
+
+@pytest.mark.parametrize("n", [6400, 9000])
+def test_xm_asm_loads_bit_identical(n, monkeypatch):
+    """The X/M kernel's hand-written K loop (inline-asm loads with counted
+    waits, csrc/band.hip xm_load_asm, the default) against the compiler-
+    scheduled loop (TG_XM_ASM=0) on the paired path (trailing matrices of
+    >= 6144 rows: xm_kernel<2> with the pair products): the same MFMAs in the
+    same order, so the reduced matrix left in A and the eigenvalues must agree
+    bit for bit.  A register read before its load landed would show here;
+    tools/check_xm_isa.py guards the same loop statically in build()."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 12)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def values(asm):
+        if asm is None:
+            monkeypatch.delenv("TG_XM_ASM", raising=False)
+        else:
+            monkeypatch.setenv("TG_XM_ASM", asm)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        torch.cuda.synchronize()
+        return w.cpu().numpy(), A
+
+    w_asm, A_asm = values(None)
+    w_cc, A_cc = values("0")
+    assert torch.equal(A_asm, A_cc)
+    assert np.array_equal(w_asm, w_cc)

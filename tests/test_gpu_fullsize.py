@@ -8,6 +8,7 @@ seeded inputs (numpy/LAPACK eigh + dgeqp3 + QR: ~5 s on the box's host cores).
   codes given U      bit-exact vs the oracle's C loop (k-ordered fmaf chain)
   codes end to end   mismatch rate <= 6e-4    (the reference's own
                                                Triton-vs-loop disagreement)
+  both for 4-bit asym (the bench quantizer) and 3-bit sym (configs[3]).
 
 n = 8192 / 12288 / 14336 / 28672 (Llama-3-70B q/o, Qwen3-8B down, Llama-3-8B
 down, Llama-3-70B down -- BASELINE configs 3-5):
@@ -17,7 +18,8 @@ size-independent identities (the oracle would take minutes there):
   U R_x^T orthogonal, max |M^T M - I| <= 1e-9
       (A = L^-1/2 V^T P, S_k = L^1/2 V^T P give A S_k^T = I_k)
   |diag R_x| non-increasing, perm a permutation, sum S^2 = trace(H)
-  codes: 256 rows quantized with the GPU's U, bit-exact vs the oracle's C loop.
+  codes: 256 rows quantized with the GPU's U, bit-exact vs the oracle's C loop,
+         4-bit asym and 3-bit sym (BASELINE configs[3]'s quantizer).
 """
 import numpy as np
 import pytest
@@ -88,6 +90,41 @@ def test_fullsize_codes_given_u(g, bench_layer, oracle_mod):
                                       gemm="fma", impl="c", nthreads=16)
     assert k == k_ref
     assert np.array_equal(Wq.cpu().numpy(), ref)
+
+
+def test_fullsize_codes_given_u_w3sym(g, bench_layer, oracle_mod):
+    """BASELINE configs[3]'s quantizer (3-bit sym, g128; the sym branch of
+    Quantizer, gptq_utils.py:235-266) at 4096x4096 given the oracle's U:
+    bit-exact vs the oracle's C loop, codes and packed tensors included."""
+    _, _, W, f = bench_layer
+    q = g.Quantizer(3, 128, True)
+    Wq, k = g.gptq_fwrd(W.to(DEV), torch.from_numpy(f.U).to(DEV),
+                        q, torch.from_numpy(f.perm).to(DEV), block_size=1024)
+    ref, k_ref, codes = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 3, 128, True, 1024,
+                                             gemm="fma", impl="c", nthreads=16,
+                                             return_codes=True)
+    assert k == k_ref
+    assert np.array_equal(Wq.cpu().numpy(), ref)
+    off = oracle_mod.code_offset(3, True)          # sym codes are stored +2^(b-1)
+    assert np.array_equal(q.codes.cpu().numpy().astype(np.int64), codes.astype(np.int64) + off)
+    s, z = oracle_mod.find_params(W.numpy(), 3, 128, True)
+    qw, qz, sc = g.pack_quantized(q)
+    rqw, rqz, rsc = oracle_mod.pack_weights(codes, s, z, 3, True)
+    assert np.array_equal(qw.cpu().numpy(), rqw) and np.array_equal(qz.cpu().numpy(), rqz)
+    assert np.array_equal(sc.cpu().numpy(), rsc)
+
+
+def test_fullsize_end_to_end_w3sym(g, bench_layer, oracle_mod):
+    """Own H -> own U/perm -> 3-bit sym codes vs the oracle's whole path."""
+    _, H, W, f = bench_layer
+    R, R_x, perm = g.process_hessian_alt(H, 1e-4, "energy")
+    q = g.Quantizer(3, 128, True)
+    Wq, k = g.gptq_fwrd(W.to(DEV), R, q, perm, block_size=1024, R_x=R_x)
+    ref, _ = oracle_mod.gptq_fwrd(W.numpy(), f.U, f.perm, 3, 128, True, 1024,
+                                  gemm="torch", impl="c", nthreads=16)
+    mism = float(np.mean(Wq.cpu().numpy() != ref))
+    print(f"4096^2 3-bit sym end-to-end code mismatch vs oracle (MKL order): {mism:.2e}")
+    assert mism <= 6e-4
 
 
 def test_fullsize_end_to_end(g, bench_layer, oracle_mod):
@@ -193,12 +230,15 @@ def test_large_n_identities(g, oracle_mod, n, path, monkeypatch):
     dg = R_x.diagonal().abs()
     assert bool((dg[1:] <= dg[:-1] * (1 + 1e-12)).all())
     assert bool((U.diagonal() > 0).all())
-    # quantize 256 rows with the GPU's own U: bit-exact vs the oracle's C loop
+    # quantize 256 rows with the GPU's own U: bit-exact vs the oracle's C loop,
+    # with the bench quantizer (4-bit asym) and BASELINE configs[3]'s (3-bit sym)
     torch.manual_seed(n)
     W = torch.randn(256, n)
-    q = g.Quantizer(4, 128, False)
-    Wq, kq = g.gptq_fwrd(W.to(DEV), U, q, perm, block_size=1024)
-    ref, _ = oracle_mod.gptq_fwrd(W.numpy(), U.cpu().numpy(), perm.cpu().numpy(), 4, 128, False,
-                                  1024, gemm="fma", impl="c", nthreads=16)
-    assert kq == k
-    assert np.array_equal(Wq.cpu().numpy(), ref)
+    Un, pn = U.cpu().numpy(), perm.cpu().numpy()
+    for bits, sym in ((4, False), (3, True)):
+        q = g.Quantizer(bits, 128, sym)
+        Wq, kq = g.gptq_fwrd(W.to(DEV), U, q, perm, block_size=1024)
+        ref, _ = oracle_mod.gptq_fwrd(W.numpy(), Un, pn, bits, 128, sym, 1024, gemm="fma",
+                                      impl="c", nthreads=16)
+        assert kq == k
+        assert np.array_equal(Wq.cpu().numpy(), ref), (bits, sym)

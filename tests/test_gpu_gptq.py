@@ -114,3 +114,31 @@ def test_hinv_chol_sizes(g, n):
     Hd = H + 0.01 * torch.diagonal(H).mean() * torch.eye(n, dtype=torch.float64, device=DEV)
     E = R.T @ R @ Hd - torch.eye(n, dtype=torch.float64, device=DEV)
     assert float(E.abs().max()) <= 1e-9
+
+
+@pytest.mark.parametrize("n,actorder", [(300, False), (1100, True)])
+def test_hinv_chol_reads_lower_triangle(g, n, actorder):
+    """The reference's torch.linalg.cholesky(H_damped) (gptq_utils.py:152)
+    reads only the lower triangle of H_p = H[perm][:, perm].  An H that is not
+    bit-symmetric (an FP64 accumulation in another order leaves one) must give
+    the factor of H_p's lower triangle: bit-identical to the factor of that
+    triangle mirrored, and different from that of the upper one mirrored.
+    With ActOrder the permutation depends on the diagonal only, so it is the
+    same for all three inputs."""
+    torch.manual_seed(n)
+    X = torch.randn(n + 64, n, dtype=torch.float64, device=DEV)
+    H = X.T @ X / X.shape[0]
+    E = torch.randn(n, n, dtype=torch.float64, device=DEV) * 1e-9 * H.abs().max()
+    Ha = H + torch.triu(E, 1)                                 # not bit-symmetric
+    p = (torch.argsort(torch.diagonal(Ha), descending=True) if actorder
+         else torch.arange(n, device=DEV))
+    inv = torch.argsort(p)
+    Hp = Ha[p][:, p]
+    lower = (torch.tril(Hp) + torch.tril(Hp, -1).T)[inv][:, inv]
+    upper = (torch.triu(Hp) + torch.triu(Hp, 1).T)[inv][:, inv]
+    Ra, pa = g.process_hessian(Ha, actorder=actorder)
+    Rl, pl = g.process_hessian(lower, actorder=actorder)
+    Ru, _ = g.process_hessian(upper, actorder=actorder)
+    assert torch.equal(pa, p) and torch.equal(pl, p)
+    assert torch.equal(Ra, Rl)
+    assert not torch.equal(Ra, Ru)
