@@ -697,6 +697,309 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Dataflow form of the same pipeline (TG_BULGE_DF=1).  The
+// step-synchronous kernel above runs every task of a step behind one
+// workgroup barrier, so a sweep advances by one task per slowest-wave step
+// and the next sweep trails by LAG whole steps.  Here every role wave of
+// every sweep runs its own task loop and waits only for the LDS progress
+// counters it depends on (counts of finished tasks per sweep and role):
+//   role 2 (G, + next reflector) of sweep q, task s:
+//       own reflector v(s) (cntG[q] >= s + 1: step 0 is first_refl),
+//       sweep q-1's A and D of task s + 1 (cntA/cntD[q-1] >= s + 2) and its
+//       G of task s + 1 (the pivot beta of its task s + 2: cntG[q-1] >= s + 3),
+//       a free reflector slot (cntA/cntD[q] >= s + 2 - DK);
+//   role 0 (A) of task s: cntG[q] >= s + 1 (v(s) and the block G(s-1) = A(s));
+//   role 1 (D) of task s: cntG[q] >= s + 1 and cntA/cntD[q-1] >= s + 2.
+// Sweep 0 of a group takes "sweep q-1"'s data from the loader instead
+// (columns [j0, loaded) of the ring hold the previous group's final values).
+// These are the task-window overlaps of the LAG = 2 pipeline (file header):
+// every hazard between the waves is read-after-write on those counters, so
+// the tasks compute exactly what the step-synchronous kernel computes, in
+// the same order on every element -- bit-identical d, e and reflectors.
+// A loader wave fills the ring b columns at a time once the previous group's
+// column watermark (prog[G-1], columns below it written back) covers them
+// and the ring slot is free; a writer wave writes back every column no task
+// of the group will touch again (below the lowest column of the slowest
+// role of every sweep), drains, and publishes that watermark as prog[G].
+// Waits are bounded (spin.h): a wait past the timeout sets the stall word and
+// the workgroup's dead flag, after which no wave waits again and the launch
+// drains with poisoned output.
+// ---------------------------------------------------------------------------
+#ifndef TG_BULGE_DF_GSW
+#define TG_BULGE_DF_GSW 2
+#endif
+constexpr int DG = TG_BULGE_DF_GSW;   // sweeps per group
+constexpr int DK = 4;                 // reflector slots per sweep
+constexpr int DNCW = 3 * DG;          // role waves
+constexpr int DBT = 64 * (DNCW + 2);  // + loader + writer
+// ring span at the tightest spacing: the loader's chunk ahead of sweep 0
+// plus LAG b columns per later sweep, plus the write-back chunk
+static_assert((2 * DG + 1) * SB_B <= RING, "LDS ring too small for TG_BULGE_DF_GSW");
+
+struct DfSync {
+  unsigned cnt[3][DG];  // [role][sweep]: tasks finished (role 2: + 1 for first_refl)
+  unsigned loaded;      // columns [j0, loaded) are in the ring, final from the previous group
+  unsigned wbs;         // columns below wbs are written back (their ring slots are free)
+  unsigned dead;        // a wait gave up: nothing waits any more
+};
+
+__device__ __forceinline__ unsigned lds_get(const unsigned *p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// publish after this wave's LDS writes (only LDS ordering matters: a release
+// fence would also wait for the wave's global stores, the reflector records)
+__device__ __forceinline__ void lds_put(unsigned *p, unsigned v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+#if TG_BULGE_STATS
+#define DF_T0() const uint64_t tw0_ = __builtin_amdgcn_s_memrealtime();
+#define DF_WAITED() st_wait += __builtin_amdgcn_s_memrealtime() - tw0_;
+#else
+#define DF_T0()
+#define DF_WAITED()
+#endif
+
+// whole-wave wait until *p >= v (LDS word); false once the launch is dead
+__device__ inline bool df_wait(const unsigned *p, unsigned v, DfSync &sy, unsigned *stall,
+                               unsigned long long timeout) {
+  if (lds_get(p) >= v) return true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned it = 0;; ++it) {
+    if (lds_get(&sy.dead)) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if (lds_get(p) >= v) break;
+    if ((it & 63u) == 63u) {
+      if (__builtin_amdgcn_readfirstlane(tg::ctl_load(stall)) != 0u ||
+          __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        tg::ctl_store(stall, 1u);
+        lds_put(&sy.dead, 1u);
+        return false;
+      }
+    }
+  }
+  asm volatile("" ::: "memory");  // the data loads stay below the poll
+  return true;
+}
+
+// lowest column any role of sweep j still touches (n once the sweep is done):
+// first_refl (cntG = 0) touches column j, task 0 columns >= j + 1, task s > 0
+// columns >= r1 - b + 1 (its pivot column is final before it starts)
+__device__ inline int df_low(int n, int j, unsigned ca, unsigned cd, unsigned cg) {
+  if (cg == 0) return j;
+  const int s = int(min(min(ca, cd), cg - 1));
+  if (s >= ntasks(n, j)) return n;
+  return s == 0 ? j + 1 : j + 2 + (s - 1) * SB_B;
+}
+
+// ctl[0] = chosen XCD + 1, ctl[1] = group queue, ctl[2] = stall word, ctl[4..68) dummies;
+// prog[G] = column watermark of group G (columns below it written back)
+__global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, int n,
+                                                      double *__restrict__ V2, int smax,
+                                                      unsigned *__restrict__ prog,
+                                                      unsigned *__restrict__ ctl,
+                                                      unsigned long long *__restrict__ stats,
+                                                      unsigned long long timeout) {
+  __shared__ double R[RING][LDB];
+  __shared__ WaveScratch wsc[DNCW];
+  __shared__ Refl rfl[DG][DK];
+  __shared__ DfSync sy;
+  __shared__ int sh_G;
+  const int tid = threadIdx.x, wlane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned *stall = ctl + 2;
+  unsigned *dummy = ctl + 4;
+#if TG_BULGE_STATS
+  uint64_t st_wait = 0, st_busy = 0, st_tasks = 0;
+  const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned expect = 0;
+    __hip_atomic_compare_exchange_strong(ctl, &expect, x + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned chosen = expect == 0 ? x + 1 : expect;
+    sh_G = (chosen == x + 1) ? 0 : -1;
+  }
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(sh_G) < 0) return;
+  const int nsw = n - 2;
+  const int ngroups = tg::cdiv(nsw, DG);
+  const int bytes = n * LDB * int(sizeof(double));
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(B, 0, bytes, 0x00020000);
+  constexpr int SC1 = 16;
+  constexpr int NTC = LDB / 2;               // 16-B chunks per column
+  constexpr int PL = SB_B * NTC / 64;        // chunks per lane of a b-column load
+  while (true) {
+    if (wid == 0) {
+      const unsigned v = atomicAdd(lane0_or_dummy(ctl + 1, dummy, wlane), 1u);
+      const int Gn = tg::ctl_load(stall) ? ngroups : int(__builtin_amdgcn_readfirstlane(v));
+      sh_G = Gn;
+      // reset the group's counters: every lane writes one word (no lane-0 branch)
+      unsigned *w = &sy.cnt[0][0];
+      constexpr int NWD = int(sizeof(DfSync) / sizeof(unsigned));
+      const int k = min(wlane, NWD - 1);
+      const int j0n = Gn * DG;
+      w[k] = (k == int(offsetof(DfSync, loaded) / sizeof(unsigned))) ? unsigned(j0n)
+             : (k == int(offsetof(DfSync, wbs) / sizeof(unsigned))) ? unsigned(j0n)
+                                                                     : 0u;
+    }
+    __syncthreads();
+    const int G = __builtin_amdgcn_readfirstlane(sh_G);
+    __syncthreads();
+    if (G >= ngroups) break;
+    const int j0 = G * DG;
+    const int g = min(DG, nsw - j0);
+    if (wid < DNCW) {
+      const int q = wid / 3, role = wid % 3;
+      const int j = j0 + q;
+      if (q < g) {
+        const int nt = ntasks(n, j);
+        const int ntp = q > 0 ? ntasks(n, j - 1) : 0;
+        unsigned *own = &sy.cnt[role][q];
+        // columns [.., c) must hold the previous sweep's results
+        auto need_prev = [&](int s_next, bool with_g) -> bool {
+          // sweep q-1 finished tasks < s_next (A, D) and its G of task s_next - 1
+          if (q > 0) {
+            const unsigned a = unsigned(min(s_next, ntp));
+            bool ok = df_wait(&sy.cnt[0][q - 1], a, sy, stall, timeout);
+            ok = ok && df_wait(&sy.cnt[1][q - 1], a, sy, stall, timeout);
+            if (with_g) ok = ok && df_wait(&sy.cnt[2][q - 1], unsigned(min(s_next + 1, ntp + 1)), sy,
+                                           stall, timeout);
+            return ok;
+          }
+          return true;
+        };
+        if (role == 2) {
+          DF_T0()
+          if (q > 0) {
+            df_wait(&sy.cnt[1][q - 1], 1u, sy, stall, timeout);
+            df_wait(&sy.cnt[2][q - 1], unsigned(min(2, ntp + 1)), sy, stall, timeout);
+          } else {
+            df_wait(&sy.loaded, unsigned(j + 1), sy, stall, timeout);
+          }
+          DF_WAITED()
+          first_refl(R, n, j, rfl[q][0]);
+          lds_put(own, 1u);
+        }
+        for (int s = 0; s < nt; ++s) {
+          const int r1 = j + 1 + s * SB_B;
+          {
+            DF_T0()
+            if (role != 2) df_wait(&sy.cnt[2][q], unsigned(s + 1), sy, stall, timeout);
+            if (role != 0) {
+              if (q == 0)
+                df_wait(&sy.loaded, unsigned(min(n, r1 + SB_B)), sy, stall, timeout);
+              else
+                need_prev(s + 2, role == 2);
+            }
+            if (role == 2 && s + 1 < nt && s + 2 - DK > 0) {
+              df_wait(&sy.cnt[0][q], unsigned(s + 2 - DK), sy, stall, timeout);
+              df_wait(&sy.cnt[1][q], unsigned(s + 2 - DK), sy, stall, timeout);
+            }
+            DF_WAITED()
+          }
+#if TG_BULGE_STATS
+          const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
+#endif
+          const bool nx = s + 1 < nt;
+          const Refl &ri = rfl[q][s % DK];
+          Refl &ro = rfl[q][(s + 1) % DK];
+          if (r1 >= SB_B && r1 + 2 * SB_B <= n)
+            bulge_task_lds<true>(R, n, j, s, role, nx, V2, smax, wsc[wid], ri, ro);
+          else
+            bulge_task_lds<false>(R, n, j, s, role, nx, V2, smax, wsc[wid], ri, ro);
+          lds_put(own, unsigned(s + 1 + (role == 2)));
+#if TG_BULGE_STATS
+          st_busy += __builtin_amdgcn_s_memrealtime() - tb0;
+          ++st_tasks;
+#endif
+        }
+      }
+    } else if (wid == DNCW) {
+      // loader: b columns at a time once the producer's watermark covers them
+      // and their ring slots are written back.  Chunks end at j0 + 1 + k b --
+      // the columns task k - 1 of sweep 0 needs, and the watermarks the
+      // producer's last sweep publishes -- after a first chunk of column j0
+      // alone (first_refl)
+      for (int ld = j0; ld < n;) {
+        const int ce = min(ld == j0 ? j0 + 1 : ld + SB_B, n);
+        DF_T0()
+        if (G > 0 && !lds_get(&sy.dead) && !tg::spin_geq(prog + G - 1, unsigned(ce), stall, timeout))
+          lds_put(&sy.dead, 1u);
+        df_wait(&sy.wbs, unsigned(max(0, ce - RING)), sy, stall, timeout);
+        DF_WAITED()
+        double2 buf[PL];
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int idx = wlane + 64 * u;
+          const int c = min(ld + idx / NTC, ce - 1), h = idx % NTC;
+          const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * LDB + 2 * h) * 8, 0, SC1);
+          buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
+                                __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
+        }
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int idx = wlane + 64 * u;
+          const int c = ld + idx / NTC, h = idx % NTC;
+          if (c < ce) {
+            R[rslot(c)][2 * h] = buf[u].x;
+            R[rslot(c)][2 * h + 1] = buf[u].y;
+          }
+        }
+        lds_put(&sy.loaded, unsigned(ce));
+        ld = ce;
+      }
+    } else {
+      // writer: every column below the group's low watermark, then publish it
+      int wb = j0;
+      while (wb < n) {
+        int low = int(lds_get(&sy.loaded));
+        if (lds_get(&sy.dead)) low = n;
+        for (int q = 0; q < g; ++q)
+          low = min(low, df_low(n, j0 + q, lds_get(&sy.cnt[0][q]), lds_get(&sy.cnt[1][q]),
+                                lds_get(&sy.cnt[2][q])));
+        if (low <= wb) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        asm volatile("" ::: "memory");
+        const int lim = (low - wb) * NTC;
+        for (int b0 = 0; b0 < lim; b0 += 64) {
+          const int idx = b0 + wlane;
+          if (idx < lim) {
+            const int c = wb + idx / NTC, h = idx % NTC;
+            const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
+            const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                   (c * LDB + 2 * h) * 8, 0, 0);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(low));
+        lds_put(&sy.wbs, unsigned(low));
+        wb = low;
+      }
+    }
+    __syncthreads();
+  }
+#if TG_BULGE_STATS
+  if (stats && wlane == 0) {
+    atomicAdd(stats + 8 + 3 * wid, (unsigned long long)st_wait);
+    atomicAdd(stats + 9 + 3 * wid, (unsigned long long)st_busy);
+    atomicAdd(stats + 10 + 3 * wid, (unsigned long long)st_tasks);
+    if (wid == 0) {
+      atomicAdd(stats + 0, 1ull);
+      atomicAdd(stats + 5, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_t0));
+    }
+  }
+#endif
+}
+
 // Bst[c][d] = A[c + d][c] for d <= b, 0 for b < d < 2b.
 __global__ void extract_band_kernel(const double *__restrict__ A, int64_t lda, int n,
                                     double *__restrict__ Bst) {
@@ -724,8 +1027,17 @@ namespace tg {
 
 int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 
-// progress word per sweep group + control words + 64 dummy words
-size_t sb2st_prog_words(int n) { return size_t(cdiv(std::max(1, n - 2), G_SW)) + 4 + 64; }
+// progress word per sweep group (at most one group per sweep, whichever
+// kernel runs) + control words + 64 dummy words; the control words start at
+// prog + (n - 2)
+size_t sb2st_prog_words(int n) { return size_t(std::max(1, n - 2)) + 4 + 64; }
+
+// TG_BULGE_DF=1: the dataflow kernel (bulge_df_kernel); default the
+// step-synchronous kernel (bulge_lds_kernel)
+static bool bulge_dataflow() {
+  const char *e = getenv("TG_BULGE_DF");
+  return e && e[0] == '1';
+}
 
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
                  unsigned *prog, double *d, double *e) {
@@ -736,10 +1048,10 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
   const int nsw = n - 2;
   const unsigned *stall = nullptr;
   if (nsw > 0) {
-    const int ngroups = cdiv(nsw, G_SW);
+    const bool df = bulge_dataflow();
     err = hipMemsetAsync(prog, 0, sizeof(unsigned) * sb2st_prog_words(n), st);
     if (err != hipSuccess) return err;
-    unsigned *ctl = prog + ngroups;  // [0] XCD + 1, [1] group queue, [2] stall flag
+    unsigned *ctl = prog + nsw;  // [0] XCD + 1, [1] group queue, [2] stall flag
     stall = ctl + 2;
     const unsigned long long timeout = spin_timeout_ticks("TG_BULGE_TIMEOUT_TICKS");
     // TG_BULGE_STATS (environment): elapsed time of the launch; with a
@@ -757,8 +1069,8 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (want) {
       if (TG_BULGE_STATS) {
-        (void)hipMalloc(&stats, 24 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(stats, 0, 24 * sizeof(unsigned long long), st);
+        (void)hipMalloc(&stats, 64 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(stats, 0, 64 * sizeof(unsigned long long), st);
       }
       (void)hipEventCreate(&e0);
       (void)hipEventCreate(&e1);
@@ -768,14 +1080,17 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     // band streamed once per sweep group (load + write-back, L2-resident)
     double ntask = 0.0;
     for (int j = 0; j < nsw; ++j) ntask += (n - 3 - j) / SB_B + 1;
-    auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / G_SW,
+    auto tok = tg::prof_begin(st, tg::PROF_BULGE, 8.0 * LDB * double(n) * n / (df ? DG : G_SW),
                               12.0 * SB_B * SB_B * ntask);
     // one workgroup per CU (the ring fills the LDS): the elected XCD's share
     // of the grid is its CUs, the other XCDs' workgroups exit at once
     const XcdInfo xi = xcd_info();
-    hipLaunchKernelGGL(bulge_lds_kernel, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st, Bst, n,
-                       V2, sb_smax(n),
-                       prog, ctl, stats, timeout);
+    if (df)
+      hipLaunchKernelGGL(bulge_df_kernel, dim3(xi.xcds * xi.cus_per_xcd), dim3(DBT), 0, st, Bst,
+                         n, V2, sb_smax(n), prog, ctl, stats, timeout);
+    else
+      hipLaunchKernelGGL(bulge_lds_kernel, dim3(xi.xcds * xi.cus_per_xcd), dim3(BT), 0, st, Bst,
+                         n, V2, sb_smax(n), prog, ctl, stats, timeout);
     tg::prof_end(st, tok);
     err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -803,12 +1118,24 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
 #endif
     if (want) {
       (void)hipEventRecord(e1, st);
-      unsigned long long h[24] = {0};
+      unsigned long long h[64] = {0};
       if (stats) (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
       (void)hipStreamSynchronize(st);
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
-      fprintf(stderr, "bulge: %.2f ms (G_SW %d)\n", ms, G_SW);
+      fprintf(stderr, "bulge: %.2f ms (%s, G_SW %d)\n", ms, df ? "dataflow" : "step", df ? DG : G_SW);
+      if (stats && df) {
+        fprintf(stderr, "  workers %llu, worker time %.1f us; per wave [wait us, busy us, tasks]:\n",
+                h[0], h[5] / 100.0 / double(h[0] ? h[0] : 1));
+        for (int w = 0; w < DNCW + 2; ++w)
+          fprintf(stderr, "   w%d %s: %.0f %.0f %llu (%.2f us/task)\n", w,
+                  w < DNCW ? (w % 3 == 0 ? "A" : w % 3 == 1 ? "D" : "G") : (w == DNCW ? "load" : "write"),
+                  h[8 + 3 * w] / 100.0 / double(h[0] ? h[0] : 1),
+                  h[9 + 3 * w] / 100.0 / double(h[0] ? h[0] : 1), h[10 + 3 * w],
+                  h[10 + 3 * w] ? h[9 + 3 * w] / 100.0 / double(h[10 + 3 * w]) : 0.0);
+        (void)hipFree(stats);
+        stats = nullptr;
+      }
       if (stats) {
         const double W = double(h[0]), S = double(h[6]);
         fprintf(stderr,
@@ -834,7 +1161,7 @@ hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stal
   const int nsw = n - 2;
   if (nsw <= 0) return hipSuccess;
   unsigned h = 0;
-  hipError_t e = hipMemcpyAsync(&h, prog + cdiv(nsw, G_SW) + 2, sizeof(unsigned),
+  hipError_t e = hipMemcpyAsync(&h, prog + nsw + 2, sizeof(unsigned),
                                 hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   *stalled = h != 0u;

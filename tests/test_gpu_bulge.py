@@ -1,0 +1,75 @@
+"""Band -> tridiagonal stage (csrc/bulge.hip, the second half of
+torch.linalg.eigh at gptq_utils.py:92) through tg_band_tridiag.
+
+* The dataflow kernel (TG_BULGE_DF=1: per-wave task loops synchronised by
+  LDS progress counters) against the step-synchronous kernel (TG_BULGE_DF=0):
+  the same tasks with the same arithmetic in the same per-element order, so
+  d, e and every reflector record must agree bit for bit -- at widths that
+  exercise empty and one-task sweeps (n = 3 .. 65), partial last groups and
+  ring wrap-around (n >= 257), and the bench width.
+* The tridiagonal's eigenvalues against LAPACK on the band (1e-12 ||B||).
+"""
+import numpy as np
+import pytest
+import scipy.linalg as sl
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+B = 32
+LDB = 2 * B
+
+
+def band(n, seed):
+    rng = np.random.default_rng(seed)
+    A = np.zeros((n, n))
+    for dg in range(min(B, n - 1) + 1):
+        v = rng.standard_normal(n - dg)
+        A[np.arange(dg, n), np.arange(n - dg)] = v
+        A[np.arange(n - dg), np.arange(dg, n)] = v
+    return A
+
+
+def run(lib, A, df, monkeypatch):
+    n = A.shape[0]
+    monkeypatch.setenv("TG_BULGE_DF", df)
+    Ad = torch.from_numpy(A).to(DEV)
+    ws = lib.workspace(lib.lib.tg_band_tridiag_workspace_size(n), torch.device(DEV))
+    ws.zero_()
+    d = torch.empty(n, dtype=torch.float64, device=DEV)
+    e = torch.empty(n, dtype=torch.float64, device=DEV)
+    lib.call("tg_band_tridiag", lib.stream(), lib.ptr(Ad), n, n, lib.ptr(d), lib.ptr(e),
+             lib.ptr(ws), ws.numel())
+    torch.cuda.synchronize()
+    # V2 (the reflector records) follows the band storage in the workspace
+    nsw, smax = max(1, n - 2), (n - 3) // B + 1 if n >= 3 else 1
+    off = -(-n * LDB * 8 // 256) * 256
+    v2 = ws[off: off + nsw * smax * B * 8].cpu().numpy().view(np.float64)
+    return d.cpu().numpy(), e.cpu().numpy(), v2
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 33, 34, 35, 64, 65, 100, 257, 600, 1000, 2049, 4096])
+def test_dataflow_bit_identical(n, monkeypatch):
+    from gptq_svd_amd import _lib as lib
+    A = band(n, n)
+    d0, e0, v0 = run(lib, A, "0", monkeypatch)
+    d1, e1, v1 = run(lib, A, "1", monkeypatch)
+    assert np.isfinite(d1).all()
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+    assert np.array_equal(e0[:n - 1].view(np.uint64), e1[:n - 1].view(np.uint64))
+    assert np.array_equal(v0.view(np.uint64), v1.view(np.uint64))
+    if n >= 64:
+        w = sl.eigvalsh_tridiagonal(d1, e1[:n - 1])
+        ref = sl.eigvalsh(A)
+        assert np.abs(w - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+def test_dataflow_repeats(monkeypatch):
+    """Run to run: the dataflow schedule changes with timing, the values may not."""
+    from gptq_svd_amd import _lib as lib
+    A = band(3000, 7)
+    ref = run(lib, A, "1", monkeypatch)
+    for _ in range(3):
+        got = run(lib, A, "1", monkeypatch)
+        for a, b in zip(ref, got):
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
