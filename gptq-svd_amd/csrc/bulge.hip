@@ -162,6 +162,7 @@ __device__ inline int rslot(int c) { return c & (RING - 1); }
 struct Refl {
   double v[SB_B];
   double tau, beta;
+  double tu[SB_B];  // dataflow kernel: tau u of the lower block (row-indexed), see df_task
 };
 
 __device__ __forceinline__ void make_refl(double x, int li, int hf, double &v, double &tau,
@@ -698,7 +699,8 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 }
 
 // ---------------------------------------------------------------------------
-// Dataflow form of the same pipeline (TG_BULGE_DF=1).  The
+// Dataflow form of the same pipeline (the default; TG_BULGE_DF=0 selects the
+// step-synchronous kernel above).  The
 // step-synchronous kernel above runs every task of a step behind one
 // workgroup barrier, so a sweep advances by one task per slowest-wave step
 // and the next sweep trails by LAG whole steps.  Here every role wave of
@@ -732,16 +734,187 @@ __global__ __launch_bounds__(BT) void bulge_lds_kernel(double *__restrict__ B, i
 constexpr int DG = TG_BULGE_DF_GSW;   // sweeps per group
 constexpr int DK = 4;                 // reflector slots per sweep
 constexpr int DNCW = 3 * DG;          // role waves
-constexpr int DBT = 64 * (DNCW + 2);  // + loader + writer
+#ifndef TG_BULGE_DF_XF
+#define TG_BULGE_DF_XF 1
+#endif
+constexpr int DXF = TG_BULGE_DF_XF;           // loader waves = writer waves (each moves 1/DXF)
+constexpr int DBT = 64 * (DNCW + 2 * DXF);    // + loaders + writers
 // ring span at the tightest spacing: the loader's chunk ahead of sweep 0
 // plus LAG b columns per later sweep, plus the write-back chunk
 static_assert((2 * DG + 1) * SB_B <= RING, "LDS ring too small for TG_BULGE_DF_GSW");
+
+// Task (j, s) for the dataflow kernel: bulge_task_lds's arithmetic with two
+// changes of WHO does it (the values and their order are the same):
+// * the lower block's rank-1 update G -= tau u v^T is applied by the role-0
+//   wave of the NEXT task, whose left block A(s+1) is exactly G(s): role 2
+//   forms u, the next reflector from the updated column 0 and writes only
+//   that pivot column (beta, 0, ..., 0) and tau u (into its reflector slot),
+//   so the next reflector is out after one matrix-vector product instead of
+//   a whole block update and store (on the last task of a sweep there is no
+//   next left block, and role 2 updates and stores G as before);
+// * each role loads its block first and waits for its reflector afterwards
+//   (`wait_v`), so the block loads overlap the wait.
+template <bool FULL, class WaitV>
+__device__ __forceinline__ void df_task(double (*R)[LDB], int n, int j, int s, int role,
+                                        bool has_next, double *__restrict__ V2, int smax,
+                                        WaveScratch &W, Refl *slots, int DKs, WaitV wait_v) {
+  // the lane index is opaque to the compiler here, so the per-lane block
+  // addresses are formed per task instead of being hoisted out of the task
+  // loop for every role (that kept ~80 loop-invariant registers live)
+  int lane = threadIdx.x & 63;
+  if constexpr (DBT > 512) asm volatile("" : "+v"(lane));  // only under a < 256-VGPR cap
+  const int li = lane & 31, hf = lane >> 5;
+  const int r1 = j + 1 + s * SB_B;
+  const int L = FULL ? SB_B : min(SB_B, n - r1);
+  const int col = (s == 0) ? j : r1 - SB_B;
+  const int lo = FULL ? r1 - SB_B : max(0, r1 - SB_B);
+  const int nl = FULL ? SB_B : r1 - lo;
+  const int ng = FULL ? SB_B : min(SB_B, n - (r1 + L));
+  double *Rf = &R[0][0];
+  auto at = [&](int c, int d) { return rslot(c) * LDB + d; };
+  const Refl &rin = slots[s % DKs];
+  if (role == 0 && s == 0) {
+    wait_v();
+    store_refl(V2 + int64_t(j) * smax * SB_B, rin, lane);
+    return;
+  }
+  double e[16];
+  if (role == 0) {
+    const int ca = FULL ? li : min(li, max(nl - 1, 0));
+    const int abase = at(lo + ca, r1 - lo - ca);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = hf + 2 * q;
+      if (FULL) e[q] = Rf[abase + i];
+      else e[q] = (li < nl && i < L) ? Rf[abase + min(i, L - 1)] : 0.0;
+    }
+  } else if (role == 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      const int cc = min(li, k), off = li > k ? li - k : k - li;
+      if (FULL) e[q] = Rf[at(r1 + cc, off)];
+      else e[q] = (li < L && k < L) ? Rf[at(r1 + min(cc, L - 1), off)] : 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      if (FULL) e[q] = Rf[at(r1 + k, SB_B + li - k)];
+      else {
+        const int kc = min(k, L - 1);
+        const double gv = Rf[at(r1 + kc, L + min(li, max(ng - 1, 0)) - kc)];
+        e[q] = (li < ng && k < L) ? gv : 0.0;
+      }
+    }
+  }
+  wait_v();
+  const double v = rin.v[li], tau = rin.tau;
+  double vk[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) vk[q] = rin.v[hf + 2 * q];
+  if (role == 2) {
+    double u0 = 0.0, u1 = 0.0, u2 = 0.0, u3 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q += 4) {
+      u0 += e[q] * vk[q];
+      u1 += e[q + 1] * vk[q + 1];
+      u2 += e[q + 2] * vk[q + 2];
+      u3 += e[q + 3] * vk[q + 3];
+    }
+    double u = (u0 + u1) + (u2 + u3);
+    u = hsum32(u);
+    const double tu = tau * u;
+    if (has_next) {
+      Refl &rout = slots[(s + 1) % DKs];
+      const double x0 = e[0] - tu * vk[0];  // updated column 0 (lanes hf == 0)
+      double vn, tn, bn;
+      make_refl((FULL || li < ng) ? x0 : 0.0, li, hf, vn, tn, bn);
+      if (hf == 0) {
+        rout.v[li] = vn;
+        const_cast<Refl &>(rin).tu[li] = tu;
+        if (FULL || li < ng) Rf[at(r1, L + li)] = (li == 0) ? bn : 0.0;
+      }
+      if (lane == 0) {
+        rout.tau = tn;
+        rout.beta = bn;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) e[q] = e[q] - tu * vk[q];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = hf + 2 * q;
+        if (FULL || (li < ng && k < L)) Rf[at(r1 + k, L + li - k)] = e[q];
+      }
+    }
+  } else if (role == 0) {
+    // the previous task's lower-block update, on this block (= that block):
+    // element (row i, column c) -= (tau u)_i v_c, as role 2 formed it
+    const Refl &rp = slots[(s - 1) % DKs];
+    const double vc = rp.v[li];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e[q] = e[q] - rp.tu[hf + 2 * q] * vc;
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q += 4) {
+      w0 += vk[q] * e[q];
+      w1 += vk[q + 1] * e[q + 1];
+      w2 += vk[q + 2] * e[q + 2];
+      w3 += vk[q + 3] * e[q + 3];
+    }
+    double wc = (w0 + w1) + (w2 + w3);
+    wc = hsum32(wc);
+    if ((FULL || li < nl) && lo + li != col) {
+      const int c = li;
+      double *Ac = Rf + at(lo + c, r1 - lo - c);
+      const double twc = tau * wc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = hf + 2 * q;
+        if (FULL || i < L) Ac[i] = e[q] - twc * vk[q];
+      }
+    }
+    store_refl(V2 + (int64_t(j) * smax + s) * SB_B, rin, lane);
+  } else {
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q += 4) {
+      p0 += e[q] * vk[q];
+      p1 += e[q + 1] * vk[q + 1];
+      p2 += e[q + 2] * vk[q + 2];
+      p3 += e[q + 3] * vk[q + 3];
+    }
+    double p = (p0 + p1) + (p2 + p3);
+    p = hsum32(p);
+    p *= tau;
+    const double pv = wsum(hf == 0 ? p * v : 0.0);
+    const double w = p - 0.5 * tau * pv * v;
+    if (hf == 0) W.ws[li] = w;
+    wave_sync();
+    double wk[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wk[q] = W.ws[hf + 2 * q];
+    double *tr = W.trash + lane;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = hf + 2 * q;
+      const bool ok = (FULL || li < L) && k <= li;
+      double *dst = ok ? Rf + at(r1 + k, li - k) : tr;
+      *dst = e[q] - v * wk[q] - w * vk[q];
+    }
+  }
+}
 
 struct DfSync {
   unsigned cnt[3][DG];  // [role][sweep]: tasks finished (role 2: + 1 for first_refl)
   unsigned loaded;      // columns [j0, loaded) are in the ring, final from the previous group
   unsigned wbs;         // columns below wbs are written back (their ring slots are free)
   unsigned dead;        // a wait gave up: nothing waits any more
+  unsigned ldone[DXF];  // chunks finished by each loader wave
+  unsigned wdone[DXF];  // write-back turns finished by each writer wave
+  unsigned wturn;       // turns posted by writer 0 (the others follow)
+  unsigned wrange[2][2];  // [turn & 1] = {lo, hi) of a posted turn
 };
 
 __device__ __forceinline__ unsigned lds_get(const unsigned *p) {
@@ -756,11 +929,13 @@ __device__ __forceinline__ void lds_put(unsigned *p, unsigned v) {
 }
 
 #if TG_BULGE_STATS
-#define DF_T0() const uint64_t tw0_ = __builtin_amdgcn_s_memrealtime();
-#define DF_WAITED() st_wait += __builtin_amdgcn_s_memrealtime() - tw0_;
+constexpr int DF_TR0 = 100;  // traced groups DF_TR0 .. DF_TR0 + 2
+#define DF_NOW() __builtin_amdgcn_s_memrealtime()
+#define DF_T0() uint64_t tw0_ = __builtin_amdgcn_s_memrealtime();
+#define DF_ACC(k) st[k] += __builtin_amdgcn_s_memrealtime() - tw0_, tw0_ = __builtin_amdgcn_s_memrealtime();
 #else
 #define DF_T0()
-#define DF_WAITED()
+#define DF_ACC(k)
 #endif
 
 // whole-wave wait until *p >= v (LDS word); false once the launch is dead
@@ -813,7 +988,10 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
   unsigned *stall = ctl + 2;
   unsigned *dummy = ctl + 4;
 #if TG_BULGE_STATS
-  uint64_t st_wait = 0, st_busy = 0, st_tasks = 0;
+  // per wave: [0] first wait kind, [1] second wait kind, [2] busy, [3] count
+  // (task waves: own reflector or slot / previous sweep or loader / task;
+  //  loader: producer watermark / ring space / load; writer: idle / drain / issue)
+  uint64_t st[4] = {0, 0, 0, 0};
   const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (tid == 0) {
@@ -882,57 +1060,68 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           } else {
             df_wait(&sy.loaded, unsigned(j + 1), sy, stall, timeout);
           }
-          DF_WAITED()
+          DF_ACC(1)
           first_refl(R, n, j, rfl[q][0]);
           lds_put(own, 1u);
         }
         for (int s = 0; s < nt; ++s) {
           const int r1 = j + 1 + s * SB_B;
-          {
-            DF_T0()
-            if (role != 2) df_wait(&sy.cnt[2][q], unsigned(s + 1), sy, stall, timeout);
-            if (role != 0) {
-              if (q == 0)
-                df_wait(&sy.loaded, unsigned(min(n, r1 + SB_B)), sy, stall, timeout);
-              else
-                need_prev(s + 2, role == 2);
-            }
-            if (role == 2 && s + 1 < nt && s + 2 - DK > 0) {
-              df_wait(&sy.cnt[0][q], unsigned(s + 2 - DK), sy, stall, timeout);
-              df_wait(&sy.cnt[1][q], unsigned(s + 2 - DK), sy, stall, timeout);
-            }
-            DF_WAITED()
+          DF_T0()
+          // the block's inputs: for role 0 the region of G(s-1) (what sweep
+          // q-1 must have finished for role 2's task s-1), else this task's
+          if (!(role == 0 && s == 0)) {
+            const int sp = role == 0 ? s - 1 : s;
+            if (q == 0)
+              df_wait(&sy.loaded, unsigned(min(n, j + 1 + (sp + 1) * SB_B)), sy, stall, timeout);
+            else
+              need_prev(sp + 2, role != 1);
           }
-#if TG_BULGE_STATS
-          const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
-#endif
+          DF_ACC(1)
+          auto wait_v = [&]() {
+            if (role != 2) {
+              df_wait(&sy.cnt[2][q], unsigned(s + 1), sy, stall, timeout);
+            } else if (s + 1 < nt) {
+              // the slot of v(s+1) held v(s+1-DK): read by A up to task s+2-DK
+              // (its tau u too), by D at task s+1-DK
+              if (s + 3 - DK > 0) df_wait(&sy.cnt[0][q], unsigned(s + 3 - DK), sy, stall, timeout);
+              if (s + 2 - DK > 0) df_wait(&sy.cnt[1][q], unsigned(s + 2 - DK), sy, stall, timeout);
+            }
+            DF_ACC(0)
+          };
           const bool nx = s + 1 < nt;
-          const Refl &ri = rfl[q][s % DK];
-          Refl &ro = rfl[q][(s + 1) % DK];
           if (r1 >= SB_B && r1 + 2 * SB_B <= n)
-            bulge_task_lds<true>(R, n, j, s, role, nx, V2, smax, wsc[wid], ri, ro);
+            df_task<true>(R, n, j, s, role, nx, V2, smax, wsc[wid], rfl[q], DK, wait_v);
           else
-            bulge_task_lds<false>(R, n, j, s, role, nx, V2, smax, wsc[wid], ri, ro);
+            df_task<false>(R, n, j, s, role, nx, V2, smax, wsc[wid], rfl[q], DK, wait_v);
           lds_put(own, unsigned(s + 1 + (role == 2)));
+          DF_ACC(2)
 #if TG_BULGE_STATS
-          st_busy += __builtin_amdgcn_s_memrealtime() - tb0;
-          ++st_tasks;
+          ++st[3];
+          if (stats && G >= DF_TR0 && G < DF_TR0 + 3 && s < 128 && wlane == 0)
+            stats[64 + ((G - DF_TR0) * 4 + role) * DG * 128 + q * 128 + s] =
+                __builtin_amdgcn_s_memrealtime();
 #endif
         }
       }
-    } else if (wid == DNCW) {
-      // loader: b columns at a time once the producer's watermark covers them
+    } else if (wid < DNCW + DXF) {
+      // loaders: b columns at a time once the producer's watermark covers them
       // and their ring slots are written back.  Chunks end at j0 + 1 + k b --
       // the columns task k - 1 of sweep 0 needs, and the watermarks the
       // producer's last sweep publishes -- after a first chunk of column j0
-      // alone (first_refl)
-      for (int ld = j0; ld < n;) {
-        const int ce = min(ld == j0 ? j0 + 1 : ld + SB_B, n);
+      // alone (first_refl).  Loader x takes chunks x, x + DXF, ... (each wave's
+      // poll -> load -> LDS round trip is latency, so DXF chunks are in
+      // flight at once); chunks are published in order.
+      const int x = wid - DNCW;
+      const int nch = n - j0 <= 1 ? 1 : 2 + (n - j0 - 2) / SB_B;  // chunks of the group
+      for (int k = x; k < nch; k += DXF) {
+        const int ld = k == 0 ? j0 : j0 + 1 + (k - 1) * SB_B;
+        const int ce = min(k == 0 ? j0 + 1 : ld + SB_B, n);
         DF_T0()
         if (G > 0 && !lds_get(&sy.dead) && !tg::spin_geq(prog + G - 1, unsigned(ce), stall, timeout))
           lds_put(&sy.dead, 1u);
+        DF_ACC(0)
         df_wait(&sy.wbs, unsigned(max(0, ce - RING)), sy, stall, timeout);
-        DF_WAITED()
+        DF_ACC(1)
         double2 buf[PL];
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
@@ -951,47 +1140,102 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
             R[rslot(c)][2 * h + 1] = buf[u].y;
           }
         }
+        if (DXF > 1) df_wait(&sy.loaded, unsigned(ld), sy, stall, timeout);  // in order
         lds_put(&sy.loaded, unsigned(ce));
-        ld = ce;
+        DF_ACC(2)
+#if TG_BULGE_STATS
+        ++st[3];
+        if (stats && G >= DF_TR0 && G < DF_TR0 + 3 && wlane == 0 && k < 128)
+          stats[64 + ((G - DF_TR0) * 4 + 3) * DG * 128 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
       }
     } else {
-      // writer: every column below the group's low watermark, then publish it
-      int wb = j0;
-      while (wb < n) {
-        int low = int(lds_get(&sy.loaded));
-        if (lds_get(&sy.dead)) low = n;
-        for (int q = 0; q < g; ++q)
-          low = min(low, df_low(n, j0 + q, lds_get(&sy.cnt[0][q]), lds_get(&sy.cnt[1][q]),
-                                lds_get(&sy.cnt[2][q])));
-        if (low <= wb) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+      // writers: every column below the group's low watermark, then publish it.
+      // Writer 0 decides each turn's range [lo, hi) and posts it; writer x
+      // stores the range's 1 KB blocks x, x + DXF, ...; the last to drain a
+      // turn publishes hi (turns publish in order: a writer publishes turn t
+      // only once every other writer has finished t, hence every earlier turn).
+      const int x = wid - DNCW - DXF;
+      DF_T0()
+      unsigned t = 0;
+      for (int hi = j0; hi < n; ++t) {
+        int lo = hi;
+        if (x == 0) {
+          int low;
+          while (true) {
+            low = int(lds_get(&sy.loaded));
+            if (lds_get(&sy.dead)) low = n;
+            for (int q = 0; q < g; ++q)
+              low = min(low, df_low(n, j0 + q, lds_get(&sy.cnt[0][q]), lds_get(&sy.cnt[1][q]),
+                                    lds_get(&sy.cnt[2][q])));
+            if (low > lo) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          hi = low;
+          if (DXF > 1) {
+            // the range slot of turn t held turn t - 2: every follower past it
+            if (t >= 2)
+              for (int y = 1; y < DXF; ++y) df_wait(&sy.wdone[y], t - 1, sy, stall, timeout);
+            sy.wrange[t & 1][0] = unsigned(lo);
+            sy.wrange[t & 1][1] = unsigned(hi);
+            lds_put(&sy.wturn, t + 1);
+          }
+        } else {
+          df_wait(&sy.wturn, t + 1, sy, stall, timeout);
+          lo = int(lds_get(&sy.wrange[t & 1][0]));
+          hi = int(lds_get(&sy.wrange[t & 1][1]));
+          if (lds_get(&sy.dead)) hi = max(hi, n);
         }
+        DF_ACC(0)
         asm volatile("" ::: "memory");
-        const int lim = (low - wb) * NTC;
-        for (int b0 = 0; b0 < lim; b0 += 64) {
-          const int idx = b0 + wlane;
-          if (idx < lim) {
-            const int c = wb + idx / NTC, h = idx % NTC;
-            const u32x2 lo2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h]);
-            const u32x2 hi2 = __builtin_bit_cast(u32x2, R[rslot(c)][2 * h + 1]);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
-                                                   (c * LDB + 2 * h) * 8, 0, 0);
+        // this writer's blocks of b columns at a time: LDS reads first, then the stores
+        constexpr int PX = PL / DXF;
+        for (int c0 = lo; c0 < hi; c0 += SB_B) {
+          const int lim = (min(c0 + SB_B, hi) - c0) * NTC;
+          double2 wv[PX];
+#pragma unroll
+          for (int u = 0; u < PX; ++u) {
+            const int idx = min(wlane + 64 * (x + DXF * u), lim - 1);
+            const int c = c0 + idx / NTC, h = idx % NTC;
+            wv[u] = *reinterpret_cast<const double2 *>(&R[rslot(c)][2 * h]);
+          }
+#pragma unroll
+          for (int u = 0; u < PX; ++u) {
+            const int idx = wlane + 64 * (x + DXF * u);
+            if (idx < lim) {
+              const int c = c0 + idx / NTC, h = idx % NTC;
+              const u32x2 lo2 = __builtin_bit_cast(u32x2, wv[u].x);
+              const u32x2 hi2 = __builtin_bit_cast(u32x2, wv[u].y);
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo2[0], lo2[1], hi2[0], hi2[1]}, rb,
+                                                     (c * LDB + 2 * h) * 8, 0, 0);
+            }
           }
         }
+        DF_ACC(2)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(low));
-        lds_put(&sy.wbs, unsigned(low));
-        wb = low;
+        bool last = true;
+        if (DXF > 1) {
+          lds_put(&sy.wdone[x], t + 1);
+#pragma unroll
+          for (int y = 0; y < DXF; ++y) last = last && lds_get(&sy.wdone[y]) >= t + 1;
+        }
+        if (last) {
+          publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(hi));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_max(&sy.wbs, unsigned(hi), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        DF_ACC(1)
+#if TG_BULGE_STATS
+        ++st[3];
+#endif
       }
     }
     __syncthreads();
   }
 #if TG_BULGE_STATS
   if (stats && wlane == 0) {
-    atomicAdd(stats + 8 + 3 * wid, (unsigned long long)st_wait);
-    atomicAdd(stats + 9 + 3 * wid, (unsigned long long)st_busy);
-    atomicAdd(stats + 10 + 3 * wid, (unsigned long long)st_tasks);
+    for (int k = 0; k < 4; ++k) atomicAdd(stats + 8 + 4 * wid + k, (unsigned long long)st[k]);
     if (wid == 0) {
       atomicAdd(stats + 0, 1ull);
       atomicAdd(stats + 5, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_t0));
@@ -1032,11 +1276,12 @@ int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 // prog + (n - 2)
 size_t sb2st_prog_words(int n) { return size_t(std::max(1, n - 2)) + 4 + 64; }
 
-// TG_BULGE_DF=1: the dataflow kernel (bulge_df_kernel); default the
-// step-synchronous kernel (bulge_lds_kernel)
+// TG_BULGE_DF=0: the step-synchronous kernel (bulge_lds_kernel); default the
+// dataflow kernel (bulge_df_kernel: bit-identical, 21.1 -> 19.0 ms at n =
+// 4096 and 80.8 -> 69.0 ms at n = 12,288 on MI355X)
 static bool bulge_dataflow() {
   const char *e = getenv("TG_BULGE_DF");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
@@ -1069,8 +1314,9 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (want) {
       if (TG_BULGE_STATS) {
-        (void)hipMalloc(&stats, 64 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(stats, 0, 64 * sizeof(unsigned long long), st);
+        const size_t ns = 64 + 3 * 4 * 4 * 128;
+        (void)hipMalloc(&stats, ns * sizeof(unsigned long long));
+        (void)hipMemsetAsync(stats, 0, ns * sizeof(unsigned long long), st);
       }
       (void)hipEventCreate(&e0);
       (void)hipEventCreate(&e1);
@@ -1124,15 +1370,40 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
       fprintf(stderr, "bulge: %.2f ms (%s, G_SW %d)\n", ms, df ? "dataflow" : "step", df ? DG : G_SW);
+#if TG_BULGE_STATS
+      if (stats && df && getenv("TG_BULGE_TRACE")) {
+        // role end times (us, relative) of tasks 0..15 of the traced groups
+        static unsigned long long tr[3 * 4 * DG * 128];
+        (void)hipMemcpy(tr, stats + 64, sizeof(tr), hipMemcpyDeviceToHost);
+        unsigned long long t0 = ~0ull;
+        for (auto x : tr) if (x && x < t0) t0 = x;
+        const char *rn[4] = {"A", "D", "G", "L"};
+        for (int gg = 0; gg < 3; ++gg)
+          for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < (r == 3 ? 1 : DG); ++q) {
+              fprintf(stderr, "  trace G%d %s%d:", DF_TR0 + gg, rn[r], q);
+              for (int t = 0; t < 16; ++t) {
+                const unsigned long long x = tr[(gg * 4 + r) * DG * 128 + q * 128 + t];
+                fprintf(stderr, " %6.2f", x ? (x - t0) / 100.0 : -1.0);
+              }
+              fprintf(stderr, "\n");
+            }
+      }
+#endif
       if (stats && df) {
-        fprintf(stderr, "  workers %llu, worker time %.1f us; per wave [wait us, busy us, tasks]:\n",
-                h[0], h[5] / 100.0 / double(h[0] ? h[0] : 1));
-        for (int w = 0; w < DNCW + 2; ++w)
-          fprintf(stderr, "   w%d %s: %.0f %.0f %llu (%.2f us/task)\n", w,
-                  w < DNCW ? (w % 3 == 0 ? "A" : w % 3 == 1 ? "D" : "G") : (w == DNCW ? "load" : "write"),
-                  h[8 + 3 * w] / 100.0 / double(h[0] ? h[0] : 1),
-                  h[9 + 3 * w] / 100.0 / double(h[0] ? h[0] : 1), h[10 + 3 * w],
-                  h[10 + 3 * w] ? h[9 + 3 * w] / 100.0 / double(h[10 + 3 * w]) : 0.0);
+        const double W = double(h[0] ? h[0] : 1);
+        fprintf(stderr, "  workers %llu, worker time %.1f us; per wave and worker (us): "
+                "[wait1 wait2 busy] count, busy per unit\n"
+                "  (tasks: own refl/slot, prev sweep/loader; loader: producer, ring; "
+                "writer: idle, drain)\n", h[0], h[5] / 100.0 / W);
+        for (int w = 0; w < DNCW + 2 * DXF; ++w) {
+          const unsigned long long *x = h + 8 + 4 * w;
+          fprintf(stderr, "   w%d %s: %.0f %.0f %.0f  %llu  %.2f\n", w,
+                  w < DNCW ? (w % 3 == 0 ? "A" : w % 3 == 1 ? "D" : "G")
+                           : (w < DNCW + DXF ? "load" : "write"),
+                  x[0] / 100.0 / W, x[1] / 100.0 / W, x[2] / 100.0 / W, x[3],
+                  x[3] ? x[2] / 100.0 / double(x[3]) : 0.0);
+        }
         (void)hipFree(stats);
         stats = nullptr;
       }

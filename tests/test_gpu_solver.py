@@ -210,10 +210,13 @@ def test_end_to_end_golden(g, name, path, monkeypatch):
     assert mism <= 6e-4  # the reference's own Triton-vs-loop disagreement
 
 
-def test_bulge_stall_reported(lib, monkeypatch):
+@pytest.mark.parametrize("df", ["1", "0"])
+def test_bulge_stall_reported(lib, monkeypatch, df):
     """A bulge-chasing hand-off that times out (forced: timeout of 0 ticks)
     is an error of tg_eigh_values, with NaN-poisoned eigenvalues, not a
-    silently wrong tridiagonal form; the next call is clean again."""
+    silently wrong tridiagonal form; the next call is clean again.  Both the
+    dataflow kernel (default) and the step-synchronous one (TG_BULGE_DF=0)."""
+    monkeypatch.setenv("TG_BULGE_DF", df)
     H = eig_problem("wishart", 1024, 3)
     n = H.shape[0]
     ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), DEV)
