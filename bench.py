@@ -424,18 +424,20 @@ PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", 
 if not os.path.exists(PMC_FILE):  # until this round's profile is committed
     PMC_FILE = PMC_FILE.replace("r04", "r03")
 LATENCY_BOUND = {"bulge_chase", "tsqr_leaf"}
-BULGE_GSW, BULGE_LAG = 2, 2  # csrc/bulge.hip G_SW, LAG
+BULGE_DG = 2  # csrc/bulge.hip TG_BULGE_DF_GSW: sweeps per workgroup of the dataflow kernel
 
 
 def bulge_chain(n, avg_ms):
-    """The bulge pipeline's critical path: a group of G_SW
-    sweeps starts 4 + LAG (G_SW - 1) steps behind its predecessor (the
-    loader of step t - 1 waits for the producer's step t + 2 + LAG (G_SW - 1)
-    + 1), so one launch is about groups x that many dependent steps."""
-    groups = -(-(n - 2) // BULGE_GSW)
-    steps = groups * (4 + BULGE_LAG * (BULGE_GSW - 1))
-    return dict(dependent_steps=steps, us_per_step=round(avg_ms * 1e3 / steps, 3),
-                model="groups x (4 + LAG (G_SW - 1)) pipeline steps, G_SW = 2, LAG = 2")
+    """The bulge pipeline's critical path (Two-stage 2.): the
+    dataflow kernel's sweep groups of DG sweeps hand the band from one CU to
+    the next through L2, and group G + 1 trails group G by a fixed latency
+    (two task periods of the chain's pace + the L2 hand-off + one task per
+    sweep of the group), so one launch is about groups x that lag."""
+    groups = -(-(n - 2) // BULGE_DG)
+    return dict(dependent_groups=groups, sweeps=n - 2,
+                us_per_group=round(avg_ms * 1e3 / groups, 3),
+                us_per_sweep=round(avg_ms * 1e3 / (n - 2), 3),
+                model=f"groups of {BULGE_DG} sweeps chained through L2 hand-offs (dataflow kernel)")
 
 
 def pmc_traffic(cls, args):

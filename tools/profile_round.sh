@@ -11,7 +11,7 @@ set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/${1:-gpurun_out/prof}
-KRE="bulge_lds_kernel|syr2k_w|xm_kernel"
+KRE="bulge_df_kernel|bulge_lds_kernel|syr2k_w|xm_kernel"
 LRE="syr2k_w|xm_kernel|syrk_compact"
 mkdir -p "$OUT"
 cd "$R"
@@ -33,7 +33,7 @@ done
 first() { find "$1" -name "$2" | sort | sed -n 1p; }
 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$(first $OUT/pmc_FETCH_SIZE '*counter_collection.csv')" \
   "$(first $OUT/pmc_WRITE_SIZE '*counter_collection.csv')" "$(first $OUT/trace '*kernel_stats.csv')" \
-  bulge_chase=bulge_lds_kernel band_update=syr2k_w band_xm=xm_kernel
+  bulge_chase=bulge_df_kernel band_update=syr2k_w band_xm=xm_kernel
 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_n12288.json" "$(first $OUT/pmc12k_FETCH_SIZE '*counter_collection.csv')" \
   "$(first $OUT/pmc12k_WRITE_SIZE '*counter_collection.csv')" "$(first $OUT/trace12k '*kernel_stats.csv')" \
   band_update=syr2k_w band_xm=xm_kernel pivot_schur=syrk_compact
