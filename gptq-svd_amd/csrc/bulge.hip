@@ -991,7 +991,7 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
   // per wave: [0] first wait kind, [1] second wait kind, [2] busy, [3] count
   // (task waves: own reflector or slot / previous sweep or loader / task;
   //  loader: producer watermark / ring space / load; writer: idle / drain / issue)
-  uint64_t st[4] = {0, 0, 0, 0};
+  uint64_t st[6] = {0, 0, 0, 0, 0, 0};  // [5] = count
   const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (tid == 0) {
@@ -1096,9 +1096,9 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           lds_put(own, unsigned(s + 1 + (role == 2)));
           DF_ACC(2)
 #if TG_BULGE_STATS
-          ++st[3];
+          ++st[5];
           if (stats && G >= DF_TR0 && G < DF_TR0 + 3 && s < 128 && wlane == 0)
-            stats[64 + ((G - DF_TR0) * 4 + role) * DG * 128 + q * 128 + s] =
+            stats[128 + ((G - DF_TR0) * 4 + role) * DG * 128 + q * 128 + s] =
                 __builtin_amdgcn_s_memrealtime();
 #endif
         }
@@ -1131,22 +1131,25 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
                                 __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
         }
+#if TG_BULGE_STATS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        DF_ACC(2)
+#endif
+        // one 16-B LDS write per chunk (two 8-B halves were 4-way bank-conflicted:
+        // lanes 16 B apart, the column pair 512 B apart)
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
           const int idx = wlane + 64 * u;
           const int c = ld + idx / NTC, h = idx % NTC;
-          if (c < ce) {
-            R[rslot(c)][2 * h] = buf[u].x;
-            R[rslot(c)][2 * h + 1] = buf[u].y;
-          }
+          if (c < ce) *reinterpret_cast<double2 *>(&R[rslot(c)][2 * h]) = buf[u];
         }
         if (DXF > 1) df_wait(&sy.loaded, unsigned(ld), sy, stall, timeout);  // in order
         lds_put(&sy.loaded, unsigned(ce));
-        DF_ACC(2)
+        DF_ACC(3)
 #if TG_BULGE_STATS
-        ++st[3];
+        ++st[5];
         if (stats && G >= DF_TR0 && G < DF_TR0 + 3 && wlane == 0 && k < 128)
-          stats[64 + ((G - DF_TR0) * 4 + 3) * DG * 128 + k] = __builtin_amdgcn_s_memrealtime();
+          stats[128 + ((G - DF_TR0) * 4 + 3) * DG * 128 + k] = __builtin_amdgcn_s_memrealtime();
 #endif
       }
     } else {
@@ -1199,6 +1202,10 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
             const int c = c0 + idx / NTC, h = idx % NTC;
             wv[u] = *reinterpret_cast<const double2 *>(&R[rslot(c)][2 * h]);
           }
+#if TG_BULGE_STATS
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          DF_ACC(1)
+#endif
 #pragma unroll
           for (int u = 0; u < PX; ++u) {
             const int idx = wlane + 64 * (x + DXF * u);
@@ -1213,6 +1220,7 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
         }
         DF_ACC(2)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        DF_ACC(3)
         bool last = true;
         if (DXF > 1) {
           lds_put(&sy.wdone[x], t + 1);
@@ -1225,9 +1233,9 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           __hip_atomic_fetch_max(&sy.wbs, unsigned(hi), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        DF_ACC(1)
+        DF_ACC(4)
 #if TG_BULGE_STATS
-        ++st[3];
+        ++st[5];
 #endif
       }
     }
@@ -1235,7 +1243,7 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
   }
 #if TG_BULGE_STATS
   if (stats && wlane == 0) {
-    for (int k = 0; k < 4; ++k) atomicAdd(stats + 8 + 4 * wid + k, (unsigned long long)st[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(stats + 8 + 6 * wid + k, (unsigned long long)st[k]);
     if (wid == 0) {
       atomicAdd(stats + 0, 1ull);
       atomicAdd(stats + 5, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_t0));
@@ -1314,7 +1322,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (want) {
       if (TG_BULGE_STATS) {
-        const size_t ns = 64 + 3 * 4 * 4 * 128;
+        const size_t ns = 128 + 3 * 4 * 4 * 128;
         (void)hipMalloc(&stats, ns * sizeof(unsigned long long));
         (void)hipMemsetAsync(stats, 0, ns * sizeof(unsigned long long), st);
       }
@@ -1364,7 +1372,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
 #endif
     if (want) {
       (void)hipEventRecord(e1, st);
-      unsigned long long h[64] = {0};
+      unsigned long long h[128] = {0};
       if (stats) (void)hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st);
       (void)hipStreamSynchronize(st);
       float ms = 0.f;
@@ -1374,7 +1382,7 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       if (stats && df && getenv("TG_BULGE_TRACE")) {
         // role end times (us, relative) of tasks 0..15 of the traced groups
         static unsigned long long tr[3 * 4 * DG * 128];
-        (void)hipMemcpy(tr, stats + 64, sizeof(tr), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(tr, stats + 128, sizeof(tr), hipMemcpyDeviceToHost);
         unsigned long long t0 = ~0ull;
         for (auto x : tr) if (x && x < t0) t0 = x;
         const char *rn[4] = {"A", "D", "G", "L"};
@@ -1393,16 +1401,19 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       if (stats && df) {
         const double W = double(h[0] ? h[0] : 1);
         fprintf(stderr, "  workers %llu, worker time %.1f us; per wave and worker (us): "
-                "[wait1 wait2 busy] count, busy per unit\n"
-                "  (tasks: own refl/slot, prev sweep/loader; loader: producer, ring; "
-                "writer: idle, drain)\n", h[0], h[5] / 100.0 / W);
+                "[t0 t1 t2 t3 t4] count; per unit (us)\n"
+                "  (tasks: own refl/slot, prev sweep/loader, task; loader: producer, ring, "
+                "issue->data, LDS+publish; writer: idle, LDS read, store issue, drain, publish)\n",
+                h[0], h[5] / 100.0 / W);
         for (int w = 0; w < DNCW + 2 * DXF; ++w) {
-          const unsigned long long *x = h + 8 + 4 * w;
-          fprintf(stderr, "   w%d %s: %.0f %.0f %.0f  %llu  %.2f\n", w,
+          const unsigned long long *x = h + 8 + 6 * w;
+          const double c = double(x[5] ? x[5] : 1);
+          fprintf(stderr, "   w%d %s: %.0f %.0f %.0f %.0f %.0f  %llu;  %.2f %.2f %.2f %.2f %.2f\n", w,
                   w < DNCW ? (w % 3 == 0 ? "A" : w % 3 == 1 ? "D" : "G")
                            : (w < DNCW + DXF ? "load" : "write"),
-                  x[0] / 100.0 / W, x[1] / 100.0 / W, x[2] / 100.0 / W, x[3],
-                  x[3] ? x[2] / 100.0 / double(x[3]) : 0.0);
+                  x[0] / 100.0 / W, x[1] / 100.0 / W, x[2] / 100.0 / W, x[3] / 100.0 / W,
+                  x[4] / 100.0 / W, x[5], x[0] / 100.0 / c, x[1] / 100.0 / c, x[2] / 100.0 / c,
+                  x[3] / 100.0 / c, x[4] / 100.0 / c);
         }
         (void)hipFree(stats);
         stats = nullptr;
