@@ -929,7 +929,10 @@ __device__ __forceinline__ void lds_put(unsigned *p, unsigned v) {
 }
 
 #if TG_BULGE_STATS
-constexpr int DF_TR0 = 100;  // traced groups DF_TR0 .. DF_TR0 + 2
+#ifndef TG_BULGE_TR0
+#define TG_BULGE_TR0 100
+#endif
+constexpr int DF_TR0 = TG_BULGE_TR0;  // traced groups DF_TR0 .. DF_TR0 + 2
 #define DF_NOW() __builtin_amdgcn_s_memrealtime()
 #define DF_T0() uint64_t tw0_ = __builtin_amdgcn_s_memrealtime();
 #define DF_ACC(k) st[k] += __builtin_amdgcn_s_memrealtime() - tw0_, tw0_ = __builtin_amdgcn_s_memrealtime();
