@@ -290,8 +290,9 @@ def random_causal_lm(shape: str, layers: int, device, seed: int = 0):
 E2E_NOTE = ("random-init weights with the named model's dimensions and random token ids: a "
             "timing of every stage at production shape, not the reference's workload -- no "
             "PPL; the ranks k come out near n (random activations) where real models keep "
-            "fewer; calibration forwards stop at each group's first linear (the reference "
-            "runs the whole layer, quantize.py:139-148); the model stays resident in HBM "
+            "fewer; each layer's calibration forward runs once, group by group from "
+            "activations cached between the groups (the reference re-runs the whole layer "
+            "for every group, quantize.py:139-148); the model stays resident in HBM "
             "(the reference moves each layer CPU<->GPU, quantize.py:101, :250) and no "
             "per-batch cleanup()/synchronize (quantize.py:28-35, :148)")
 

@@ -39,6 +39,23 @@ def tiny_opt(seed):
     return OPTForCausalLM(cfg).float().eval()
 
 
+def tiny_decoder(kind, seed):
+    """Tiny random Llama / Qwen3 (the harness's staged layer path)."""
+    import transformers as tf
+    cls = {"llama": (tf.LlamaConfig, tf.LlamaForCausalLM),
+           "qwen3": (tf.Qwen3Config, tf.Qwen3ForCausalLM)}[kind]
+    cfg = cls[0](vocab_size=256, hidden_size=64, intermediate_size=192, num_hidden_layers=2,
+                 num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64,
+                 head_dim=16)
+    cfg._attn_implementation = "eager"
+    torch.manual_seed(seed)
+    return cls[1](cfg).float().eval()
+
+
+def tiny_model(kind, seed):
+    return tiny_opt(seed) if kind == "opt" else tiny_decoder(kind, seed)
+
+
 def _patch(harness, hs):
     """CPU stand-ins for the HIP solver calls; `hs` collects every group's H."""
     import sys
@@ -81,11 +98,11 @@ def _patch(harness, hs):
     harness.log_quantization_error = lambda *a, **k: None
 
 
-def _run(ids):
+def _run(ids, kind="opt"):
     import gptq_svd_amd.harness as harness
     hs = []
     _patch(harness, hs)
-    model = tiny_opt(5)
+    model = tiny_model(kind, 5)
     res = harness.quantize_model(model, ids, mode="eigh", w_bits=4, group_size=64, sym=False,
                                  eps=1e-3, threshold_method="energy", batch_size=2, device="cpu")
     W = {n: p.detach().clone().numpy() for n, p in model.named_parameters()
@@ -93,7 +110,7 @@ def _run(ids):
     return hs, res, W
 
 
-def _worker(rank, world, port, ids, out):
+def _worker(rank, world, port, ids, out, kind):
     torch.set_num_threads(1)
     import sys
     sys.path.insert(0, ROOT)
@@ -101,7 +118,7 @@ def _worker(rank, world, port, ids, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        hs, res, W = _run(ids)
+        hs, res, W = _run(ids, kind)
         out[rank] = dict(H=[h.numpy() for h in hs], W=W,
                          ranks=[s["rank"] for s in res["layer_stats"]])
         dist.barrier()
@@ -109,14 +126,16 @@ def _worker(rank, world, port, ids, out):
         dist.destroy_process_group()
 
 
-def test_token_sharded_harness_matches_single():
+@pytest.mark.parametrize("kind", ["opt", "llama"])
+def test_token_sharded_harness_matches_single(kind):
+    """OPT runs the generic per-group layer passes, Llama the staged ones."""
     torch.set_num_threads(2)
     gen = torch.Generator().manual_seed(9)
     ids = [torch.randint(0, 256, (1, 16), generator=gen) for _ in range(6)]
-    hs1, res1, W1 = _run(ids)
+    hs1, res1, W1 = _run(ids, kind)
     manager = mp.Manager()
     out = manager.dict()
-    mp.spawn(_worker, args=(2, _free_port(), ids, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), ids, out, kind), nprocs=2, join=True)
     r0, r1 = out[0], out[1]
     assert len(r0["H"]) == len(hs1) == 8  # 2 layers x 4 groups
     for a, b, c in zip(r0["H"], r1["H"], hs1):
@@ -153,6 +172,52 @@ def test_early_stop_matches_full_layer_passes():
         assert torch.equal(a, b)
     for n in w1:
         assert torch.equal(w1[n], w2[n]), n
+
+
+@pytest.mark.parametrize("kind", ["llama", "qwen3"])
+def test_staged_layers_match_generic(kind, monkeypatch):
+    """harness.quantize_model(staged=True) -- each group's calibration pass
+    starts from the previous group's cached activations -- accumulates the
+    same H, and produces the same weights and next-layer inputs, bit for bit,
+    as re-running every layer from its input per group (staged=False).  Five
+    sequences in batches of 2: a short last batch included."""
+    import gptq_svd_amd.harness as harness
+    for name in ("HessianAccumulator", "process_hessian_alt", "gptq_fwrd",
+                 "log_quantization_error"):
+        monkeypatch.setattr(harness, name, getattr(harness, name))
+    torch.set_num_threads(2)
+    gen = torch.Generator().manual_seed(6)
+    ids = [torch.randint(0, 256, (1, 16), generator=gen) for _ in range(5)]
+    assert harness._staged_layer(harness.get_layers(tiny_model(kind, 0))[0])
+    out = []
+    for staged in (True, False):
+        hs = []
+        _patch(harness, hs)
+        model = tiny_model(kind, 5)
+        res = harness.quantize_model(model, ids, mode="eigh", w_bits=4, group_size=32,
+                                     sym=False, eps=1e-3, threshold_method="energy",
+                                     batch_size=2, device="cpu", staged=staged)
+        with torch.no_grad():
+            logits = model(torch.cat(ids)).logits
+        out.append((hs, {n: p.detach().clone() for n, p in model.named_parameters()}, logits,
+                    [s["rank"] for s in res["layer_stats"]]))
+    (h1, w1, l1, r1), (h2, w2, l2, r2) = out
+    assert len(h1) == len(h2) == 8 and r1 == r2
+    for a, b in zip(h1, h2):
+        assert torch.equal(a, b)
+    for n in w1:
+        assert torch.equal(w1[n], w2[n]), n
+    assert torch.equal(l1, l2)
+
+
+def test_staged_layer_eligibility():
+    import gptq_svd_amd.harness as harness
+    assert not harness._staged_layer(harness.get_layers(tiny_opt(0))[0])
+    layer = harness.get_layers(tiny_decoder("llama", 0))[0]
+    assert harness._staged_layer(layer)
+    h = layer.mlp.register_forward_hook(lambda *a: None)
+    assert not harness._staged_layer(layer)  # a user hook would be skipped
+    h.remove()
 
 
 def _factor_worker(rank, world, port, out):

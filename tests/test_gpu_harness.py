@@ -97,3 +97,43 @@ def test_export_roundtrip(name, tmp_path, oracle_mod):
         assert name_mod + ".weight" not in tensors
     # non-quantised tensors travel unchanged
     assert torch.equal(tensors["model.embed_tokens.weight"], sd["model.embed_tokens.weight"].cpu())
+
+
+@pytest.mark.parametrize("shape", ["tiny", "llama3_8b"])
+def test_staged_matches_generic(shape):
+    """quantize_model's staged layer path (cached activations between the
+    groups, the default for Llama/Qwen decoder layers) against the generic
+    path (every group's calibration pass re-runs the layer from its input):
+    same ranks, same quantised weights and same model output, bit for bit,
+    on the GPU -- the tiny Qwen3 golden in f32 and one Llama-3-8B layer in
+    fp16 (8 x 1024 random tokens, a short last batch of 3)."""
+    import bench
+    from gptq_svd_amd import harness
+    out = []
+    for staged in (True, False):
+        if shape == "tiny":
+            d = load_golden(golden_names("h_")[0])
+            model = build(d)
+            ids = [torch.from_numpy(r[None]) for r in d["ids"]]
+            kw = dict(mode=str(d["mode"]), w_bits=int(d["bits"]), group_size=int(d["group"]),
+                      sym=bool(d["sym"]), eps=float(d["eps"]),
+                      threshold_method=str(d["method"]), batch_size=int(d["batch"]))
+        else:
+            torch.cuda.empty_cache()
+            model, gen = bench.random_causal_lm(shape, 1, DEV, seed=3)
+            t = torch.randint(0, model.config.vocab_size, (8, 1024), generator=gen, device=DEV)
+            ids = [t[i:i + 1].cpu() for i in range(8)]
+            kw = dict(mode="eigh", w_bits=4, group_size=128, sym=False, eps=1e-4,
+                      threshold_method="energy", batch_size=5)
+        assert harness._staged_layer(harness.get_layers(model)[0])
+        res = harness.quantize_model(model, ids, device=DEV, staged=staged, **kw)
+        with torch.no_grad():
+            y = model.model(torch.cat(ids[:2]).to(DEV)).last_hidden_state
+        w = {n: p.detach().clone() for n, p in model.named_parameters() if "layers" in n}
+        out.append(([s["rank"] for s in res["layer_stats"]], w, y))
+        del model
+    (r1, w1, y1), (r2, w2, y2) = out
+    assert r1 == r2
+    for n in w1:
+        assert torch.equal(w1[n], w2[n]), n
+    assert torch.equal(y1, y2)
