@@ -5,20 +5,23 @@
 // Work: rows x n^2 / 2 FMAs on the lower 128 x 128 tiles (mirrored).  The
 // inputs are exact in FP64, every product is formed and summed in FP64.
 //
-// Layout and schedule:
+// Layout and schedule (two kernels, same decomposition):
 //  * a workgroup (8 waves as 2 x 4, 64 x 32 per wave = 4 x 2 MFMA blocks;
-//    two workgroups per CU) owns one 128 x 128 tile of H at a time and streams the two 128-column
-//    strips of X it needs (tile row I, tile column J) in slabs of 32 rows;
-//  * X stays 16-bit in LDS: a strip slab is 128 columns x 32 rows, column
-//    major, 64 B per column, its four 16-B chunks (8 consecutive rows each)
-//    XOR-swizzled by the column's (c >> 2) & 3 so that the ds_read_b128
-//    fragment reads of a wave hit 64 distinct banks; lane group g = lane >> 4
-//    takes rows 8g..8g+7 of the slab, so one 16-B read holds the lane's
-//    operand for 8 consecutive MFMA steps (converted to FP64 in registers);
-//  * global loads are 16 B per lane (8 columns of one row), one slab ahead,
-//    written to LDS as row pairs (one ds_write_b32 per column);
+//    two workgroups per CU) owns one 128 x 128 tile of H at a time and
+//    streams the two 128-column strips of X it needs (tile row I, tile
+//    column J) in slabs of rows, global loads 16 B per lane (8 columns of
+//    one row) one slab ahead;
+//  * default, `syrk64l_kernel`: each staged element is converted to FP64
+//    once and the slab (16 rows) is kept FP64 in LDS, pieces permuted per row
+//    for conflict-free writes and MFMA operand reads; 68.4 TF/s at n =
+//    12,288, 65.4 at 4096 (`tools/syrk_time.py`);
+//  * `syrk16_kernel` (TG_SYRK_LDS64=0): X stays 16-bit in LDS, column
+//    major, 32-row sub-slabs whose 16-B chunks are XOR-swizzled; one 16-B
+//    read holds a lane's operand for 8 MFMA steps and every wave converts
+//    its operands in registers (each A value in 4 waves, each B in 2):
+//    63.5 / 61.0 TF/s;
 //  * a persistent grid (CUs x 2 workgroups) takes work units from an atomic
-//    queue: whole tiles first, then the last round's tiles cut into four
+//    queue: whole tiles first, then the last round's tiles cut into NC = 8
 //    chunks of K; a whole tile is added to H directly, a chunk leaves a
 //    partial tile in the workspace and `syrk_fixup_kernel` adds a tile's
 //    chunks to H in chunk order -- the decomposition is static, so H is
@@ -37,6 +40,7 @@ namespace {
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef double doublex2 __attribute__((ext_vector_type(2)));
 
 constexpr int BT = 128;  // tile edge
 constexpr int KC = 32;   // rows of X per sub-slab (one LDS image)
@@ -82,6 +86,8 @@ __device__ inline void tile_of(int b, int &I, int &J) {
 // (t >> 4) & 15), columns cg * 8 .. cg * 8 + 7 (cg = t & 15).
 struct Stage {
   u32x4 v[2];  // [row]
+  bool ok[2];  // out-of-range rows / columns: a clamped load, zeroed at the store
+               // (a select right after the load would wait for it there)
   __device__ inline void load(const SyrkArgs &a, int c0A, int c0B, int64_t k0) {
     const int t = threadIdx.x, cg = t & 15, rp = (t >> 4) & 15, sp = t >> 8;
     const int c = (sp == 0 ? c0A : c0B) + cg * 8;
@@ -89,11 +95,10 @@ struct Stage {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int64_t k = k0 + 2 * rp + r;
-      const bool ok = cok && k < a.rows;
-      const int64_t kc = ok ? k : 0;
-      const int cc = ok ? c : 0;
-      u32x4 x = *reinterpret_cast<const u32x4 *>(a.X + kc * a.ldx + cc);
-      v[r] = ok ? x : u32x4{0u, 0u, 0u, 0u};
+      ok[r] = cok && k < a.rows;
+      const int64_t kc = ok[r] ? k : 0;
+      const int cc = ok[r] ? c : 0;
+      v[r] = *reinterpret_cast<const u32x4 *>(a.X + kc * a.ldx + cc);
     }
   }
   // registers -> LDS: column c, rows 2rp, 2rp+1 as one 4-byte word
@@ -104,8 +109,8 @@ struct Stage {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = cg * 8 + j;
-      const unsigned lo = (v[0][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-      const unsigned hi = (v[1][j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+      const unsigned lo = ok[0] ? (v[0][j >> 1] >> ((j & 1) * 16)) & 0xffffu : 0u;
+      const unsigned hi = ok[1] ? (v[1][j >> 1] >> ((j & 1) * 16)) & 0xffffu : 0u;
       *reinterpret_cast<unsigned *>(S + c * KC + ((q ^ swz(c)) << 3) + kin) = lo | (hi << 16);
     }
   }
@@ -267,6 +272,151 @@ __global__ __launch_bounds__(NT, 4) void syrk16_kernel(SyrkArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// FP64-in-LDS variant (TG_SYRK_LDS64=1): every element of X is converted to
+// FP64 once, by the thread that stages it, instead of once per wave that
+// reads it (the 16-bit form converts each A operand in 4 waves and each B
+// operand in 2: 768 conversions per row of a tile against 256).  A slab is
+// 16 rows of both strips, row-major FP64 (2 x 16 x 128 x 8 B = 32 KB, two
+// stages = 64 KB per workgroup, two workgroups per CU), its pieces permuted
+// within each row (lpos) so that staging writes and MFMA operand reads are
+// free of bank conflicts.  Same units, queue and fix-up as the
+// 16-bit kernel; H agrees with it to FP64 rounding (every product is exact,
+// only the grouping of rows into MFMA k-steps differs), deterministic.
+constexpr int KL = 16;  // rows per slab
+
+// Column c of slab row r: 16-B piece P = c / 2 of the row goes to piece
+// P ^ ((P >> 4) & 3) ^ 8(r & 1).  The first term spreads a staging write
+// (16 lanes, piece q of columns 8cg .. 8cg + 7 each) over all 64 banks; the
+// second puts the odd row of a ds_read_b64 pass in the other bank half.
+// Both permute pieces within aligned groups of 8, so a wave's 16 consecutive
+// columns of a row still cover 32 distinct banks.
+__device__ inline int lpos(int r, int c) {
+  const int P = c >> 1;
+  return r * BT + 2 * (P ^ ((P >> 4) & 3) ^ ((r & 1) << 3)) + (c & 1);
+}
+
+struct Stage64 {
+  u32x4 v;  // 8 16-bit values: row (t >> 4) & 15, columns (t & 15) * 8 .. + 7 of strip t >> 8
+  bool ok;  // rows past the end / columns past n: a clamped load, zeroed at the store
+  __device__ inline void load(const SyrkArgs &a, int c0A, int c0B, int64_t k0) {
+    const int t = threadIdx.x, cg = t & 15, r = (t >> 4) & 15, sp = t >> 8;
+    const int c = (sp == 0 ? c0A : c0B) + cg * 8;
+    const int64_t k = k0 + r;
+    ok = c < a.n && k < a.rows;
+    v = *reinterpret_cast<const u32x4 *>(a.X + (ok ? k : 0) * a.ldx + (ok ? c : 0));
+  }
+  template <bool BF16>
+  __device__ inline void store(double *S) const {  // S: [strip][KL][BT]
+    const int t = threadIdx.x, cg = t & 15, r = (t >> 4) & 15, sp = t >> 8;
+    double *p = S + sp * (KL * BT);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned w = ok ? v[q] : 0u;
+      doublex2 d{h2d<BF16>(w & 0xffffu), h2d<BF16>(w >> 16)};
+      *reinterpret_cast<doublex2 *>(p + lpos(r, cg * 8 + 2 * q)) = d;
+    }
+  }
+};
+
+template <bool BF16>
+__global__ __launch_bounds__(NT, 4) void syrk64l_kernel(SyrkArgs a) {
+  __shared__ __attribute__((aligned(16))) double S[2][2 * KL * BT];  // [stage][strip][row][col]
+  __shared__ unsigned s_unit;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wm = wv >> 2, wn = wv & 3, g = lane >> 4, l16 = lane & 15;
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) s_unit = atomicAdd(a.next, 1u);
+    __syncthreads();
+    const int u = int(s_unit);
+    if (u >= a.U) break;
+    int t, s0, s1, slot = -1;
+    if (u < a.head) {
+      t = u, s0 = 0, s1 = a.NS;
+    } else {
+      const int v = u - a.head, c = v / a.Tt, i = v - c * a.Tt;
+      t = a.head + i;
+      s0 = c * a.CK;
+      s1 = min(a.NS, s0 + a.CK);
+      slot = i * a.NC + c;
+    }
+    int I, J;
+    tile_of(t, I, J);
+    const int tm = I * BT, tn = J * BT;
+    doublex4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+    Stage64 st;
+    st.load(a, tm, tn, int64_t(s0) * KL);
+    st.store<BF16>(S[0]);
+    if (s0 + 1 < s1) st.load(a, tm, tn, int64_t(s0 + 1) * KL);
+    __syncthreads();
+    auto slab = [&]<int CUR>(std::integral_constant<int, CUR>, int s) __attribute__((always_inline)) {
+      const double *SA = S[CUR], *SB = S[CUR] + KL * BT;
+      // one k-step's operands at a time, a schedule barrier after its MFMAs:
+      // the other three waves of the SIMD cover the read latency, and the
+      // compiler cannot hoist the slab's reads (which spilled at the
+      // 128-register cap of four waves per SIMD)
+#pragma unroll
+      for (int kk = 0; kk < KL / 4; ++kk) {
+        const int r = 4 * kk + g;
+        double av[FI], bv[FJ];
+#pragma unroll
+        for (int i = 0; i < FI; ++i) av[i] = SA[lpos(r, wm * 64 + i * 16 + l16)];
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) bv[j] = SB[lpos(r, wn * 32 + j * 16 + l16)];
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (s + 1 < s1) {
+        st.store<BF16>(S[CUR ^ 1]);
+        if (s + 2 < s1) st.load(a, tm, tn, int64_t(s + 2) * KL);
+      }
+      __syncthreads();
+    };
+    for (int s = s0; s < s1; s += 2) {
+      slab(std::integral_constant<int, 0>{}, s);
+      if (s + 1 < s1) slab(std::integral_constant<int, 1>{}, s + 1);
+    }
+    if (slot < 0) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int gi = tm + wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
+            const int gj = tn + wn * 32 + j * 16 + (lane & 15);
+            if (gi < a.n && gj < a.n) {
+              double *p = a.H + int64_t(gi) * a.ldh + gj;
+              const double v = *p + acc[i][j][rr];
+              *p = v;
+              if (I != J) a.H[int64_t(gj) * a.ldh + gi] = v;
+            }
+          }
+    } else {
+      double *P = a.piece + int64_t(slot) * (BT * BT);
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int li = wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
+            const int lj = wn * 32 + j * 16 + (lane & 15);
+            P[li * BT + lj] = acc[i][j][rr];
+          }
+    }
+  }
+}
+
 // Tail tiles: H += their chunks' partial tiles in chunk order, mirrored.
 __global__ __launch_bounds__(NT) void syrk_fixup_kernel(SyrkArgs a) {
   const int i = blockIdx.x, t = a.head + i;
@@ -307,7 +457,7 @@ int resident_groups() {
 
 namespace tg {
 
-constexpr int NCMAX = 4;  // chunks per tail tile (G tail tiles)
+constexpr int NCMAX = 8;  // chunks per tail tile (G tail tiles); TG_SYRK_NC picks 1..NCMAX, default 8
 
 // tail tiles cut into chunks: the last min(T, G) of the T lower tiles
 static int syrk16_tail_tiles(int n) {
@@ -330,10 +480,11 @@ bool syrk16_supported(const void *X, int n, int64_t ldx) {
 // is one unit; units are handed out by an atomic queue, so a workgroup that
 // runs faster (the older of the two on a CU wins the issue arbitration: with
 // equal static shares their times differed by up to 1.8x, TG_SYRK_STAMPS)
-// simply takes more of them, and the last round is made of quarter tiles.
-// (Eighth tiles over the last G / 2 tiles measured slower at n = 4096, 24.8
-// against 19.8 ms: the whole tiles then handed to the slower workgroups of
-// the first round finish last.)
+// simply takes more of them, and the last round is made of eighth tiles
+// (quarters: 62.4 TF/s at n = 4096, eighths 65.4; n = 12,288 alike).
+// (Eighth tiles over only the last G / 2 tiles measured slower at n = 4096,
+// 24.8 against 19.8 ms: the whole tiles then handed to the slower workgroups
+// of the first round finish last.)
 hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n, int64_t ldx,
                   double *H, int64_t ldh, void *ws) {
   SyrkArgs a{};
@@ -345,11 +496,16 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   a.ldh = ldh;
   const int nt = cdiv(n, BT);
   a.T = nt * (nt + 1) / 2;
-  a.NS = cdiv(rows, NSUB * KC);
+  // development switch (read per call): the FP64-in-LDS kernel
+  const char *l64 = getenv("TG_SYRK_LDS64");
+  const bool lds64 = !(l64 && l64[0] == '0');
+  a.NS = cdiv(rows, lds64 ? KL : NSUB * KC);
   const int G = resident_groups();
   a.Tt = syrk16_tail_tiles(n);
   a.head = a.T - a.Tt;
-  a.NC = std::min(NCMAX, a.NS);
+  const char *ncs = getenv("TG_SYRK_NC");  // development switch (read per call)
+  const int nc = ncs ? std::max(1, std::min(NCMAX, atoi(ncs))) : 8;
+  a.NC = std::min(nc, a.NS);
   a.CK = cdiv(a.NS, a.NC);
   a.U = a.head + a.Tt * a.NC;
   a.piece = static_cast<double *>(ws);
@@ -361,7 +517,11 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   hipError_t e = hipMemsetAsync(a.next, 0, sizeof(unsigned), st);
   if (e != hipSuccess) return e;
   const int grid = std::min(G, a.U);
-  if (bf16)
+  if (lds64 && bf16)
+    hipLaunchKernelGGL(syrk64l_kernel<true>, dim3(grid), dim3(NT), 0, st, a);
+  else if (lds64)
+    hipLaunchKernelGGL(syrk64l_kernel<false>, dim3(grid), dim3(NT), 0, st, a);
+  else if (bf16)
     hipLaunchKernelGGL(syrk16_kernel<true>, dim3(grid), dim3(NT), 0, st, a);
   else
     hipLaunchKernelGGL(syrk16_kernel<false>, dim3(grid), dim3(NT), 0, st, a);

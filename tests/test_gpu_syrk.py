@@ -6,13 +6,20 @@ the oracle is the FP64 summation order: rel. Frobenius <= 1e-14.  Cases: the
 bench / real-model widths, widths that are not a multiple of the 128 tile,
 row counts that are not a multiple of the 32-row slab, one row, a stream-K
 split with many partial tiles (rows >> tiles), bf16, repeated accumulation,
-and the fallbacks (n % 8 != 0, a strided view)."""
+and the fallbacks (n % 8 != 0, a strided view).  Both kernels: X converted to
+FP64 at staging (default) and X 16-bit in LDS (TG_SYRK_LDS64=0)."""
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
+
+
+@pytest.fixture(params=["lds16", "lds64"])
+def kernel(request, monkeypatch):
+    monkeypatch.setenv("TG_SYRK_LDS64", "1" if request.param == "lds64" else "0")
+    return request.param
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +44,7 @@ def rel(a, b):
     (256, 384, torch.float16), (4096, 3072, torch.float16), (1000, 65, torch.bfloat16),
     (1032, 1, torch.float16), (128, 100_000, torch.float16), (2056, 2085, torch.bfloat16),
     (768, 4096, torch.float16)])
-def test_syrk16_matches_fp64(g, n, rows, dtype):
+def test_syrk16_matches_fp64(g, kernel, n, rows, dtype):
     gen = torch.Generator().manual_seed(n + rows)
     X = (torch.randn(rows, n, generator=gen) * 3).to(dtype)
     acc = g.HessianAccumulator(n, DEV)
@@ -48,7 +55,7 @@ def test_syrk16_matches_fp64(g, n, rows, dtype):
     assert np.array_equal(H, H.T), "both triangles must be written, mirrored exactly"
 
 
-def test_syrk16_repeated_and_deterministic(g):
+def test_syrk16_repeated_and_deterministic(g, kernel):
     n = 1536
     gen = torch.Generator().manual_seed(3)
     xs = [torch.randn(777, n, generator=gen).half() for _ in range(3)]
@@ -64,7 +71,7 @@ def test_syrk16_repeated_and_deterministic(g):
     assert rel(hs[0], R) <= 1e-14
 
 
-def test_syrk16_vs_generic_kernel(g):
+def test_syrk16_vs_generic_kernel(g, kernel):
     """The workspace path and the generic FP64 GEMM path agree to rounding."""
     from gptq_svd_amd import _lib
     n, rows = 2048, 4099
