@@ -37,5 +37,7 @@ python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$(first $OUT/pmc_FETCH_SIZ
 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_n12288.json" "$(first $OUT/pmc12k_FETCH_SIZE '*counter_collection.csv')" \
   "$(first $OUT/pmc12k_WRITE_SIZE '*counter_collection.csv')" "$(first $OUT/trace12k '*kernel_stats.csv')" \
   band_update=syr2k_w band_xm=xm_kernel pivot_schur=syrk_compact
-timeout -k 10 900 python3 bench.py > "$OUT/bench.log" 2>&1
-tail -c 3000 "$OUT/bench.log"
+if [ -z "$SKIP_BENCH" ]; then  # SKIP_BENCH=1: profiles only
+  timeout -k 10 900 python3 bench.py > "$OUT/bench.log" 2>&1
+  tail -c 3000 "$OUT/bench.log"
+fi
