@@ -694,7 +694,7 @@ __global__ __launch_bounds__(256) void syr2k_bs_kernel(double *__restrict__ A, i
 // M = Tᵀ (Yᵀ X) -- replaces the split-K GEMM over 256-row blocks of A22ᵀ,
 // its partial sum and the separate M reduction (three launches).
 // One workgroup per XR rows of X, XW waves splitting K (interleaved steps),
-// each accumulating a 16 x 32 tile on FP64 MFMA with XDA steps of loads in
+// each accumulating a 16 x 32 tile on FP64 MFMA with DA steps of loads in
 // flight; the XW tiles are summed in wave order.  Yᵀ X partials: per
 // workgroup, then per group of XG workgroups by its last arriver, then (more
 // than one group) over the groups by the last group -- fixed orders, so the
@@ -729,25 +729,78 @@ __host__ __device__ inline int xm_np(const XmArgs &g) { return g.Ya ? 5 : 1; }
 // YT[k + l/16][16 i + l%16], 128 B of an L2-resident row.  All workgroups
 // sweep K in the same order, so at any moment they read neighbouring strips
 // of the same rows of A22.
-constexpr int XDA = 8;  // K steps (4 rows of A22 each) loaded per round per wave
 // NBC 16-column blocks per workgroup (XR = 16 NBC rows of X): the YT
 // fragments of a step feed all NBC blocks, so YT's L2 -> CU traffic is
 // 16 m^2 / NBC bytes per panel against A22's 8 m^2.  NBC = 2 once the grid
 // still covers the chip (m >= XM_WIDE).
 constexpr int XM_WIDE = 6144;
+// TG_XM_PACK (build-time, NBC = 2): a lane's two A22 values are adjacent
+// columns (r0 + 2j, r0 + 2j + 1) and its two YT values adjacent YT columns
+// (2j, 2j + 1), one 16-byte load each -- two load instructions per step
+// instead of four, the same bytes.  MFMA block c then holds the columns of
+// parity c and block i the YT columns of parity i; the products, their k
+// order and so every X entry are unchanged, only where they land in the
+// accumulators (the reduction's LDS image is written accordingly).
+#ifndef TG_XM_PACK
+#define TG_XM_PACK 0
+#endif
+#ifndef TG_XM_DA2
+#define TG_XM_DA2 6
+#endif
+#ifndef TG_XM_MINW2
+#define TG_XM_MINW2 4
+#endif
+// NBC = 1: TG_XM_PACK1 packs the two YT values (the single A22 value stays
+// one 8-byte load), TG_XM_DA1 steps in flight
+#ifndef TG_XM_PACK1
+#define TG_XM_PACK1 0
+#endif
+#ifndef TG_XM_DA1
+#define TG_XM_DA1 8
+#endif
+template <int NBC>
+constexpr bool xm_pack() { return NBC == 2 && TG_XM_PACK; }
+template <int NBC>
+constexpr bool xm_pack_yt() { return NBC == 2 ? TG_XM_PACK : TG_XM_PACK1; }
+typedef double xm_d2 __attribute__((ext_vector_type(2)));
 template <int NBC>
 struct XmStep {
-  double b[NBC], a[2];
+  double b[NBC];
+  xm_d2 ap;  // YT values (a[0], a[1])
 };
+template <>
+struct XmStep<2> {
+  xm_d2 bp, ap;  // packed: (b[0], b[1]), (a[0], a[1]) -- or unpacked, element-wise
+};
+template <int NBC>
+__device__ __forceinline__ double xm_b(const XmStep<NBC> &f, int c) { return f.b[c]; }
+template <>
+__device__ __forceinline__ double xm_b<2>(const XmStep<2> &f, int c) { return f.bp[c]; }
+template <int NBC>
+__device__ __forceinline__ double xm_a(const XmStep<NBC> &f, int i) { return f.ap[i]; }
 template <int NBC>
 __device__ __forceinline__ void xm_load(const XmArgs &g, const int (&col)[NBC], int k0,
                                         XmStep<NBC> &f) {
   const int lane = threadIdx.x & 63;
   const int k = min(k0 + (lane >> 4), g.m - 1);
+  if constexpr (xm_pack<NBC>()) {  // col[0] = the pair's first column
+    f.bp = *reinterpret_cast<const xm_d2 *>(g.A + int64_t(k) * g.lda + col[0]);
+    f.ap = *reinterpret_cast<const xm_d2 *>(g.YT + int64_t(k) * SB_B + 2 * (lane & 15));
+  } else if constexpr (NBC == 2) {
+    f.bp[0] = g.A[int64_t(k) * g.lda + col[0]];
+    f.bp[1] = g.A[int64_t(k) * g.lda + col[1]];
+    f.ap[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
+    f.ap[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
+  } else {
 #pragma unroll
-  for (int c = 0; c < NBC; ++c) f.b[c] = g.A[int64_t(k) * g.lda + col[c]];
-  f.a[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
-  f.a[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
+    for (int c = 0; c < NBC; ++c) f.b[c] = g.A[int64_t(k) * g.lda + col[c]];
+    if constexpr (xm_pack_yt<NBC>()) {
+      f.ap = *reinterpret_cast<const xm_d2 *>(g.YT + int64_t(k) * SB_B + 2 * (lane & 15));
+    } else {
+      f.ap[0] = g.YT[int64_t(k) * SB_B + (lane & 15)];
+      f.ap[1] = g.YT[int64_t(k) * SB_B + 16 + (lane & 15)];
+    }
+  }
 }
 // The same loads as inline asm, with the waits written out (TG_XM_ASM, the
 // default): with the compiler's loads the K loop's back edge carried DA
@@ -763,34 +816,59 @@ __device__ __forceinline__ double xm_gload(const double *p) {
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
   return v;
 }
+__device__ __forceinline__ xm_d2 xm_gload2(const double *p) {
+  xm_d2 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
 template <int NBC>
 __device__ __forceinline__ void xm_load_asm(const XmArgs &g, const int (&col)[NBC], int k0,
                                             XmStep<NBC> &f) {
   const int lane = threadIdx.x & 63;
   const int k = min(k0 + (lane >> 4), g.m - 1);
+  if constexpr (xm_pack<NBC>()) {
+    f.bp = xm_gload2(g.A + int64_t(k) * g.lda + col[0]);
+    f.ap = xm_gload2(g.YT + int64_t(k) * SB_B + 2 * (lane & 15));
+  } else if constexpr (NBC == 2) {
+    f.bp[0] = xm_gload(g.A + int64_t(k) * g.lda + col[0]);
+    f.bp[1] = xm_gload(g.A + int64_t(k) * g.lda + col[1]);
+    const double *yt = g.YT + int64_t(k) * SB_B + (lane & 15);
+    f.ap[0] = xm_gload(yt);
+    f.ap[1] = xm_gload(yt + 16);
+  } else {
 #pragma unroll
-  for (int c = 0; c < NBC; ++c) f.b[c] = xm_gload(g.A + int64_t(k) * g.lda + col[c]);
-  const double *yt = g.YT + int64_t(k) * SB_B + (lane & 15);
-  f.a[0] = xm_gload(yt);
-  f.a[1] = xm_gload(yt + 16);
+    for (int c = 0; c < NBC; ++c) f.b[c] = xm_gload(g.A + int64_t(k) * g.lda + col[c]);
+    if constexpr (xm_pack_yt<NBC>()) {
+      f.ap = xm_gload2(g.YT + int64_t(k) * SB_B + 2 * (lane & 15));
+    } else {
+      const double *yt = g.YT + int64_t(k) * SB_B + (lane & 15);
+      f.ap[0] = xm_gload(yt);
+      f.ap[1] = xm_gload(yt + 16);
+    }
+  }
 }
+// load instructions per step slot
+template <int NBC>
+constexpr int xm_lps() { return xm_pack<NBC>() ? 2 : NBC + (xm_pack_yt<NBC>() ? 1 : 2); }
 // wait until step slot f's loads are in: the DA - 1 younger steps' loads
-// (NBC + 2 each) may stay outstanding
+// may stay outstanding
 template <int NBC, int DA>
 __device__ __forceinline__ void xm_wait_slot(XmStep<NBC> &f) {
-  static_assert((DA - 1) * (NBC + 2) == 20 || (DA - 1) * (NBC + 2) == 21, "xm wait count");
+  constexpr int W = (DA - 1) * xm_lps<NBC>();
+  static_assert(W <= 63, "xm wait count exceeds the vmcnt field");
   if constexpr (NBC == 2) {
-    asm volatile("s_waitcnt vmcnt(20)" : "+v"(f.b[0]), "+v"(f.b[1]), "+v"(f.a[0]), "+v"(f.a[1]));
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(f.bp[0]), "+v"(f.bp[1]), "+v"(f.ap[0]), "+v"(f.ap[1])
+                 : "n"(W));
   } else {
-    asm volatile("s_waitcnt vmcnt(21)" : "+v"(f.b[0]), "+v"(f.a[0]), "+v"(f.a[1]));
+    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(f.b[0]), "+v"(f.ap[0]), "+v"(f.ap[1]) : "n"(W));
   }
 }
 template <int NBC>
 __device__ __forceinline__ void xm_drain_slot(XmStep<NBC> &f) {
   if constexpr (NBC == 2) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.b[1]), "+v"(f.a[0]), "+v"(f.a[1]));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.bp[0]), "+v"(f.bp[1]), "+v"(f.ap[0]), "+v"(f.ap[1]));
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.a[0]), "+v"(f.a[1]));
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.ap[0]), "+v"(f.ap[1]));
   }
 }
 template <int NBC>
@@ -799,10 +877,10 @@ __device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[N
   const bool kok = k0 + ((threadIdx.x & 63) >> 4) < m;
 #pragma unroll
   for (int c = 0; c < NBC; ++c) {
-    const double b = (cok[c] && kok) ? f.b[c] : 0.0;
+    const double b = (cok[c] && kok) ? xm_b<NBC>(f, c) : 0.0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      acc[c][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[i], b, acc[c][i], 0, 0, 0);
+      acc[c][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(xm_a<NBC>(f, i), b, acc[c][i], 0, 0, 0);
   }
 }
 // sum over z in [z0, z1) of p[z * 1024 + e], in z order, with the L1-
@@ -829,9 +907,9 @@ __device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e,
 // (<= 80 KB of LDS), so one workgroup's reductions and ramp-up overlap the
 // other's stream; at 1 per CU the stream paused through both.
 template <int NBC>
-constexpr int xm_depth() { return NBC == 2 ? 6 : XDA; }
+constexpr int xm_depth() { return NBC == 2 ? TG_XM_DA2 : TG_XM_DA1; }
 template <int NBC>
-__global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g) {
+__global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel(XmArgs g) {
   constexpr int RB = XR * NBC;                // rows of X per workgroup
   constexpr int DA = xm_depth<NBC>();
   __shared__ double red[XW][RB][SB_B + 1];   // the last workgroup reuses it for C, T
@@ -856,9 +934,15 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
   bool cok[NBC];
 #pragma unroll
   for (int c = 0; c < NBC; ++c) {
-    const int col = r0 + 16 * c + (lane & 15);
-    cok[c] = col < g.m;
-    colc[c] = min(col, g.m - 1);
+    if constexpr (xm_pack<NBC>()) {  // columns r0 + 2j + c; colc[0]: the pair, inside A22
+      const int col = r0 + 2 * (lane & 15) + c;
+      cok[c] = col < g.m;
+      colc[c] = min(r0 + 2 * (lane & 15), g.m - 2);
+    } else {
+      const int col = r0 + 16 * c + (lane & 15);
+      cok[c] = col < g.m;
+      colc[c] = min(col, g.m - 1);
+    }
   }
   doublex4 acc[NBC][2];
 #pragma unroll
@@ -910,7 +994,12 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? 4 : 1) void xm_kernel(XmArgs g)
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        red[wid][16 * c + (lane & 15)][16 * i + (lane >> 4) + 4 * q] = acc[c][i][q];
+        if constexpr (xm_pack<NBC>())
+          red[wid][2 * (lane & 15) + c][2 * ((lane >> 4) + 4 * q) + i] = acc[c][i][q];
+        else if constexpr (xm_pack_yt<NBC>())
+          red[wid][16 * c + (lane & 15)][2 * ((lane >> 4) + 4 * q) + i] = acc[c][i][q];
+        else
+          red[wid][16 * c + (lane & 15)][16 * i + (lane >> 4) + 4 * q] = acc[c][i][q];
   __syncthreads();
   double xv[YPT];
 #pragma unroll

@@ -56,22 +56,29 @@ def _loop(nbc=1, da=2, wait=None, read_early=False, extra=None):
 
 def test_synthetic_safe_loop_passes():
     ins, da, wait = _loop()
-    assert cx.check_kernel("k", ins, 1, da, wait) == []
+    assert cx.check_kernel("k", ins, 1, da, 3, wait, {"global_load_dwordx2"}) == []
 
 
 def test_read_before_wait_is_caught():
     ins, da, wait = _loop(read_early=True)
-    errs = cx.check_kernel("k", ins, 1, da, wait)
+    errs = cx.check_kernel("k", ins, 1, da, 3, wait, {"global_load_dwordx2"})
     assert any("before its load's wait" in e for e in errs), errs
 
 
 def test_extra_memory_op_is_caught():
     ins, da, wait = _loop(extra=("scratch_store_dwordx2", ["off", "v[10:11]", "s0"]))
-    errs = cx.check_kernel("k", ins, 1, da, wait)
+    errs = cx.check_kernel("k", ins, 1, da, 3, wait, {"global_load_dwordx2"})
     assert any("unexpected vector-memory op" in e for e in errs), errs
 
 
 def test_too_loose_wait_is_caught():
     ins, da, _ = _loop(wait=3 * 2)   # waits that leave the slot's own loads in flight
-    errs = cx.check_kernel("k", ins, 1, da, 3 * 2)
+    errs = cx.check_kernel("k", ins, 1, da, 3, 3 * 2, {"global_load_dwordx2"})
     assert any("before its load's wait" in e for e in errs), errs
+
+
+def test_build_config_follows_the_source_defaults():
+    cfg = cx.build_config()
+    frag, da, lps, wait, lmn = cfg[2]
+    assert frag == "xm_kernelILi2E" and wait == (da - 1) * lps and 0 < wait <= 63
+    assert cfg[1][3] == (cfg[1][1] - 1) * 3

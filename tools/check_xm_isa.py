@@ -11,9 +11,11 @@ the gfx950 code object of build/band.o and, for xm_kernel<1> and <2>:
 
 * requires no scratch (private segment 0, no VGPR/SGPR spills) and no
   scratch / store / buffer instruction inside the K loop;
-* requires the loop body to hold exactly DA (NBC + 2) ``global_load_dwordx2``
-  and no other vector-memory instruction, and its waits to be the expected
-  ``vmcnt(20)`` (NBC = 2) / ``vmcnt(21)`` (NBC = 1);
+* requires the loop body to hold exactly DA x (loads per step) loads of the
+  build's kind (``global_load_dwordx2``; ``dwordx4`` for NBC = 2 with
+  TG_XM_PACK) and no other vector-memory instruction, and its waits to be
+  the expected ``vmcnt((DA - 1) x loads per step)`` -- the constants are read
+  from band.hip's defaults;
 * simulates the vector-memory counter in issue order (loads return in order
   for vmcnt) over the prologue's loads, two passes of the loop body and the
   loop exit, and fails on ANY instruction that reads or writes a register
@@ -31,10 +33,29 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 HERE = os.path.dirname(os.path.abspath(__file__))
 OBJ = os.path.join(HERE, "..", "gptq-svd_amd", "build", "band.o")
-KERNELS = {  # NBC -> (mangled-name fragment, DA, expected vmcnt of a slot wait)
-    2: ("xm_kernelILi2E", 6, 20),
-    1: ("xm_kernelILi1E", 8, 21),
-}
+SRC = os.path.join(HERE, "..", "gptq-svd_amd", "csrc", "band.hip")
+
+
+def build_config(src=SRC):
+    """The default build's X/M constants (band.hip's #define / constexpr):
+    NBC -> (mangled-name fragment, DA, loads per step, vmcnt of a slot wait,
+    load mnemonics)"""
+    text = open(src).read()
+
+    def define(name):
+        return int(re.search(rf"#define {name} (\d+)", text).group(1))
+    pack, da2 = define("TG_XM_PACK"), define("TG_XM_DA2")
+    pack1, da1 = define("TG_XM_PACK1"), define("TG_XM_DA1")
+    lps2, lps1 = (2 if pack else 4), (2 if pack1 else 3)
+    return {
+        2: ("xm_kernelILi2E", da2, lps2, (da2 - 1) * lps2,
+            {"global_load_dwordx4"} if pack else {"global_load_dwordx2"}),
+        1: ("xm_kernelILi1E", da1, lps1, (da1 - 1) * lps1,
+            {"global_load_dwordx2", "global_load_dwordx4"} if pack1 else {"global_load_dwordx2"}),
+    }
+
+
+KERNELS = build_config()
 VMEM = re.compile(r"^(global_|buffer_|flat_|scratch_)")
 REG = re.compile(r"^([va])(?:(\d+)|\[(\d+):(\d+)\])$")
 
@@ -107,7 +128,7 @@ def regs(op: str):
     return {(kind, r) for r in range(int(m.group(3)), int(m.group(4)) + 1)}
 
 
-def check_kernel(name, insns, nbc, da, wait):
+def check_kernel(name, insns, nbc, da, lps, wait, lmn):
     base = insns[0][0]
     off = [a - base for a, _, _, _ in insns]
     # the K loop: the backward branch whose body holds the slot waits
@@ -124,10 +145,10 @@ def check_kernel(name, insns, nbc, da, wait):
     j, i = loop
     body = insns[j:i + 1]
     errs = []
-    loads = [x for x in body if x[1] == "global_load_dwordx2"]
-    other = [x for x in body if VMEM.match(x[1]) and x[1] != "global_load_dwordx2"]
-    if len(loads) != da * (nbc + 2):
-        errs.append(f"{name}: {len(loads)} loads in the K loop, expected {da * (nbc + 2)}")
+    loads = [x for x in body if x[1] in lmn]
+    other = [x for x in body if VMEM.match(x[1]) and x[1] not in lmn]
+    if len(loads) != da * lps:
+        errs.append(f"{name}: {len(loads)} loads in the K loop, expected {da * lps}")
     for x in other:
         errs.append(f"{name}: unexpected vector-memory op in the K loop: {x[1]} {', '.join(x[2])}")
     waits = [" ".join(x[2]) for x in body if x[1] == "s_waitcnt" and "vmcnt" in " ".join(x[2])]
@@ -137,9 +158,9 @@ def check_kernel(name, insns, nbc, da, wait):
     # prologue: the DA (NBC + 2) loads before the loop head and what follows
     pro = j
     seen = 0
-    while pro > 0 and seen < da * (nbc + 2):
+    while pro > 0 and seen < da * lps:
         pro -= 1
-        if insns[pro][1] == "global_load_dwordx2":
+        if insns[pro][1] in lmn:
             seen += 1
     # exit: from the instruction after the back edge to the drain
     k = i + 1
@@ -157,12 +178,12 @@ def check_kernel(name, insns, nbc, da, wait):
         touched = set().union(*[regs(o) for o in ops]) if ops else set()
         pend = set().union(*q) if q else set()
         hit = touched & pend
-        if hit and mn != "global_load_dwordx2":
+        if hit and mn not in lmn:
             errs.append(f"{name}: {mn} {', '.join(ops)} at 0x{addr:x} touches "
                         f"{sorted(hit)[:4]} before its load's wait")
             break
         if VMEM.match(mn):
-            if mn == "global_load_dwordx2" and hit:
+            if mn in lmn and hit:
                 errs.append(f"{name}: load at 0x{addr:x} reuses a register with a load in flight")
                 break
             q.append(regs(ops[0]) if "load" in mn else set())
@@ -175,7 +196,7 @@ def main(obj=OBJ) -> int:
         meta = kernel_meta(co)
         funcs = disasm(co)
     errs = []
-    for nbc, (frag, da, wait) in KERNELS.items():
+    for nbc, (frag, da, lps, wait, lmn) in KERNELS.items():
         names = [n for n in funcs if frag in n]
         if len(names) != 1:
             errs.append(f"xm_kernel<{nbc}> not found exactly once ({names})")
@@ -187,7 +208,7 @@ def main(obj=OBJ) -> int:
                 errs.append(f"{name}: {key} = {md[key]} (the asm K loop requires none)")
         if any(m.startswith("scratch_") for _, m, _, _ in funcs[name]):
             errs.append(f"{name}: scratch instructions present")
-        errs += check_kernel(name, funcs[name], nbc, da, wait)
+        errs += check_kernel(name, funcs[name], nbc, da, lps, wait, lmn)
     if errs:
         print("check_xm_isa: FAILED\n  " + "\n  ".join(errs), file=sys.stderr)
         return 1
