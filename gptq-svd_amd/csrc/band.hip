@@ -742,7 +742,7 @@ constexpr int XM_WIDE = 6144;
 // order and so every X entry are unchanged, only where they land in the
 // accumulators (the reduction's LDS image is written accordingly).
 #ifndef TG_XM_PACK
-#define TG_XM_PACK 0
+#define TG_XM_PACK 1
 #endif
 #ifndef TG_XM_DA2
 #define TG_XM_DA2 6
@@ -1290,24 +1290,14 @@ __device__ __forceinline__ void syr2k_tile(int b, int &tm, int &tn) {
   tm = I * WT;
   tn = (b - I * (I + 1) / 2) * WT;
 }
-// xskip (look-ahead, TG_SB_LA): workgroups b with b % 8 == 0 -- the ones the
-// round-robin dispatch puts on XCD 0, where the next panel's QR runs
-// meanwhile (pqr.hip filters to the same XCD) -- exit at once, the others
-// take the tiles with a dense index.  Which workgroups skip changes only
-// where tiles run, not the tiles' values.
 template <int NP>
 __global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A, int64_t lda,
-                                                          int m, YW2 yw, int ntiles, int xskip) {
+                                                          int m, YW2 yw, int ntiles) {
   __shared__ double Aop[WK][WT + WP];
   __shared__ double Bop[WK][WT + WP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  int b = blockIdx.x, G = int(gridDim.x);
-  if (xskip) {
-    if (b % 8 == 0) return;
-    b = b - b / 8 - 1;
-    G = G - (G + 7) / 8;
-  }
+  int b = blockIdx.x;
   if (b >= ntiles) return;
   auto load_old = [&](int tb, double (&o)[2][2][4]) __attribute__((always_inline)) {
     int tm, tn;
@@ -1325,7 +1315,7 @@ __global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A
   };
   double old[2][2][4], nold[2][2][4];
   load_old(b, old);
-  for (; b < ntiles; b += G) {
+  for (; b < ntiles; b += gridDim.x) {
     int tm, tn;
     syr2k_tile(b, tm, tn);
     const int rl = tid >> 2, k0 = (tid & 3) * 8;
@@ -1352,7 +1342,7 @@ __global__ __launch_bounds__(256, 2) void syr2k_wp_kernel(double *__restrict__ A
       }
       if (pp == 0) {
         __builtin_amdgcn_sched_barrier(0);
-        const int bn = b + G;
+        const int bn = b + int(gridDim.x);
         if (bn < ntiles) load_old(bn, nold);  // in flight through this tile
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1710,7 +1700,11 @@ static hipError_t side_stream(SideStream *&out) {
 // with the next panel's QR on a side stream, +5 ms -- the QR's workgroups need
 // a whole CU's LDS and wait for the trailing update to drain; the same on
 // CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
-// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
+// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.  Round 5: the look-ahead
+// with the update's workgroups kept off the QR's XCD (b % 8 != 0, dense
+// tile index) does overlap the two, but the next panel's column update and
+// the cross-stream waits cost what the overlap saves: 59.11 vs 59.11 ms at
+// n = 4096, +2 ms at 12,288.)
 // X = A22 YT and M = T^T Y^T X in one launch (row blocks of A22)
 static int xm_nbc(int m) {
   const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
@@ -1750,7 +1744,11 @@ constexpr int PAIR_MIN_ALL = 256, PAIR_MIN = 6144;
 // with the next panel's QR on a side stream, +5 ms -- the QR's workgroups need
 // a whole CU's LDS and wait for the trailing update to drain; the same on
 // CU-masked streams, update kernels 1.3-2x slower; A22 kept as its lower
-// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.)
+// triangle, X 27 -> 35 us for syr2k 38 -> 35 us.  Round 5: the look-ahead
+// with the update's workgroups kept off the QR's XCD (b % 8 != 0, dense
+// tile index) does overlap the two, but the next panel's column update and
+// the cross-stream waits cost what the overlap saves: 59.11 vs 59.11 ms at
+// n = 4096, +2 ms at 12,288.)
 static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const SbPlan &pl,
                                const SbBufs &b) {
   TG_CHK(hipMemsetAsync(b.pq_ctl, 0, sizeof(unsigned) * pq_ctl_words(n), st));
@@ -1770,13 +1768,6 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
   const char *psd = getenv("TG_SB_PAIR_SIDE");
   const bool pair_side = psd && psd[0] == '1';
   double *Xa = b.X, *Xb = b.X + size_t(n) * SB_B;
-  // TG_SB_LA=1: look-ahead for single panels of >= TG_SB_LA_MIN rows
-  // (development switch, read per call)
-  const char *las = getenv("TG_SB_LA");
-  const bool la = las && las[0] == '1';
-  const char *lam = getenv("TG_SB_LA_MIN");
-  const int la_min = lam ? atoi(lam) : 512;
-  bool la_pending = false;
   for (int pi = 0; pi < np; ++pi) {
     const SbPanel &P = pl.panels[pi];
     const int m = P.m, r0 = P.r0;
@@ -1784,41 +1775,17 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
     TG_CHK(panel_qr(st, A, lda, P.p, P.r0, P.m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    if (la_pending) {  // the previous panel's update of this trailing matrix
-      TG_CHK(hipStreamWaitEvent(st, ss->ev1[1], 0));
-      la_pending = false;
-    }
     TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b));
     // W = X - Y M / 2 in place
     hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
     TG_CHK(hipGetLastError());
     const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= pair_min;
-    if (!pair && la && persist && pi + 1 < np && m >= la_min) {
-      // look-ahead: the next panel's columns get this panel's update now
-      // (panel_upd_kernel, as for panel pairs), the rest of A22 on the side
-      // stream beside the next panel's QR, on XCDs 1-7
-      hipLaunchKernelGGL(panel_upd_kernel, dim3(cdiv(m, SB_B)), dim3(256), 0, st, A22,
-                         int64_t(lda), m, Yp, Xa);
-      TG_CHK(hipGetLastError());
-      if (!ss) TG_CHK(side_stream(ss));
-      TG_CHK(hipEventRecord(ss->ev0[1], st));
-      TG_CHK(hipStreamWaitEvent(ss->s, ss->ev0[1], 0));
-      const int mr = m - SB_B, nt = cdiv(mr, WT), tiles = nt * (nt + 1) / 2;
-      const int grid = std::min(2 * ncu, cdiv(tiles * 8, 7) + 8);
-      hipLaunchKernelGGL(syr2k_wp_kernel<1>, dim3(grid), dim3(256), 0, ss->s,
-                         A22 + int64_t(SB_B) * lda + SB_B, int64_t(lda), mr,
-                         YW2{{Yp + SB_B * SB_B, nullptr}, {Xa + SB_B * SB_B, nullptr}}, tiles, 1);
-      TG_CHK(hipGetLastError());
-      TG_CHK(hipEventRecord(ss->ev1[1], ss->s));
-      la_pending = true;
-      continue;
-    }
     if (!pair) {  // A22 -= Y W^T + W Y^T
       const int nt = cdiv(m, WT), tiles = nt * (nt + 1) / 2;
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);
       if (persist)
         hipLaunchKernelGGL(syr2k_wp_kernel<1>, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st,
-                           A22, int64_t(lda), m, YW2{{Yp, nullptr}, {Xa, nullptr}}, tiles, 0);
+                           A22, int64_t(lda), m, YW2{{Yp, nullptr}, {Xa, nullptr}}, tiles);
       else
         hipLaunchKernelGGL(syr2k_w_kernel<1>, dim3(tiles), dim3(256), 0, st, A22, int64_t(lda), m,
                            YW2{{Yp, nullptr}, {Xa, nullptr}});
@@ -1865,7 +1832,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     const int tiles = nt * (nt + 1) / 2;
     if (persist)
       hipLaunchKernelGGL(syr2k_wp_kernel<2>, dim3(std::min(tiles, 2 * ncu)), dim3(256), 0, st,
-                         A22b, int64_t(lda), mb, YW2{{Ya, Yb}, {Wa, Xb}}, tiles, 0);
+                         A22b, int64_t(lda), mb, YW2{{Ya, Yb}, {Wa, Xb}}, tiles);
     else
       hipLaunchKernelGGL(syr2k_w_kernel<2>, dim3(tiles), dim3(256), 0, st, A22b, int64_t(lda), mb,
                          YW2{{Ya, Yb}, {Wa, Xb}});

@@ -61,8 +61,6 @@ def rel(a, b):
     {"TG_XM_NBC": "2"},
     {"TG_URX_SMALLM": "1"},
     {"TG_SCHUR_MIRROR": "1"},
-    {"TG_SB_LA": "1"},
-    {"TG_SB_LA": "1", "TG_SB_LA_MIN": "64"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
     {"TG_ORTH_MGS": "1"},
