@@ -737,6 +737,12 @@ constexpr int DNCW = 3 * DG;          // role waves
 #ifndef TG_BULGE_DF_XF
 #define TG_BULGE_DF_XF 1
 #endif
+// the loader issues a chunk's loads before it waits for ring space (the
+// space is needed only by the LDS write): n = 12,288 69.0 -> 68.4 ms, 4096
+// unchanged, bit-identical; 0 restores the old order
+#ifndef TG_BULGE_LD_EARLY
+#define TG_BULGE_LD_EARLY 1
+#endif
 constexpr int DXF = TG_BULGE_DF_XF;           // loader waves = writer waves (each moves 1/DXF)
 constexpr int DBT = 64 * (DNCW + 2 * DXF);    // + loaders + writers
 // ring span at the tightest spacing: the loader's chunk ahead of sweep 0
@@ -1123,7 +1129,9 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
         if (G > 0 && !lds_get(&sy.dead) && !tg::spin_geq(prog + G - 1, unsigned(ce), stall, timeout))
           lds_put(&sy.dead, 1u);
         DF_ACC(0)
+#if !TG_BULGE_LD_EARLY
         df_wait(&sy.wbs, unsigned(max(0, ce - RING)), sy, stall, timeout);
+#endif
         DF_ACC(1)
         double2 buf[PL];
 #pragma unroll
@@ -1134,6 +1142,11 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           buf[u] = make_double2(__builtin_bit_cast(double, u32x2{v4[0], v4[1]}),
                                 __builtin_bit_cast(double, u32x2{v4[2], v4[3]}));
         }
+#if TG_BULGE_LD_EARLY
+        // the ring space is needed only by the LDS write: the chunk's loads
+        // are in flight while the writer retires the slots
+        df_wait(&sy.wbs, unsigned(max(0, ce - RING)), sy, stall, timeout);
+#endif
 #if TG_BULGE_STATS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         DF_ACC(2)
