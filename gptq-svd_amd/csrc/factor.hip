@@ -2311,8 +2311,18 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
         TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, C, m, ZT, m, 1.0, Nm, k));  // + C V^T
       }
     } else {
-      TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));               // Yr = R11^-1
-      if (m > 0) TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));  // C
+      // C = R11^-1 R12 by block back substitution over 256-row blocks, as in
+      // the small-m form (k^2 m flops, no k^3 / 3 inverse: n = 12,288 at
+      // 3n/4 rank -14 ms); TG_URX_INV=1 (development switch, read per call)
+      // keeps the explicit inverse and its triangular product
+      const char *ui = getenv("TG_URX_INV");
+      if (ui && ui[0] == '1') {
+        TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));             // Yr = R11^-1
+        if (m > 0) TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));
+      } else if (m > 0) {
+        TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));         // 256-block inverses
+        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C)) return e;
+      }
       if (const int e = form_zt()) return e;
       TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
     }

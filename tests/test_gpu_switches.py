@@ -60,6 +60,7 @@ def rel(a, b):
     {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
     {"TG_URX_SMALLM": "1"},
+    {"TG_URX_INV": "1"},
     {"TG_SCHUR_MIRROR": "1"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
