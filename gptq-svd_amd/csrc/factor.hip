@@ -2285,11 +2285,26 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
     hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, Rx, ldr, k, Yr,
                        k);
     TG_LAUNCHED();
-    auto form_zt = [&]() -> int {  // Z^T = R11 + R12 C^T
+    auto form_zt = [&](bool scratch_free) -> int {  // Z^T = R11 + R12 C^T
       TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr,
                               sizeof(double) * k, k, hipMemcpyDeviceToDevice, st));
-      if (m > 0)
+      if (m <= 0) return 0;
+      // the DGEMM stages 16-byte vectors only from 16-byte-aligned rows: with
+      // an odd k (R12's rows start mid-vector) or an odd m (C's ld), copy both
+      // operands to even-ld buffers first (Y and Rq, when the caller says
+      // they are not live; n = 12,288 at 3n/4 rank, k = 9173: 13.7 -> ~9 ms)
+      const int mp = m + (m & 1);
+      const bool pad = scratch_free && ((k & 1) || (m & 1) || (ldr & 1)) && mp <= k;
+      if (pad) {
+        double *R12p = Yr, *Cp = Rq;
+        TG_HIP(hipMemcpy2DAsync(R12p, sizeof(double) * mp, Rx + k, sizeof(double) * ldr,
+                                sizeof(double) * m, k, hipMemcpyDeviceToDevice, st));
+        TG_HIP(hipMemcpy2DAsync(Cp, sizeof(double) * mp, C, sizeof(double) * m,
+                                sizeof(double) * m, k, hipMemcpyDeviceToDevice, st));
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, R12p, mp, Cp, mp, 1.0, ZT, k));
+      } else {
         TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));
+      }
       return 0;
     };
     if (small_m) {
@@ -2323,7 +2338,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
         TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));         // 256-block inverses
         if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C)) return e;
       }
-      if (const int e = form_zt()) return e;
+      if (const int e = form_zt(true)) return e;
       TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
     }
     hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, Rq);  // N' = J N J
@@ -2338,7 +2353,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
       double *Yq = Nm;
       TG_HIP(zero_lower(st, Rq, k, k));
       if (small_m) {  // ZT held V
-        if (const int e = form_zt()) return e;
+        if (const int e = form_zt(false)) return e;
       }
       hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, ZT, k, Yq);
       TG_LAUNCHED();

@@ -104,3 +104,27 @@ def test_small_m_u_factor_near_full_rank(monkeypatch):
     assert np.array_equal(got["perm"], ref["perm"])
     assert rel(got["R_x"], ref["R_x"]) == 0.0
     assert rel(got["U"], ref["U"]) <= 1e-10
+
+
+def test_explicit_u_factor_odd_widths(monkeypatch):
+    """The explicit-form U factor (m > k/16) with an odd rank and an odd
+    complement (k = 1001, m = 499: R12's rows and C's ld are not 16-byte
+    aligned, so Z's product runs on padded copies) against the explicit
+    inverse form (TG_URX_INV=1): perm and R_x identical, U to 1e-10.  n = 1536
+    (a whole number of 128-column groups), 1001 calibration rows."""
+    import gptq_svd_amd.gptq_utils as g
+    torch.manual_seed(8)
+    n, rows = 1536, 1001
+    acc = g.HessianAccumulator(n, DEV)
+    acc.add_batch(torch.randn(rows, n).half().to(DEV))
+    H = acc.get_hessian()
+    W = torch.randn(64, n, device=DEV)
+    monkeypatch.setenv("TG_SPECTRAL_PATH", "complement")
+    got = solve(g, H, W)
+    k = got["R_x"].shape[0]
+    assert k % 2 == 1 and (n - k) % 2 == 1 and (n - k) * 16 > k, k
+    monkeypatch.setenv("TG_URX_INV", "1")
+    ref = solve(g, H, W)
+    assert np.array_equal(got["perm"], ref["perm"])
+    assert rel(got["R_x"], ref["R_x"]) == 0.0
+    assert rel(got["U"], ref["U"]) <= 1e-10
