@@ -2237,16 +2237,16 @@ extern "C" size_t tg_ufactor_rx_workspace_size(int n, int k) {
 // explicit R11^-1's k^3 / 3 (the near-full-rank layers' m = n - k is tiny).
 constexpr int TB = 256;
 static int trsm_upper_blocks(hipStream_t st, const double *R, int ldr, int k, const double *B,
-                             int m, const double *Dinv, int ldd, double *Cw, double *C) {
-  TG_HIP(hipMemcpy2DAsync(Cw, sizeof(double) * m, B, sizeof(double) * ldr, sizeof(double) * m, k,
-                          hipMemcpyDeviceToDevice, st));
+                             int m, const double *Dinv, int ldd, double *Cw, double *C, int ldc) {
+  TG_HIP(hipMemcpy2DAsync(Cw, sizeof(double) * ldc, B, sizeof(double) * ldr, sizeof(double) * m,
+                          k, hipMemcpyDeviceToDevice, st));
   for (int bi = tg::cdiv(k, TB) - 1; bi >= 0; --bi) {
     const int p = bi * TB, pb = std::min(TB, k - p);
     TG_HIP(tg::dgemm(st, false, false, pb, m, pb, 1.0, Dinv + size_t(p) * ldd + p, ldd,
-                     Cw + size_t(p) * m, m, 0.0, C + size_t(p) * m, m));
+                     Cw + size_t(p) * ldc, ldc, 0.0, C + size_t(p) * ldc, ldc));
     if (p > 0)
-      TG_HIP(tg::dgemm(st, false, false, p, m, pb, -1.0, R + p, ldr, C + size_t(p) * m, m, 1.0, Cw,
-                       m));
+      TG_HIP(tg::dgemm(st, false, false, p, m, pb, -1.0, R + p, ldr, C + size_t(p) * ldc, ldc, 1.0,
+                       Cw, ldc));
   }
   return 0;
 }
@@ -2279,8 +2279,11 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
   if (!two_chol) {
     const int m = n - k;
     const dim3 gk(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k);
-    double *Yr = Y, *C = Bm, *ZT = S, *Nm = A;  // C: k x m (ld m)
     const bool small_m = urx_small_m(k, m);
+    // C: k x m; the explicit form keeps its ld even so the DGEMMs that read
+    // it stage 16-byte vectors
+    const int ldc = small_m ? m : m + (m & 1);
+    double *Yr = Y, *C = Bm, *ZT = S, *Nm = A;
     TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
     hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, Rx, ldr, k, Yr,
                        k);
@@ -2290,20 +2293,18 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
                               sizeof(double) * k, k, hipMemcpyDeviceToDevice, st));
       if (m <= 0) return 0;
       // the DGEMM stages 16-byte vectors only from 16-byte-aligned rows: with
-      // an odd k (R12's rows start mid-vector) or an odd m (C's ld), copy both
-      // operands to even-ld buffers first (Y and Rq, when the caller says
-      // they are not live; n = 12,288 at 3n/4 rank, k = 9173: 13.7 -> ~9 ms)
+      // an odd k R12's rows start mid-vector, so it is copied to an even-ld
+      // buffer first (Y, when the caller says it is not live; C has an even
+      // ld already)
       const int mp = m + (m & 1);
-      const bool pad = scratch_free && ((k & 1) || (m & 1) || (ldr & 1)) && mp <= k;
+      const bool pad = scratch_free && ((k & 1) || (ldr & 1)) && mp <= k;
       if (pad) {
-        double *R12p = Yr, *Cp = Rq;
+        double *R12p = Yr;
         TG_HIP(hipMemcpy2DAsync(R12p, sizeof(double) * mp, Rx + k, sizeof(double) * ldr,
                                 sizeof(double) * m, k, hipMemcpyDeviceToDevice, st));
-        TG_HIP(hipMemcpy2DAsync(Cp, sizeof(double) * mp, C, sizeof(double) * m,
-                                sizeof(double) * m, k, hipMemcpyDeviceToDevice, st));
-        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, R12p, mp, Cp, mp, 1.0, ZT, k));
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, R12p, mp, C, ldc, 1.0, ZT, k));
       } else {
-        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, m, 1.0, ZT, k));
+        TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, ldc, 1.0, ZT, k));
       }
       return 0;
     };
@@ -2314,7 +2315,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
       // the first term a triangular SYRK (a third of the square's flops)
       if (m > 0) {
         TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));          // 256-block inverses
-        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C)) return e;
+        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C, ldc)) return e;
         double *V = ZT, *G = Rq;  // k x m and m x m (ld m)
         TG_HIP(tg::dgemm(st, true, false, k, m, k, 1.0, Rx, ldr, Rx + k, ldr, 0.0, V, m));
         TG_HIP(tg::dgemm(st, true, false, m, m, k, 1.0, Rx + k, ldr, Rx + k, ldr, 0.0, G, m));
@@ -2333,10 +2334,10 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
       const char *ui = getenv("TG_URX_INV");
       if (ui && ui[0] == '1') {
         TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt));             // Yr = R11^-1
-        if (m > 0) TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, m));
+        if (m > 0) TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, Yr, k, Rx + k, ldr, 0.0, C, ldc));
       } else if (m > 0) {
         TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));         // 256-block inverses
-        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C)) return e;
+        if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C, ldc)) return e;
       }
       if (const int e = form_zt(true)) return e;
       TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
@@ -2364,7 +2365,7 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
     hipLaunchKernelGGL(flip_transpose_kernel, gk, dim3(256), 0, st, Yr, k, U, int64_t(ldu));
     TG_LAUNCHED();                                                    // U11 = V^-1 = J R^-T J
     if (m > 0)
-      TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, U, ldu, C, m, 0.0, U + k, ldu));  // V^-1 C
+      TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, U, ldu, C, ldc, 0.0, U + k, ldu));  // V^-1 C
     return 0;
   }
   CholStat h{};
