@@ -21,7 +21,7 @@
 //    its operands in registers (each A value in 4 waves, each B in 2):
 //    63.5 / 61.0 TF/s;
 //  * a persistent grid (CUs x 2 workgroups) takes work units from an atomic
-//    queue: whole tiles first, then the last round's tiles cut into NC = 8
+//    queue: whole tiles first, then the last round's tiles cut into NC = 16
 //    chunks of K; a whole tile is added to H directly, a chunk leaves a
 //    partial tile in the workspace and `syrk_fixup_kernel` adds a tile's
 //    chunks to H in chunk order -- the decomposition is static, so H is
@@ -457,7 +457,7 @@ int resident_groups() {
 
 namespace tg {
 
-constexpr int NCMAX = 8;  // chunks per tail tile (G tail tiles); TG_SYRK_NC picks 1..NCMAX, default 8
+constexpr int NCMAX = 16;  // chunks per tail tile (G tail tiles); TG_SYRK_NC picks 1..NCMAX, default 16
 
 // tail tiles cut into chunks: the last min(T, G) of the T lower tiles
 static int syrk16_tail_tiles(int n) {
@@ -480,8 +480,9 @@ bool syrk16_supported(const void *X, int n, int64_t ldx) {
 // is one unit; units are handed out by an atomic queue, so a workgroup that
 // runs faster (the older of the two on a CU wins the issue arbitration: with
 // equal static shares their times differed by up to 1.8x, TG_SYRK_STAMPS)
-// simply takes more of them, and the last round is made of eighth tiles
-// (quarters: 62.4 TF/s at n = 4096, eighths 65.4; n = 12,288 alike).
+// simply takes more of them, and the last round is made of sixteenth tiles
+// (interleaved medians, tools/syrk_nc_ab.py, n = 4096: quarters 62.4 TF/s,
+// eighths 65.4-66.2, sixteenths 66.2-67.6; n = 12,288 68.2-68.3 alike).
 // (Eighth tiles over only the last G / 2 tiles measured slower at n = 4096,
 // 24.8 against 19.8 ms: the whole tiles then handed to the slower workgroups
 // of the first round finish last.)
@@ -504,7 +505,7 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   a.Tt = syrk16_tail_tiles(n);
   a.head = a.T - a.Tt;
   const char *ncs = getenv("TG_SYRK_NC");  // development switch (read per call)
-  const int nc = ncs ? std::max(1, std::min(NCMAX, atoi(ncs))) : 8;
+  const int nc = ncs ? std::max(1, std::min(NCMAX, atoi(ncs))) : NCMAX;
   a.NC = std::min(nc, a.NS);
   a.CK = cdiv(a.NS, a.NC);
   a.U = a.head + a.Tt * a.NC;
