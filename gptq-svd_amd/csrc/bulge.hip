@@ -738,11 +738,13 @@ constexpr int DNCW = 3 * DG;          // role waves
 #define TG_BULGE_DF_XF 1
 #endif
 // the loader issues a chunk's loads before it waits for ring space (the
-// space is needed only by the LDS write): n = 12,288 69.0 -> 68.4 ms, 4096
-// unchanged, bit-identical; 0 restores the old order
+// space is needed only by the LDS write; 0 restores the old order).  Measured
+// 69.0 -> 68.4 ms at n = 12,288 before df_wait's fast path had its compiler
+// barrier; with it 69.1 ms (no gain), kept as the form the race hunt covers
 #ifndef TG_BULGE_LD_EARLY
 #define TG_BULGE_LD_EARLY 1
 #endif
+
 constexpr int DXF = TG_BULGE_DF_XF;           // loader waves = writer waves (each moves 1/DXF)
 constexpr int DBT = 64 * (DNCW + 2 * DXF);    // + loaders + writers
 // ring span at the tightest spacing: the loader's chunk ahead of sweep 0
@@ -950,7 +952,16 @@ constexpr int DF_TR0 = TG_BULGE_TR0;  // traced groups DF_TR0 .. DF_TR0 + 2
 // whole-wave wait until *p >= v (LDS word); false once the launch is dead
 __device__ inline bool df_wait(const unsigned *p, unsigned v, DfSync &sy, unsigned *stall,
                                unsigned long long timeout) {
-  if (lds_get(p) >= v) return true;
+  // Both exits carry the compiler barrier: the relaxed LDS atomic orders
+  // nothing else, and without it on the fast path the compiler may move the
+  // caller's LDS accesses above the poll (measured, tools/bulge_hunt.py: with
+  // the loader's loads issued before its ring-space wait and no barrier here,
+  // ~1 in 1500 launches at n = 384 and 1024 returned a different last 32
+  // (d, e); with it 0 in 20,000)
+  if (lds_get(p) >= v) {
+    asm volatile("" ::: "memory");
+    return true;
+  }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned it = 0;; ++it) {
     if (lds_get(&sy.dead)) return false;

@@ -56,6 +56,7 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
     }
   }
   if (seen) *seen = v;
+  asm volatile("" ::: "memory");  // the caller's data accesses stay below the poll
   return ok;
 }
 

@@ -73,3 +73,26 @@ def test_dataflow_repeats(monkeypatch):
         got = run(lib, A, "1", monkeypatch)
         for a, b in zip(ref, got):
             assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+@pytest.mark.parametrize("n", [384, 1024])
+def test_dataflow_repeats_many(n, monkeypatch):
+    """Thousands of launches (round 5: a missing compiler barrier on the LDS
+    wait's fast path let ~1 in 1500 launches return a different last 32 (d, e);
+    tools/bulge_hunt.py).  At that rate 3000 launches miss it with p ~ 0.14."""
+    from gptq_svd_amd import _lib as lib
+    monkeypatch.setenv("TG_BULGE_DF", "1")
+    Ad = torch.from_numpy(band(n, n)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_band_tridiag_workspace_size(n), torch.device(DEV))
+    d = torch.empty(n, dtype=torch.float64, device=DEV)
+    e = torch.empty(n, dtype=torch.float64, device=DEV)
+    ref = None
+    bad = 0
+    for _ in range(3000 if n <= 384 else 1000):
+        lib.call("tg_band_tridiag", lib.stream(), lib.ptr(Ad), n, n, lib.ptr(d), lib.ptr(e),
+                 lib.ptr(ws), ws.numel())
+        if ref is None:
+            ref = (d.clone(), e[:n - 1].clone())
+        else:
+            bad += int(not (torch.equal(d, ref[0]) and torch.equal(e[:n - 1], ref[1])))
+    assert bad == 0
