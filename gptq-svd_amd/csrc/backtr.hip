@@ -577,7 +577,7 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
                  gridDim.x) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-          __hip_atomic_store((gu32 *)(a.cnt + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tg::stall_set(a.cnt + 1);
           break;
         }
       }

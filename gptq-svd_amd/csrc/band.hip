@@ -31,6 +31,7 @@
 #include "band.h"
 #include "gemm64.h"
 #include "reduce.h"
+#include "spin.h"
 
 namespace tg {
 
@@ -871,13 +872,19 @@ __device__ __forceinline__ void xm_drain_slot(XmStep<NBC> &f) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(f.b[0]), "+v"(f.ap[0]), "+v"(f.ap[1]));
   }
 }
+// sh (packed loads only): the lane's pair starts at column m - 1 (m odd), so
+// its 16-byte load was moved one column left, (m - 2, m - 1), and column
+// m - 1's value is the load's second element
 template <int NBC>
-__device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[NBC], int k0,
-                                       doublex4 (&acc)[NBC][2], int m) {
+__device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[NBC], bool sh,
+                                       int k0, doublex4 (&acc)[NBC][2], int m) {
   const bool kok = k0 + ((threadIdx.x & 63) >> 4) < m;
 #pragma unroll
   for (int c = 0; c < NBC; ++c) {
-    const double b = (cok[c] && kok) ? xm_b<NBC>(f, c) : 0.0;
+    double v = xm_b<NBC>(f, c);
+    if constexpr (xm_pack<NBC>())
+      if (c == 0) v = sh ? xm_b<NBC>(f, 1) : v;
+    const double b = (cok[c] && kok) ? v : 0.0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       acc[c][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(xm_a<NBC>(f, i), b, acc[c][i], 0, 0, 0);
@@ -932,6 +939,8 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   const int KS = 4 * XW, kb = 4 * wid;
   int colc[NBC];
   bool cok[NBC];
+  // packed pair (m - 1, m) of an odd m: loaded as (m - 2, m - 1), see xm_mma
+  const bool csh = xm_pack<NBC>() && r0 + 2 * (lane & 15) > g.m - 2;
 #pragma unroll
   for (int c = 0; c < NBC; ++c) {
     if constexpr (xm_pack<NBC>()) {  // columns r0 + 2j + c; colc[0]: the pair, inside A22
@@ -959,7 +968,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
       for (int u = 0; u < DA; ++u) {
         const int k0 = kb + KS * (it + u);
         xm_wait_slot<NBC, DA>(f[u]);
-        xm_mma<NBC>(f[u], cok, k0, acc, g.m);
+        xm_mma<NBC>(f[u], cok, csh, k0, acc, g.m);
         xm_load_asm<NBC>(g, colc, k0 + KS * DA, f[u]);
       }
     }
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
         // then the load of step it + u + DA into the freed slot): the
         // machine scheduler otherwise sinks prefetches next to their uses
         const int k0 = kb + KS * (it + u);
-        xm_mma<NBC>(f[u], cok, k0, acc, g.m);
+        xm_mma<NBC>(f[u], cok, csh, k0, acc, g.m);
         __builtin_amdgcn_sched_barrier(0);
         xm_load<NBC>(g, colc, k0 + KS * DA, f[u]);
         __builtin_amdgcn_sched_barrier(0);
@@ -1086,7 +1095,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      g.tick[grp] = 0u;
+      tg::ctl_reset(&g.tick[grp]);
       s_last = __hip_atomic_fetch_add(&g.tick[NG], 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == unsigned(NG - 1);
     }
@@ -1125,8 +1134,8 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     }
   }
   if (tid == 0) {
-    g.tick[grp] = 0u;
-    if (NG > 1) g.tick[NG] = 0u;
+    tg::ctl_reset(&g.tick[grp]);
+    if (NG > 1) tg::ctl_reset(&g.tick[NG]);
   }
 }
 

@@ -737,12 +737,13 @@ constexpr int DNCW = 3 * DG;          // role waves
 #ifndef TG_BULGE_DF_XF
 #define TG_BULGE_DF_XF 1
 #endif
-// the loader issues a chunk's loads before it waits for ring space (the
-// space is needed only by the LDS write; 0 restores the old order).  Measured
-// 69.0 -> 68.4 ms at n = 12,288 before df_wait's fast path had its compiler
-// barrier; with it 69.1 ms (no gain), kept as the form the race hunt covers
+// 1: the loader issues a chunk's loads before it waits for ring space (the
+// space is needed only by the LDS write).  Measured 69.0 -> 68.4 ms at n =
+// 12,288 with a relaxed poll; with an ordered poll 69.1 ms, no gain, and it
+// was the order that exposed the round-5 race, so the default is 0 (loads
+// after the ring-space wait)
 #ifndef TG_BULGE_LD_EARLY
-#define TG_BULGE_LD_EARLY 1
+#define TG_BULGE_LD_EARLY 0
 #endif
 
 constexpr int DXF = TG_BULGE_DF_XF;           // loader waves = writer waves (each moves 1/DXF)
@@ -925,15 +926,24 @@ struct DfSync {
   unsigned wrange[2][2];  // [turn & 1] = {lo, hi) of a posted turn
 };
 
+// The LDS progress words are the waves' only hand-offs inside a workgroup,
+// and every one is a memory-model edge: the waits read them with workgroup-
+// scope ACQUIRE loads (no later LDS or global access of the waiting wave is
+// moved above the read) and the producers write them with workgroup-scope
+// RELEASE stores (every earlier LDS access of the producing wave is complete
+// first).  On gfx950 (no threadgroup split) these lower to exactly the
+// hand-placed form of round 5 -- `ds_read; s_waitcnt lgkmcnt(0)` and
+// `s_waitcnt lgkmcnt(0); ds_write` -- with no vmcnt wait (a workgroup-scope
+// release needs none there), so the reflector records' global stores stay in
+// flight; the difference is that the compiler now knows the order, which the
+// round-5 race (a relaxed poll, the loader's ring writes scheduled above it)
+// showed it did not (tools/check_handoff_isa.py checks the lowering).
 __device__ __forceinline__ unsigned lds_get(const unsigned *p) {
   return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// publish after this wave's LDS writes (only LDS ordering matters: a release
-// fence would also wait for the wave's global stores, the reflector records)
 __device__ __forceinline__ void lds_put(unsigned *p, unsigned v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 #if TG_BULGE_STATS
@@ -952,16 +962,12 @@ constexpr int DF_TR0 = TG_BULGE_TR0;  // traced groups DF_TR0 .. DF_TR0 + 2
 // whole-wave wait until *p >= v (LDS word); false once the launch is dead
 __device__ inline bool df_wait(const unsigned *p, unsigned v, DfSync &sy, unsigned *stall,
                                unsigned long long timeout) {
-  // Both exits carry the compiler barrier: the relaxed LDS atomic orders
-  // nothing else, and without it on the fast path the compiler may move the
-  // caller's LDS accesses above the poll (measured, tools/bulge_hunt.py: with
-  // the loader's loads issued before its ring-space wait and no barrier here,
-  // ~1 in 1500 launches at n = 384 and 1024 returned a different last 32
-  // (d, e); with it 0 in 20,000)
-  if (lds_get(p) >= v) {
-    asm volatile("" ::: "memory");
-    return true;
-  }
+  // Both exits leave through an acquire load of *p (lds_get), so the caller's
+  // accesses stay below the wait on every path.  (Round 5: the poll was a
+  // relaxed load, which orders nothing; with the loader's loads issued before
+  // its ring-space wait ~1 in 1500 launches at n = 384 and 1024 returned a
+  // different last 32 (d, e), tools/bulge_hunt.py.)
+  if (lds_get(p) >= v) return true;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned it = 0;; ++it) {
     if (lds_get(&sy.dead)) return false;
@@ -970,13 +976,12 @@ __device__ inline bool df_wait(const unsigned *p, unsigned v, DfSync &sy, unsign
     if ((it & 63u) == 63u) {
       if (__builtin_amdgcn_readfirstlane(tg::ctl_load(stall)) != 0u ||
           __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-        tg::ctl_store(stall, 1u);
+        tg::stall_set(stall);
         lds_put(&sy.dead, 1u);
         return false;
       }
     }
   }
-  asm volatile("" ::: "memory");  // the data loads stay below the poll
   return true;
 }
 
@@ -1217,7 +1222,6 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
           if (lds_get(&sy.dead)) hi = max(hi, n);
         }
         DF_ACC(0)
-        asm volatile("" ::: "memory");
         // this writer's blocks of b columns at a time: LDS reads first, then the stores
         constexpr int PX = PL / DXF;
         for (int c0 = lo; c0 < hi; c0 += SB_B) {
@@ -1256,8 +1260,9 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
         }
         if (last) {
           publish(lane0_or_dummy(prog + G, dummy, wlane), unsigned(hi));
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __hip_atomic_fetch_max(&sy.wbs, unsigned(hi), __ATOMIC_RELAXED,
+          // the ring slots below hi are free: release (this wave's LDS reads
+          // of them are complete) to the loader's acquire in df_wait
+          __hip_atomic_fetch_max(&sy.wbs, unsigned(hi), __ATOMIC_RELEASE,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         DF_ACC(4)

@@ -762,8 +762,7 @@ __device__ __forceinline__ void householder(const PqrArgs &g, PqrSm &sm, int w, 
     }
   }
   if (w == 0 && tid == 0)
-    __hip_atomic_store((gu32 *)(g.cnt + 1), unsigned(DEC_FALLBACK * 16), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    tg::ctl_record(g.cnt + 1, unsigned(DEC_FALLBACK * 16));
   grid_bar(g, ep);
   {
     double t[4];
@@ -905,8 +904,7 @@ __device__ __forceinline__ int ph_decide(int npass) {
   DBG_STAMP(dk + 6)
   if (tid == 0) {
     st_sc1(g.bc + BC_DEC, double(d));
-    __hip_atomic_store((gu32 *)(g.cnt + 1), unsigned(d * 16 + npass), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    tg::ctl_record(g.cnt + 1, unsigned(d * 16 + npass));
   }
   return d;
 }

@@ -25,6 +25,22 @@ __device__ __forceinline__ unsigned ctl_load(const unsigned *p) {
 __device__ __forceinline__ void ctl_store(unsigned *p, unsigned v) {
   __hip_atomic_store((spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Give-up path of a bounded wait: mark the launch's stall word.  An atomic OR
+// (not a store), so tools/check_handoff_isa.py can tell it from the
+// hand-off signals, which must follow a drain of the signalling wave's stores.
+__device__ __forceinline__ void stall_set(unsigned *p) {
+  (void)__hip_atomic_fetch_or((spin_u32 *)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Words no wave of the launch waits on -- a ticket counter reset by its last
+// user for the next launch, a path record the host reads afterwards -- are
+// written by an atomic exchange, so the hand-off check can tell them from
+// signals too.
+__device__ __forceinline__ void ctl_reset(unsigned *p) {
+  (void)__hip_atomic_exchange((spin_u32 *)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ctl_record(unsigned *p, unsigned v) {
+  (void)__hip_atomic_exchange((spin_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Wait until *word >= target.  Called by EVERY lane of a wave (the lanes
 // load the same word in one request and the value is made scalar), so the
@@ -48,7 +64,7 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
           break;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-          ctl_store(stall, 1u);
+          stall_set(stall);
           ok = false;
           break;
         }
@@ -56,7 +72,11 @@ __device__ inline bool spin_geq(const unsigned *word, unsigned target, unsigned 
     }
   }
   if (seen) *seen = v;
-  asm volatile("" ::: "memory");  // the caller's data accesses stay below the poll
+  // acquire edge for the compiler: no load of the caller moves above the poll
+  // (no instruction: the hand-offs behind these waits are read with sc1 loads
+  // from the one L2 they were stored to, or behind a workgroup barrier the
+  // polling wave joins -- see each caller and tools/check_handoff_isa.py)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return ok;
 }
 

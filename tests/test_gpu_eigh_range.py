@@ -190,3 +190,37 @@ def test_xm_asm_loads_bit_identical(n, monkeypatch):
     w_cc, A_cc = values("0")
     assert torch.equal(A_asm, A_cc)
     assert np.array_equal(w_asm, w_cc)
+
+
+@pytest.mark.parametrize("n,switches", [
+    (1025, {"TG_XM_NBC": "2"}), (1025, {"TG_XM_NBC": "2", "TG_XM_ASM": "0"}),
+    (1999, {"TG_XM_NBC": "2"}), (6401, {})])
+def test_xm_packed_odd_width(n, switches, monkeypatch):
+    """the packed X/M loads (NBC = 2, two adjacent A22 columns per
+    16-byte load) at an odd trailing width m: the pair (m - 1, m) is loaded
+    one column left and column m - 1 must take the load's second element.
+    Every panel's m has n's parity, so an odd n runs the tail pair on every
+    panel (n = 6401 takes NBC = 2 by default).  Eigenvalues vs LAPACK to
+    1e-12 ||H|| and vs the unpacked NBC = 1 kernel to 1e-12 ||H||."""
+    from gptq_svd_amd import _lib as lib
+    H = _wishart(n, 31)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def values(env):
+        for k in ("TG_XM_NBC", "TG_XM_ASM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        A = torch.from_numpy(H).to(DEV)
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        torch.cuda.synchronize()
+        return np.sort(w.cpu().numpy())
+
+    got = values(switches)
+    nrm = np.abs(got).max()
+    ref = np.linalg.eigvalsh(H)
+    assert np.abs(got - ref).max() <= 1e-12 * nrm, np.abs(got - ref).max() / nrm
+    one = values({"TG_XM_NBC": "1"})
+    assert np.abs(got - one).max() <= 1e-12 * nrm
