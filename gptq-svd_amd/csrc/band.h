@@ -131,7 +131,11 @@ hipError_t sy2sb_timed_out(hipStream_t st, const SbPlan &pl, const SbBufs &b, bo
 // in prog and is read back by sb2st_stalled (one D2H copy + stream sync).
 hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, double *V2,
                  unsigned *prog, double *d, double *e);
-hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled);
+// *broken: the tridiagonal guard fired (trace / Frobenius norm of the band not
+// preserved by the chase; d and e poisoned).  TG_TRI_GUARD_PRINT=1 prints the
+// guard's residuals.
+hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled,
+                         bool *broken = nullptr);
 // Z (n x k row-major) <- Q2 Z.
 hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2,
                        double *T2);

@@ -938,12 +938,19 @@ struct DfSync {
 // flight; the difference is that the compiler now knows the order, which the
 // round-5 race (a relaxed poll, the loader's ring writes scheduled above it)
 // showed it did not (tools/check_handoff_isa.py checks the lowering).
+// TG_BULGE_RACE_DEMO=1 (build-time, tools/bulge_hunt.py only): the round-5
+// relaxed form, to show the tridiagonal guard catching the race it allowed.
+#ifndef TG_BULGE_RACE_DEMO
+#define TG_BULGE_RACE_DEMO 0
+#endif
+constexpr int LDS_ACQ = TG_BULGE_RACE_DEMO ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE;
+constexpr int LDS_REL = TG_BULGE_RACE_DEMO ? __ATOMIC_RELAXED : __ATOMIC_RELEASE;
 __device__ __forceinline__ unsigned lds_get(const unsigned *p) {
-  return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, LDS_ACQ, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 __device__ __forceinline__ void lds_put(unsigned *p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if constexpr (TG_BULGE_RACE_DEMO) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, LDS_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 #if TG_BULGE_STATS
@@ -1293,14 +1300,106 @@ __global__ void extract_band_kernel(const double *__restrict__ A, int64_t lda, i
   Bst[idx] = (d <= SB_B && c + d < n) ? A[int64_t(c + d) * lda + c] : 0.0;
 }
 
+// ---------------------------------------------------------------------------
+// Tridiagonal guard.  Band -> tridiagonal is an orthogonal similarity, so it
+// keeps trace(B) = sum d and ||B||_F^2 = sum d^2 + 2 sum e^2.  Both sides are
+// O(n) sums: band_inv_kernel sums the band (GINV workgroups, fixed order)
+// before the chase, tri_check_kernel the tridiagonal after it and compares.
+// A violation (a race or fault in the pipeline, the round-5 kind: one bad
+// launch in ~1500 moved the last 32 d by up to 9e-2) sets the guard word
+// (ctl[3]): extract_tri_kernel then poisons (d, e) with NaN and the host
+// raises, so a corrupted tridiagonal never reaches k, perm or U.  Bars
+// (relative): |sum d - tr B| <= TRI_TOL_TR sqrt(n) ||B||_F and
+// |F(T) - F(B)| <= TRI_TOL_F F(B), F = squared Frobenius norm; measured
+// residuals are ~1e-15 .. 1e-14 (TG_TRI_GUARD_PRINT=1 prints them), so the
+// bars leave three to four orders of margin and still catch a change of one
+// d by ~1e-7 ||B||_F.
+// ---------------------------------------------------------------------------
+constexpr int GINV = 64;                 // band-sum workgroups
+constexpr double TRI_TOL_TR = 1e-10, TRI_TOL_F = 1e-10;
+
+template <int NT>
+__device__ inline void block_sum2(double &a, double &b, double (*sh)[NT]) {
+  const int t = threadIdx.x;
+  sh[0][t] = a;
+  sh[1][t] = b;
+  __syncthreads();
+#pragma unroll
+  for (int h = NT / 2; h > 0; h >>= 1) {
+    if (t < h) {
+      sh[0][t] += sh[0][t + h];
+      sh[1][t] += sh[1][t + h];
+    }
+    __syncthreads();
+  }
+  a = sh[0][0];
+  b = sh[1][0];
+}
+
+// part[2 b + {0, 1}] = (trace, squared Frobenius norm) of workgroup b's slice
+__global__ __launch_bounds__(256) void band_inv_kernel(const double *__restrict__ Bst, int n,
+                                                       double *__restrict__ part) {
+  __shared__ double sh[2][256];
+  const int64_t tot = int64_t(n) * LDB, per = (tot + GINV - 1) / GINV;
+  const int64_t e0 = blockIdx.x * per, e1 = min(tot, e0 + per);
+  double tr = 0.0, fr = 0.0;
+  for (int64_t x = e0 + threadIdx.x; x < e1; x += 256) {
+    const double v = Bst[x];
+    const bool dg = (x % LDB) == 0;  // d > b entries are zero in the extracted band
+    tr += dg ? v : 0.0;
+    fr += (dg ? 1.0 : 2.0) * v * v;
+  }
+  block_sum2<256>(tr, fr, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = tr;
+    part[2 * blockIdx.x + 1] = fr;
+  }
+}
+
+// One workgroup.  corrupt >= 0 (TG_TRI_GUARD_CORRUPT, tests): first change
+// d[corrupt] by 1e-3 (1 + |d|), as a faulty pipeline would.  res[0..1] =
+// the two relative residuals; *guard = 1 on a violation (or a NaN).
+__global__ __launch_bounds__(256) void tri_check_kernel(double *__restrict__ Bst, int n,
+                                                        const double *__restrict__ part,
+                                                        int corrupt, double *__restrict__ res,
+                                                        unsigned *__restrict__ guard) {
+  __shared__ double sh[2][256];
+  if (corrupt >= 0 && corrupt < n && threadIdx.x == 0) {
+    const double v = Bst[int64_t(corrupt) * LDB];
+    Bst[int64_t(corrupt) * LDB] = v + 1e-3 * (1.0 + fabs(v));
+  }
+  __syncthreads();
+  double tr = 0.0, fr = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const double dv = Bst[int64_t(i) * LDB];
+    const double ev = i + 1 < n ? Bst[int64_t(i) * LDB + 1] : 0.0;
+    tr += dv;
+    fr += dv * dv + 2.0 * ev * ev;
+  }
+  block_sum2<256>(tr, fr, sh);
+  if (threadIdx.x == 0) {
+    double t0 = 0.0, f0 = 0.0;
+    for (int b = 0; b < GINV; ++b) {
+      t0 += part[2 * b];
+      f0 += part[2 * b + 1];
+    }
+    const double rt = f0 > 0.0 ? fabs(tr - t0) / (sqrt(double(n)) * sqrt(f0)) : fabs(tr - t0);
+    const double rf = f0 > 0.0 ? fabs(fr - f0) / f0 : fabs(fr - f0);
+    res[0] = rt;
+    res[1] = rf;
+    if (!(rt <= TRI_TOL_TR && rf <= TRI_TOL_F)) tg::ctl_record(guard, 1u);
+  }
+}
+
 __global__ void extract_tri_kernel(const double *__restrict__ Bst, int n,
                                    const unsigned *__restrict__ stall, double *__restrict__ dg,
                                    double *__restrict__ e) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  // a stalled pipeline chased on stale band data: poison (d, e) so no
-  // consumer takes its eigenvalues for real ones
-  const bool bad = stall && *stall != 0u;
+  // a stalled pipeline chased on stale band data, or a tridiagonal that
+  // failed the invariant check (stall[1], the guard word): poison (d, e) so
+  // no consumer takes its eigenvalues for real ones
+  const bool bad = stall && (stall[0] != 0u || stall[1] != 0u);
   dg[i] = bad ? __builtin_nan("") : Bst[int64_t(i) * LDB];
   e[i] = bad ? __builtin_nan("") : (i + 1 < n) ? Bst[int64_t(i) * LDB + 1] : 0.0;
 }
@@ -1314,7 +1413,10 @@ int sb_smax(int n) { return n >= 3 ? (n - 3) / SB_B + 1 : 1; }
 // progress word per sweep group (at most one group per sweep, whichever
 // kernel runs) + control words + 64 dummy words; the control words start at
 // prog + (n - 2)
-size_t sb2st_prog_words(int n) { return size_t(std::max(1, n - 2)) + 4 + 64; }
+// + the tridiagonal guard's doubles (band partials, residuals) from the next
+// even word
+static size_t guard_off(int n) { return (size_t(std::max(1, n - 2)) + 4 + 64 + 1) & ~size_t(1); }
+size_t sb2st_prog_words(int n) { return guard_off(n) + 2 * (2 * GINV + 2); }
 
 // TG_BULGE_DF=0: the step-synchronous kernel (bulge_lds_kernel); default the
 // dataflow kernel (bulge_df_kernel: bit-identical, 21.1 -> 19.0 ms at n =
@@ -1335,6 +1437,10 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
   if (nsw > 0) {
     const bool df = bulge_dataflow();
     err = hipMemsetAsync(prog, 0, sizeof(unsigned) * sb2st_prog_words(n), st);
+    if (err != hipSuccess) return err;
+    double *gpart = reinterpret_cast<double *>(prog + guard_off(n));
+    hipLaunchKernelGGL(band_inv_kernel, dim3(GINV), dim3(256), 0, st, Bst, n, gpart);
+    err = hipGetLastError();
     if (err != hipSuccess) return err;
     unsigned *ctl = prog + nsw;  // [0] XCD + 1, [1] group queue, [2] stall flag
     stall = ctl + 2;
@@ -1465,20 +1571,36 @@ hipError_t sb2st(hipStream_t st, const double *A, int lda, int n, double *Bst, d
       (void)hipEventDestroy(e1);
     }
   }
+  if (nsw > 0) {
+    const char *cx = getenv("TG_TRI_GUARD_CORRUPT");  // tests: corrupt one d before the check
+    double *gpart = reinterpret_cast<double *>(prog + guard_off(n));
+    hipLaunchKernelGGL(tri_check_kernel, dim3(1), dim3(256), 0, st, Bst, n, gpart,
+                       cx ? atoi(cx) : -1, gpart + 2 * GINV, prog + nsw + 3);
+    err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
   hipLaunchKernelGGL(extract_tri_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, Bst, n, stall, d,
                      e);
   return hipGetLastError();
 }
 
-hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled) {
+hipError_t sb2st_stalled(hipStream_t st, int n, const unsigned *prog, bool *stalled,
+                         bool *broken) {
   *stalled = false;
+  if (broken) *broken = false;
   const int nsw = n - 2;
   if (nsw <= 0) return hipSuccess;
-  unsigned h = 0;
-  hipError_t e = hipMemcpyAsync(&h, prog + nsw + 2, sizeof(unsigned),
-                                hipMemcpyDeviceToHost, st);
+  unsigned h[2] = {0u, 0u};
+  double r[2] = {0.0, 0.0};
+  hipError_t e = hipMemcpyAsync(h, prog + nsw + 2, sizeof(h), hipMemcpyDeviceToHost, st);
+  const bool pr = getenv("TG_TRI_GUARD_PRINT") != nullptr;
+  if (e == hipSuccess && pr)
+    e = hipMemcpyAsync(r, prog + guard_off(n) + 4 * GINV, sizeof(r), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  *stalled = h != 0u;
+  if (pr) fprintf(stderr, "tri_guard n=%d: trace %.3e frobenius %.3e%s\n", n, r[0], r[1],
+                  h[1] ? " VIOLATED" : "");
+  *stalled = h[0] != 0u;
+  if (broken) *broken = h[1] != 0u;
   return e;
 }
 
@@ -1773,11 +1895,16 @@ extern "C" int tg_band_tridiag(void *stream, const double *A, int n, int lda, do
   band_ws_layout(ar, n, &b);
   TG_WS(ar);
   TG_HIP(tg::sb2st(st, A, lda, n, b.Bst, b.V2, b.prog, d, e));
-  bool stalled = false;
-  TG_HIP(tg::sb2st_stalled(st, n, b.prog, &stalled));
+  bool stalled = false, broken = false;
+  TG_HIP(tg::sb2st_stalled(st, n, b.prog, &stalled, &broken));
   if (stalled) {
     tg::set_error("tg_band_tridiag: bulge-chasing pipeline stalled (a hand-off wait timed out)");
     return int(hipErrorLaunchTimeOut);
+  }
+  if (broken) {
+    tg::set_error("tg_band_tridiag: the tridiagonal failed its invariant check (trace / Frobenius "
+                  "norm of the band not preserved); d and e are poisoned");
+    return int(hipErrorIllegalState);
   }
   return 0;
 }

@@ -1464,18 +1464,26 @@ extern "C" int tg_eigh_values(void *stream, double *A, int n, int lda, double *w
   if (ts) {
     TG_HIP(tg::sy2sb(st, A, lda, n, pl, sb));
     TG_HIP(tg::sb2st(st, A, lda, n, sb.Bst, sb.V2, sb.prog, w.d, w.e));
-    bool stalled = false;
-    TG_HIP(tg::sb2st_stalled(st, n, sb.prog, &stalled));
+    bool stalled = false, broken = false;
+    TG_HIP(tg::sb2st_stalled(st, n, sb.prog, &stalled, &broken));
     bool ptmo = false;
     TG_HIP(tg::sy2sb_timed_out(st, pl, sb, &ptmo));
     if (ptmo) {
       tg::set_error("tg_eigh_values: panel-QR grid barrier timed out; the band form is invalid");
       return int(hipErrorLaunchTimeOut);
     }
+    if (stalled || broken)  // all-ones bytes: NaN eigenvalues for any caller that ignores the code
+      TG_HIP(hipMemsetAsync(w_asc, 0xff, sizeof(double) * size_t(n), st));
     if (stalled) {
       tg::set_error("tg_eigh_values: bulge-chasing pipeline stalled (a hand-off wait timed out); "
                     "the tridiagonal form is invalid");
       return int(hipErrorLaunchTimeOut);
+    }
+    if (broken) {
+      tg::set_error("tg_eigh_values: the tridiagonal failed its invariant check (trace / "
+                    "Frobenius norm of the band not preserved by the bulge chase); the "
+                    "eigenvalues are poisoned");
+      return int(hipErrorIllegalState);
     }
   }
   if (!ts) {

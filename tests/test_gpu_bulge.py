@@ -96,3 +96,56 @@ def test_dataflow_repeats_many(n, monkeypatch):
         else:
             bad += int(not (torch.equal(d, ref[0]) and torch.equal(e[:n - 1], ref[1])))
     assert bad == 0
+
+
+@pytest.mark.parametrize("n", [64, 1000, 4096])
+def test_tri_guard_quiet(n, monkeypatch, capfd):
+    """The tridiagonal guard (csrc/bulge.hip tri_check_kernel: trace and
+    squared Frobenius norm of the band preserved by the chase) stays quiet on
+    healthy launches, with its residuals far below its 1e-10 bars."""
+    import re
+    from gptq_svd_amd import _lib as lib
+    monkeypatch.setenv("TG_TRI_GUARD_PRINT", "1")
+    d, e = run(lib, band(n, n + 3), "1", monkeypatch)[:2]
+    assert np.isfinite(d).all() and np.isfinite(e[:n - 1]).all()
+    out = capfd.readouterr().err
+    m = re.search(r"tri_guard n=(\d+): trace (\S+) frobenius (\S+)", out)
+    assert m and int(m.group(1)) == n, out
+    print(out.strip())
+    assert float(m.group(2)) <= 1e-13 and float(m.group(3)) <= 1e-13
+
+
+@pytest.mark.parametrize("entry", ["tg_band_tridiag", "tg_eigh_values"])
+def test_tri_guard_fires(entry, monkeypatch):
+    """A corrupted tridiagonal (TG_TRI_GUARD_CORRUPT=i: d[i] moved by
+    1e-3 (1 + |d_i|) on the device after the chase, as a faulty pipeline
+    would leave it) fails the invariant check: the call raises and the
+    outputs are NaN, so no rank, perm or U is formed from it; the next call
+    without the switch is clean again."""
+    from gptq_svd_amd import _lib as lib
+    n = 700
+    A = band(n, 11) if entry == "tg_band_tridiag" else (lambda X: X.T @ X / 1000)(
+        np.random.default_rng(5).standard_normal((1000, n)))
+    Ad = torch.from_numpy(A).to(DEV)
+    if entry == "tg_band_tridiag":
+        ws = lib.workspace(lib.lib.tg_band_tridiag_workspace_size(n), torch.device(DEV))
+        d = torch.empty(n, dtype=torch.float64, device=DEV)
+        e = torch.empty(n, dtype=torch.float64, device=DEV)
+        args = lambda: (lib.stream(), lib.ptr(Ad), n, n, lib.ptr(d), lib.ptr(e), lib.ptr(ws),
+                        ws.numel())
+        outs = lambda: [d, e[:n - 1]]
+    else:
+        ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        args = lambda: (lib.stream(), lib.ptr(Ad.clone()), n, n, lib.ptr(w), lib.ptr(ws),
+                        ws.numel())
+        outs = lambda: [w]
+    monkeypatch.setenv("TG_TRI_GUARD_CORRUPT", "37")
+    with pytest.raises(RuntimeError, match="invariant check"):
+        lib.call(entry, *args())
+    torch.cuda.synchronize()
+    assert all(torch.isnan(t).all() for t in outs())
+    monkeypatch.delenv("TG_TRI_GUARD_CORRUPT")
+    lib.call(entry, *args())
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(t).all() for t in outs())

@@ -1,7 +1,8 @@
 """Rare-race hunt in the band -> tridiagonal stage (development tool):
 tg_band_tridiag on a fixed random band, REPS calls per width, each (d, e)
-compared on the device with the first call's.  Prints the number of differing
-calls and, for the first few, the first differing index of d and of e.
+compared on the device with the first call's.  Prints the number of calls
+that differ silently and of calls the tridiagonal guard rejected (the call
+raises, outputs poisoned), and for the first few where they differ.
     TRUNCGPTQ_LIB=variant.so N=384,1024 REPS=20000 python tools/bulge_hunt.py"""
 import os
 import sys
@@ -32,9 +33,16 @@ for n in [int(x) for x in os.environ.get("N", "384,1024").split(",")]:
     bad, shown = 0, 0
     reps = int(os.environ.get("REPS", "20000"))
     t0 = time.time()
+    caught = 0
     for r in range(reps):
-        lib.call("tg_band_tridiag", lib.stream(), lib.ptr(Ad), n, n, lib.ptr(d), lib.ptr(e),
-                 lib.ptr(ws), ws.numel())
+        try:
+            lib.call("tg_band_tridiag", lib.stream(), lib.ptr(Ad), n, n, lib.ptr(d), lib.ptr(e),
+                     lib.ptr(ws), ws.numel())
+        except RuntimeError as exc:  # the tridiagonal guard fired: outputs poisoned
+            caught += 1
+            if caught <= 5:
+                print(f"  n={n} call {r}: guard: {exc}", flush=True)
+            continue
         if ref is None:
             ref = (d.clone(), e[:n - 1].clone())
             continue
@@ -48,4 +56,5 @@ for n in [int(x) for x in os.environ.get("N", "384,1024").split(",")]:
                       f"({de.size}); max |dd| {float((d - ref[0]).abs().max()):.2e}", flush=True)
         if r % 5000 == 0:
             print(f"  n={n} call {r} ({time.time() - t0:.0f} s)", flush=True)
-    print(f"{tag} n={n}: {bad} of {reps - 1} calls differ ({time.time() - t0:.0f} s)", flush=True)
+    print(f"{tag} n={n}: {bad} of {reps - 1} calls differ silently, {caught} caught by the "
+          f"tridiagonal guard ({time.time() - t0:.0f} s)", flush=True)
