@@ -2259,6 +2259,73 @@ static bool urx_small_m(int k, int m) {
   return int64_t(m) * 16 <= int64_t(k);
 }
 
+// Stages of the explicit form (below), shared with the column-sharded entry
+// points (tg_urx_c / tg_urx_u11 / tg_urx_u12, gptq_svd_amd.dist.
+// u_factor_rx_sharded): each column of C = R11^-1 R12 and of U12 = V^-1 C
+// depends on its own column of R12 / C only (block back substitution and
+// GEMMs with a fixed k order per entry), so a rank computing a column block
+// gets the single-call values bit for bit.
+// (a) the 256-block diagonal inverses of R11 into Yr (k x k, zeroed first)
+static int urx_diag_inverses(hipStream_t st, const double *Rx, int ldr, int k, double *Yr,
+                             double *Tt) {
+  TG_HIP(hipMemsetAsync(Yr, 0, sizeof(double) * size_t(k) * k, st));
+  hipLaunchKernelGGL(trinv_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, Rx, ldr, k, Yr,
+                     k);
+  TG_LAUNCHED();
+  TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));
+  return 0;
+}
+// (b) from the full C (k x m, ld ldc): Z^T = R11 + R12 C^T, N = Z Z^T, the
+// Cholesky of N' = J N J (refined when ill-conditioned) and U11 = V^-1 into
+// U; Yr, ZT, Nm, Rq: k x k scratch
+static int urx_u11_from_c(hipStream_t st, const double *Rx, int ldr, int n, int k, const double *C,
+                          int ldc, double *U, int ldu, double *Yr, double *ZT, double *Nm,
+                          double *Rq, double *Tt, double *Wb, int *info, RefineWs &rw) {
+  const int m = n - k;
+  const dim3 gk(tg::cdiv(k, 256) < 16 ? tg::cdiv(k, 256) : 16, k);
+  auto form_zt = [&](bool scratch_free) -> int {  // Z^T = R11 + R12 C^T
+    TG_HIP(hipMemcpy2DAsync(ZT, sizeof(double) * k, Rx, sizeof(double) * ldr, sizeof(double) * k,
+                            k, hipMemcpyDeviceToDevice, st));
+    if (m <= 0) return 0;
+    // the DGEMM stages 16-byte vectors only from 16-byte-aligned rows: with
+    // an odd k R12's rows start mid-vector, so it is copied to an even-ld
+    // buffer first (Y, when the caller says it is not live; C has an even
+    // ld already)
+    const int mp = m + (m & 1);
+    const bool pad = scratch_free && ((k & 1) || (ldr & 1)) && mp <= k;
+    if (pad) {
+      double *R12p = Yr;
+      TG_HIP(hipMemcpy2DAsync(R12p, sizeof(double) * mp, Rx + k, sizeof(double) * ldr,
+                              sizeof(double) * m, k, hipMemcpyDeviceToDevice, st));
+      TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, R12p, mp, C, ldc, 1.0, ZT, k));
+    } else {
+      TG_HIP(tg::dgemm(st, false, true, k, k, m, 1.0, Rx + k, ldr, C, ldc, 1.0, ZT, k));
+    }
+    return 0;
+  };
+  if (const int e = form_zt(true)) return e;
+  TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
+  hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, Rq);  // N' = J N J
+  TG_LAUNCHED();
+  TG_HIP(chol_upper_rows(st, Rq, k, k, k, Wb, info));               // N' = R^T R
+  hipLaunchKernelGGL(diag_range_kernel, dim3(1), dim3(256), 0, st, Rq, int64_t(k), k, rw.stats);
+  TG_LAUNCHED();
+  CholStat h{};
+  TG_HIP(read_stat(st, rw.stats, info, h));
+  if (needs_refine(h)) {
+    double *Yq = Nm;
+    TG_HIP(zero_lower(st, Rq, k, k));
+    hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, ZT, k, Yq);
+    TG_LAUNCHED();
+    const int e = refine_factor(st, Yq, k, k, Rq, rw, Wb, info, h);
+    if (e != 0) return e;
+  }
+  TG_HIP(trinv(st, Rq, k, k, Yr, Tt));                              // Yr = R^-1
+  hipLaunchKernelGGL(flip_transpose_kernel, gk, dim3(256), 0, st, Yr, k, U, int64_t(ldu));
+  TG_LAUNCHED();                                                    // U11 = V^-1 = J R^-T J
+  return 0;
+}
+
 extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U,
                               int ldu, void *ws, size_t ws_bytes) {
   TG_ARG(Rx, 2, "null Rx");
@@ -2339,8 +2406,12 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
         TG_HIP(trinv_offdiag(st, Rx, ldr, Yr, k, k, Tt, TB));         // 256-block inverses
         if (const int e = trsm_upper_blocks(st, Rx, ldr, k, Rx + k, m, Yr, k, Nm, C, ldc)) return e;
       }
-      if (const int e = form_zt(true)) return e;
-      TG_HIP(tg::dsyrk_tn(st, k, k, 1.0, ZT, k, 0.0, Nm, k));         // N = Z Z^T
+      if (const int e = urx_u11_from_c(st, Rx, ldr, n, k, C, ldc, U, ldu, Yr, ZT, Nm, Rq, Tt, Wb,
+                                       info, rw))
+        return e;
+      if (m > 0)
+        TG_HIP(tg::dgemm_upper_a(st, k, m, k, 1.0, U, ldu, C, ldc, 0.0, U + k, ldu));  // V^-1 C
+      return 0;
     }
     hipLaunchKernelGGL(flip_both_kernel, gk, dim3(256), 0, st, Nm, k, Rq);  // N' = J N J
     TG_LAUNCHED();

@@ -435,23 +435,29 @@ __global__ __launch_bounds__(NT) void syrk_fixup_kernel(SyrkArgs a) {
   }
 }
 
-int resident_groups() {
-  static int cached[64] = {0};
+// Persistent grid: resident workgroups of the kernel that launches (both
+// kernels run two per CU on MI355X: syrk64l_kernel's 64 KB of static LDS and
+// syrk16_kernel's registers), cached per device and kernel.
+int resident_groups(bool lds64) {
+  static int cached[64][2] = {{0}};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 512;
-  if (cached[dev] == 0) {
+  int &c = cached[dev][lds64 ? 1 : 0];
+  if (c == 0) {
     int ncu = 0, occ = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         ncu < 1)
       ncu = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk16_kernel<false>, NT, 0) !=
-            hipSuccess ||
-        occ < 1)
-      occ = 1;
-    cached[dev] = ncu * std::min(occ, 2);
+    const hipError_t e =
+        lds64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk64l_kernel<false>, NT, 0)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, syrk16_kernel<false>, NT, 0);
+    if (e != hipSuccess || occ < 1) occ = 1;
+    c = ncu * std::min(occ, 2);
   }
-  return cached[dev];
+  return c;
 }
+// workspace sizing: the larger of the two (TG_SYRK_LDS64 is read per call)
+int resident_groups() { return std::max(resident_groups(true), resident_groups(false)); }
 
 }  // namespace
 
@@ -501,8 +507,8 @@ hipError_t syrk16(hipStream_t st, const void *X, bool bf16, int64_t rows, int n,
   const char *l64 = getenv("TG_SYRK_LDS64");
   const bool lds64 = !(l64 && l64[0] == '0');
   a.NS = cdiv(rows, lds64 ? KL : NSUB * KC);
-  const int G = resident_groups();
-  a.Tt = syrk16_tail_tiles(n);
+  const int G = resident_groups(lds64);
+  a.Tt = std::min(syrk16_tail_tiles(n), G);
   a.head = a.T - a.Tt;
   const char *ncs = getenv("TG_SYRK_NC");  // development switch (read per call)
   const int nc = ncs ? std::max(1, std::min(NCMAX, atoi(ncs))) : NCMAX;

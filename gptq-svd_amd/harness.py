@@ -335,11 +335,15 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
     `early_stop`: a calibration pass ends each batch at the group's first
     linear -- its input is accumulated into H, then the rest of the layer is
     skipped (the reference runs the whole layer and discards the output,
-    quantize.py:139-148, so H is the same).  `staged` (default: `early_stop`):
-    Llama / Qwen2 / Qwen3 / Mistral decoder layers keep each batch's
-    intermediate activations between groups instead of re-running the layer
-    from its input for every group (``_staged_layer``; bit-identical result,
-    about a third of the forward work).  `clock`: a StageClock that
+    quantize.py:139-148, so H is the same).  `staged` (default: `early_stop`
+    and not `offload`): Llama / Qwen2 / Qwen3 / Mistral decoder layers keep
+    each batch's intermediate activations between groups instead of re-running
+    the layer from its input for every group (``_staged_layer``; bit-identical
+    result, about a third of the forward work).  Its memory cost is about
+    tokens x (2 hidden + intermediate) x 2 bytes on the device (13 GB for
+    128 x 2048 tokens at Qwen3-8B widths, ~19 GB at Llama-3-70B's), which the
+    per-group passes never hold -- hence off by default with `offload`, the
+    memory-tight mode.  `clock`: a StageClock that
     receives per-stage device times.
     `save_path`: write the run's ``quantization.log`` and ``results.json`` there
     in the reference's schema (``runlog.py``; rank 0 only in multi-GPU mode);
@@ -550,7 +554,7 @@ def quantize_model(model: nn.Module, input_ids_list: Sequence[torch.Tensor], mod
         t_layer = time.time()
         if offload:
             layer = layer.to(device)
-        use_staged = early_stop if staged is None else staged
+        use_staged = (early_stop and not offload) if staged is None else staged
         if use_staged and _staged_layer(layer):
             layer_staged(i, layer)
         else:

@@ -49,7 +49,9 @@ int tg_syrk_accum(void *stream, const void *X, int x_dtype, int64_t rows, int n,
                   double *H, int ldh);
 
 /* The same update with a caller workspace (tg_syrk_workspace_size(n) bytes,
- * independent of rows; up to ~256 MiB at n >= 2944): fp16 / bf16 X with n and ldx
+ * independent of rows: the partial tiles of the last round of 128 x 128 tiles,
+ * Tt = min(tiles, resident workgroups) tiles x 16 chunks x 128 KiB, i.e. about
+ * 1 GiB on a 256-CU MI355X once n >= ~4000): fp16 / bf16 X with n and ldx
  * multiples of 8 and a 16-byte aligned X take the dedicated 16-bit SYRK
  * (syrk.hip: X kept 16-bit in LDS, lower 128 x 128 tiles handed out by an
  * atomic queue over a static decomposition whose partial tiles are summed in

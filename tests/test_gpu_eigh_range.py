@@ -224,3 +224,34 @@ def test_xm_packed_odd_width(n, switches, monkeypatch):
     assert np.abs(got - ref).max() <= 1e-12 * nrm, np.abs(got - ref).max() / nrm
     one = values({"TG_XM_NBC": "1"})
     assert np.abs(got - one).max() <= 1e-12 * nrm
+
+
+@pytest.mark.parametrize("n,count", [(4096, 14), (4096, 16), (1000, 1), (600, 14), (4100, 14),
+                                     (9000, 14)])
+def test_q2_lds_bit_identical(n, count, monkeypatch):
+    """The few-vector Q2 with Z resident in LDS (csrc/backtr.hip
+    q2_lds_kernel, the default for <= 16 vectors: one wave per pair column
+    of blocks, LDS progress counters inside a workgroup, write-through
+    boundary chunks between workgroups) gives the level-by-level form's
+    eigenvectors (TG_BT_Q2_LDS=0) bit for bit, twice in a row -- partial last
+    workgroups (n = 600, 1000), n not a multiple of 32, and more workgroups
+    than one XCD has CUs (n = 9000: 36)."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 17)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def vectors(flag):
+        monkeypatch.setenv("TG_BT_Q2_LDS", flag)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - count, count,
+                 lib.ptr(V), n, lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    ref = vectors("0")
+    for _ in range(2):
+        assert np.array_equal(vectors("1"), ref)

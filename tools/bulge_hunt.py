@@ -42,6 +42,13 @@ for n in [int(x) for x in os.environ.get("N", "384,1024").split(",")]:
             caught += 1
             if caught <= 5:
                 print(f"  n={n} call {r}: guard: {exc}", flush=True)
+                if os.environ.get("TG_TRI_GUARD_NOPOISON") and ref is not None:
+                    # values kept: where and by how much they differ
+                    dd = (d != ref[0]).nonzero().flatten().cpu().numpy()
+                    de = (e[:n - 1] != ref[1]).nonzero().flatten().cpu().numpy()
+                    print(f"    d differs at {dd[:8]} ({dd.size}), e at {de[:8]} ({de.size}); "
+                          f"max |dd| {float((d - ref[0]).abs().max()):.2e} "
+                          f"max |de| {float((e[:n - 1] - ref[1]).abs().max()):.2e}", flush=True)
             continue
         if ref is None:
             ref = (d.clone(), e[:n - 1].clone())

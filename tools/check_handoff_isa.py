@@ -5,7 +5,8 @@ kernels (csrc/spin.h, DESIGN.md §3 "Persistent kernels").
 The kernels hand data from one workgroup to another inside a launch in two
 forms (MI355X_MICROARCH.md § visibility):
 
-* write-through form (pqr_kernel, xm_kernel, the pivot kernels): payload
+* write-through form (pqr_kernel, xm_kernel, the pivot kernels, the
+  boundary chunks of q2_lds_kernel): payload
   stored `sc1`, every storing wave drains `vmcnt(0)`, one lane signals (an
   agent-scope atomic add or `sc1` store); the consumer polls the word and
   reads the payload with `sc1` loads -- the guide's "Valid forms" row 1;
@@ -56,7 +57,8 @@ KERNELS = {
     "backtr.o": [("bt_few_kernelILi1ELb1E", True, False, True),
                  ("bt_few_kernelILi2ELb1E", True, False, True),
                  ("bt_few_kernelILi1ELb0E", True, False, True),
-                 ("bt_few_kernelILi2ELb0E", True, False, True)],
+                 ("bt_few_kernelILi2ELb0E", True, False, True),
+                 ("q2_lds_kernelILi1E", False, False, True)],
     # pqr: the hand-off words and payloads go through explicit address_space(1)
     # sc1 atomics (st_sc1 / ld_sc1); its flat accesses are the panel rows of
     # the launch's input and its outputs, reached through the LDS copy of the
