@@ -53,6 +53,9 @@ _SIGS = {
                                       _sz], _i),
     "tg_ufactor_rx_workspace_size": ([_i, _i], _sz),
     "tg_u_factor_rx": ([_vp, _vp, _i, _i, _i, _vp, _i, _vp, _sz], _i),
+    "tg_urx_c": ([_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _sz], _i),
+    "tg_urx_u11": ([_vp, _vp, _i, _i, _i, _vp, _i, _vp, _i, _vp, _sz], _i),
+    "tg_urx_u12": ([_vp, _vp, _i, _i, _vp, _i, _i, _vp, _i], _i),
     "tg_group_params": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp], _i),
     "tg_process_block_workspace_size": ([_i], _sz),
     "tg_process_block": ([_vp, _vp, _i, _vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _i,

@@ -729,42 +729,46 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Q2 with Z resident in LDS (the default for k <= 32; TG_BT_Q2_LDS=0 keeps
+// Q2 with Z resident in LDS (the default for k <= 16; TG_BT_Q2_LDS=0 keeps
 // bt_few_kernel's level-by-level Q2).  Block (G2, s) touches Z rows
 // [32 c + 1, 32 c + 64), c = G2 + s: row chunks c and c + 1 (chunk c = rows
-// 32 c + 1 .. 32 c + 32).  So the blocks of "pair column" c (G2 = min(c,
-// NG2 - 1) down to 0, every one valid: s = c - G2 < ntasks(n, 32 G2) for all
-// c < smax) form one sequence, and block (G2, c) needs exactly (G2, c - 1)
-// (shares chunk c, one level earlier) and (G2 + 1, c + 1) (shares chunk
-// c + 1, one level earlier) -- the level order of the block schedule as
-// point-to-point edges.  One wave per pair column; QW consecutive columns per
-// workgroup, whose chunks live in the workgroup's LDS, so every hand-off
-// between them is an LDS progress counter (workgroup acquire / release).
-// Only the first chunk of each workgroup (w > 0) is shared with the previous
-// workgroup's last column: it stays in global memory, stored write-through
-// (sc1) and read with sc1 loads, and the two boundary columns publish their
-// progress in global words after draining their stores (MI355X_MICROARCH.md
-// "Valid forms" row 1, placement-independent).  Same blocks, reflectors, T
-// factors and MFMA sequence as q2_block, so Z is bit-identical to the
-// level-by-level form.  The level chain (smax + NG2 - 1 = 255 blocks at
-// n = 4096) then costs a block's arithmetic plus an LDS hand-off per link
-// instead of an L2 round trip and a grid barrier.
+// 32 c + 1 .. 32 c + 32), and must follow exactly (G2, s - 1) and (G2 + 1, s)
+// (the blocks it shares a chunk with one level earlier; the last block of a
+// group, s = nb(G2) - 1 = nb(G2 + 1), follows the whole of group G2 + 1).
+// One wave per sweep group G2 walks its blocks s = 0, 1, ...; QW consecutive
+// groups form a workgroup whose waves hand chunks down through LDS (group
+// G2 + 1 finishes a chunk, G2 takes it one block later) with LDS progress
+// counters (workgroup acquire / release).  A chunk enters a workgroup once,
+// from the next workgroup's lowest wave (or from Z), and leaves it once,
+// through its own lowest wave: that wave stores the first chunk of each block
+// to global memory write-through (sc1), drains and publishes its progress in a
+// global word; the next lower workgroup's top wave polls the word and loads
+// the chunk with sc1 loads (MI355X_MICROARCH.md "Valid forms" row 1,
+// placement-independent).  So the 255-block chain at n = 4096 crosses a
+// global hand-off only once per workgroup (16); the rest are LDS hand-offs.
+// (The first form, one wave per pair column c, shared each boundary chunk
+// between two workgroups that alternated on it every level: 254 global
+// hand-offs on the critical path, 1.76 ms.)  The workgroup keeps a ring of
+// RS chunks; the top wave reuses a slot only after the lowest wave is done
+// with its previous chunk.  Same blocks, reflectors, T factors and MFMA
+// sequence as q2_block: Z is bit-identical to the level-by-level form.
 // ---------------------------------------------------------------------------
-constexpr int QW = 8;  // pair columns (waves) per workgroup
+constexpr int QW = 8;   // sweep groups (waves) per workgroup
+constexpr int RS = 16;  // chunk ring slots per workgroup
 
 struct Q2LArgs {
   double *Z;
   int n, k;
   const double *V2, *T2;
   int smax, ng2;
-  unsigned *gprog;  // [smax]: blocks done per pair column (boundary columns only), zeroed
+  unsigned *gprog;  // [ng2]: blocks done by each workgroup's lowest group (zeroed)
   unsigned *stall;  // set on a timed-out wait (the host reports it)
   unsigned long long timeout;
 };
 
 template <int NCB>
 struct Q2LShared {
-  double Zs[QW][32][16 * NCB + 1];  // chunk 8 w + q in slot q (slot 0 unused for w > 0)
+  double Zs[RS][32][16 * NCB + 1];  // chunk c in slot c % RS
   double Vs[QW][QB][SB_B + 1];
   unsigned done[QW];
   unsigned dead;
@@ -814,179 +818,169 @@ __device__ inline void q2l_fetch(const Q2LArgs &a, int G2, int s, Q2Pre &p) {
         p.tt[(kb * 4 + qq) * 2 + ia] = Tb[(ia * 16 + lc) * QB + kb * 16 + 4 * qq + lr];
 }
 
+__device__ __forceinline__ int q2l_nb(int n, int G2) { return ntasks(n, G2 * QB); }
+
 template <int NCB>
 __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
   __shared__ Q2LShared<NCB> sm;
   const int n = a.n, k = a.k, tid = threadIdx.x, lane = tid & 63;
-  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int w = blockIdx.x, c0 = w * QW, c = c0 + q;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = blockIdx.x, G0 = w * QW, G2 = G0 + g;
+  const int gtop = min(QW, a.ng2 - G0) - 1;  // highest wave with a sweep group
   const int lr = lane >> 4, lc = lane & 15;
   constexpr int KC = 16 * NCB;
-  // chunk ch of this workgroup in LDS, or in global memory (the shared first
-  // chunk of w > 0, and chunks past the grid: rows >= n, all masked)
-  auto in_lds = [&](int ch) { return ch >= c0 + (w > 0 ? 1 : 0) && ch < c0 + QW; };
-  // load this workgroup's LDS chunks
+  // this workgroup's own chunks G0 .. G0 + QW - 1 from Z (no higher group touches them)
   for (int e = tid; e < QW * 32 * KC; e += 64 * QW) {
-    const int sl = e / (32 * KC), r = (e / KC) % 32, col = e % KC;
-    const int row = 32 * (c0 + sl) + 1 + r;
-    sm.Zs[sl][r][col] = (in_lds(c0 + sl) && row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
+    const int q = e / (32 * KC), r = (e / KC) % 32, col = e % KC;
+    const int c = G0 + q, row = 32 * c + 1 + r;
+    sm.Zs[c % RS][r][col] = (row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
   }
   if (tid < QW) sm.done[tid] = 0u;
   if (tid == 0) sm.dead = 0u;
   __syncthreads();
-  if (c < a.smax) {
-    const int hi = min(c, a.ng2 - 1);
-    const bool g0 = !in_lds(c), g1 = !in_lds(c + 1);
-    const int s0 = c - c0, s1 = c + 1 - c0;  // LDS slots (when in LDS)
-    Q2Pre pre;
-    q2l_fetch(a, hi, c - hi, pre);
-    for (int G2 = hi, t = 0; G2 >= 0; --G2, ++t) {
-      const int s = c - G2, j0 = G2 * QB, rb0 = j0 + 1 + s * SB_B;
-      // (G2, c - 1) and (G2 + 1, c + 1): one level earlier, sharing a chunk
-      if (c > 0 && G2 <= min(c - 1, a.ng2 - 1)) {
-        const unsigned need = unsigned(min(c - 1, a.ng2 - 1) - G2 + 1);
-        if (q > 0) q2l_wait(&sm.done[q - 1], need, &sm.dead, a.stall, a.timeout);
-        else if (!q2l_get(&sm.dead) && !tg::spin_geq(a.gprog + c - 1, need, a.stall, a.timeout))
-          sm.dead = 1u;
-      }
-      if (c + 1 < a.smax && G2 + 1 <= min(c + 1, a.ng2 - 1)) {
-        const unsigned need = unsigned(min(c + 1, a.ng2 - 1) - G2);
-        if (q < QW - 1) q2l_wait(&sm.done[q + 1], need, &sm.dead, a.stall, a.timeout);
-        else if (!q2l_get(&sm.dead) && !tg::spin_geq(a.gprog + c + 1, need, a.stall, a.timeout))
-          sm.dead = 1u;
-      }
-      // Z tile: rows i < 32 from chunk c, i >= 32 from chunk c + 1
-      doublex4 F[4][NCB];
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const bool gl = rb < 2 ? g0 : g1;
-        const int sl = rb < 2 ? s0 : s1;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int i = rb * 16 + lr + 4 * qq, r = i & 31, row = rb0 + i;
-          const bool ok = i < QR && row < n;
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) {
-            const int col = cb * 16 + lc;
-            double v;
-            if (gl)
-              v = __hip_atomic_load(&a.Z[int64_t(min(row, n - 1)) * k + min(col, k - 1)],
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              v = sm.Zs[sl][r][col];
-            F[rb][cb][qq] = (ok && col < k) ? v : 0.0;
-          }
-        }
-      }
-      double(*Vs)[SB_B + 1] = sm.Vs[q];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int idx = lane + 64 * u, r = idx >> 5, d = idx & 31;
-        Vs[r][d] = refl_valid(n, j0 + r, s) ? pre.vv[u] : 0.0;
-      }
-      double tv[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) tv[u] = pre.tt[u];
-      // next block's reflectors: in flight through this block's arithmetic
-      if (G2 > 0) q2l_fetch(a, G2 - 1, s + 1, pre);
-      wave_sync();
-      auto yval = [&](int i, int cc) -> double {
-        const int d = i - cc;
-        return (d >= 0 && d < SB_B) ? Vs[cc][d] : 0.0;
-      };
-      doublex4 Pa[2][NCB];
-#pragma unroll
-      for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int i = rb * 16 + 4 * qq + lr;
-          double ya[2];
-#pragma unroll
-          for (int ia = 0; ia < 2; ++ia) ya[ia] = yval(i, ia * 16 + lc);
-#pragma unroll
-          for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-              Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][qq], Pa[ia][cb], 0,
-                                                                0, 0);
-        }
-      doublex4 Ma[2][NCB];
-#pragma unroll
-      for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) Ma[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int kk = kb * 16 + 4 * qq + lr;
-          (void)kk;
-#pragma unroll
-          for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-              Ma[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[(kb * 4 + qq) * 2 + ia],
-                                                                Pa[kb][cb][qq], Ma[ia][cb], 0, 0, 0);
-        }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int kk = kb * 16 + 4 * qq + lr;
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb) {
-            const double ya = -yval(rb * 16 + lc, kk);
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-              F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][qq], F[rb][cb], 0, 0,
-                                                               0);
-          }
-        }
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const bool gl = rb < 2 ? g0 : g1;
-        const int sl = rb < 2 ? s0 : s1;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int i = rb * 16 + lr + 4 * qq, r = i & 31, row = rb0 + i;
-          if (i >= QR || row >= n) continue;
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) {
-            const int col = cb * 16 + lc;
-            if (col >= k) continue;
-            if (gl)
-              __hip_atomic_store((gu64 *)&a.Z[int64_t(row) * k + col],
-                                 __double_as_longlong(F[rb][cb][qq]), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-            else
-              sm.Zs[sl][r][col] = F[rb][cb][qq];
-          }
-        }
-      }
-      // publish block t + 1 of column c: LDS release (this wave's Z stores to
-      // LDS before it); the boundary columns also to their global word after
-      // draining their write-through stores
-      __hip_atomic_store(&sm.done[q], unsigned(t + 1), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (q == 0 || q == QW - 1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store((gu32 *)(a.gprog + c), unsigned(t + 1), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      wave_sync();  // Vs reused by the next block
+  const int nb = g <= gtop ? q2l_nb(n, G2) : 0;
+  const int nbu = G2 + 1 < a.ng2 ? q2l_nb(n, G2 + 1) : 0;  // blocks of the group above
+  Q2Pre pre;
+  if (nb > 0) q2l_fetch(a, G2, 0, pre);
+  for (int s = 0; s < nb; ++s) {
+    const int j0 = G2 * QB, c = G2 + s, rb0 = j0 + 1 + s * SB_B;
+    // (G2 + 1, s) -- or, for the last block, all of group G2 + 1
+    if (nbu > 0) {
+      const unsigned need = unsigned(min(s + 1, nbu));
+      if (g < gtop) q2l_wait(&sm.done[g + 1], need, &sm.dead, a.stall, a.timeout);
+      else if (!q2l_get(&sm.dead) && !tg::spin_geq(a.gprog + G2 + 1, need, a.stall, a.timeout))
+        sm.dead = 1u;
     }
-  }
-  __syncthreads();
-  // write back this workgroup's LDS chunks (read by later launches)
-  for (int e = tid; e < QW * 32 * KC; e += 64 * QW) {
-    const int sl = e / (32 * KC), r = (e / KC) % 32, col = e % KC;
-    const int row = 32 * (c0 + sl) + 1 + r;
-    if (in_lds(c0 + sl) && row < n && col < k) a.Z[int64_t(row) * k + col] = sm.Zs[sl][r][col];
+    // the top wave brings chunk c + 1 into the ring: its slot held chunk
+    // c + 1 - RS, done once the lowest wave finished that as a first chunk
+    const bool from_g = g == gtop;
+    if (from_g) {
+      const int prev = c + 1 - RS - G0;  // the lowest wave's block that released the slot
+      if (prev >= 0) q2l_wait(&sm.done[0], unsigned(prev + 1), &sm.dead, a.stall, a.timeout);
+    }
+    // Z tile: rows i < 32 from chunk c (LDS), i >= 32 from chunk c + 1 (LDS,
+    // or global for the top wave)
+    doublex4 F[4][NCB];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const bool gl = rb >= 2 && from_g;
+      const int sl = (rb < 2 ? c : c + 1) % RS;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int i = rb * 16 + lr + 4 * qq, r = i & 31, row = rb0 + i;
+        const bool ok = i < QR && row < n;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int col = cb * 16 + lc;
+          double v;
+          if (gl)
+            v = __hip_atomic_load(&a.Z[int64_t(min(row, n - 1)) * k + min(col, k - 1)],
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            v = sm.Zs[sl][r][col];
+          F[rb][cb][qq] = (ok && col < k) ? v : 0.0;
+        }
+      }
+    }
+    double(*Vs)[SB_B + 1] = sm.Vs[g];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = lane + 64 * u, r = idx >> 5, d = idx & 31;
+      Vs[r][d] = refl_valid(n, j0 + r, s) ? pre.vv[u] : 0.0;
+    }
+    double tv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tv[u] = pre.tt[u];
+    // next block's reflectors: in flight through this block's arithmetic
+    if (s + 1 < nb) q2l_fetch(a, G2, s + 1, pre);
+    wave_sync();
+    auto yval = [&](int i, int cc) -> double {
+      const int d = i - cc;
+      return (d >= 0 && d < SB_B) ? Vs[cc][d] : 0.0;
+    };
+    doublex4 Pa[2][NCB];
+#pragma unroll
+    for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) Pa[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int i = rb * 16 + 4 * qq + lr;
+        double ya[2];
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia) ya[ia] = yval(i, ia * 16 + lc);
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+            Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][qq], Pa[ia][cb], 0,
+                                                              0, 0);
+      }
+    doublex4 Ma[2][NCB];
+#pragma unroll
+    for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) Ma[ia][cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+            Ma[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[(kb * 4 + qq) * 2 + ia],
+                                                              Pa[kb][cb][qq], Ma[ia][cb], 0, 0, 0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int kk = kb * 16 + 4 * qq + lr;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const double ya = -yval(rb * 16 + lc, kk);
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb)
+            F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][qq], F[rb][cb], 0, 0, 0);
+        }
+      }
+    // stores: the lowest wave hands its first chunk (and, at its last block,
+    // the second) to global memory write-through; everything else to the ring
+    const bool last = s + 1 == nb;
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const bool gl = g == 0 && (rb < 2 || last);
+      const int sl = (rb < 2 ? c : c + 1) % RS;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int i = rb * 16 + lr + 4 * qq, r = i & 31, row = rb0 + i;
+        if (i >= QR || row >= n) continue;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int col = cb * 16 + lc;
+          if (col >= k) continue;
+          if (gl)
+            __hip_atomic_store((gu64 *)&a.Z[int64_t(row) * k + col],
+                               __double_as_longlong(F[rb][cb][qq]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          else
+            sm.Zs[sl][r][col] = F[rb][cb][qq];
+        }
+      }
+    }
+    // publish block s: LDS release (this wave's ring stores before it); the
+    // lowest wave also to its global word after draining its sc1 stores
+    __hip_atomic_store(&sm.done[g], unsigned(s + 1), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (g == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store((gu32 *)(a.gprog + G2), unsigned(s + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    wave_sync();  // Vs reused by the next block
   }
 }
 
@@ -1066,12 +1060,12 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   const XcdInfo xq = xcd_info();
   {
     const char *ql = getenv("TG_BT_Q2_LDS");  // development switch, read per call
-    const int Wq = cdiv(a.smax, QW);
-    // (k <= 16: one 16-column block; with two, 49 registers spill at the
+    const int Wq = cdiv(a.ng2, QW);
+    // (k <= 16: one 16-column block; with two, registers spill at the
     // 256-VGPR cap of two waves per SIMD, so k = 17 .. 32 keeps bt_few's Q2)
     if (!(ql && ql[0] == '0') && !a.q2_wave && a.nlev2 > 0 && k <= 16 &&
         Wq <= xq.xcds * xq.cus_per_xcd) {
-      e = hipMemsetAsync(a.colflag, 0, ((size_t(a.smax) * 4 + 15) & ~size_t(15)), st);
+      e = hipMemsetAsync(a.colflag, 0, ((size_t(a.ng2) * 4 + 15) & ~size_t(15)), st);
       if (e != hipSuccess) return e;
       Q2LArgs qa{Z, n, k, b.V2, b.T2, a.smax, a.ng2, a.colflag, cnt + 1, a.timeout};
       auto tq = prof_begin(st, PROF_Q2, 0.0, 0.0);

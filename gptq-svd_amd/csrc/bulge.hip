@@ -1107,6 +1107,18 @@ __global__ __launch_bounds__(DBT) void bulge_df_kernel(double *__restrict__ B, i
               df_wait(&sy.loaded, unsigned(min(n, j + 1 + (sp + 1) * SB_B)), sy, stall, timeout);
             else
               need_prev(sp + 2, role != 1);
+            // D (q, s) overlaps G (q - 1, s) in its last row (r1 + b - 1).
+            // That G block's rank-1 update is normally deferred to A (q - 1,
+            // s + 1), which need_prev waits for -- but the LAST task of sweep
+            // q - 1 has no next task and applies it itself, and a 1-row G
+            // block remains when n - r1' = b + 1.  So D of the task with the
+            // previous sweep's last index waits for that sweep's G roles too.
+            // (Found by the tridiagonal guard: ~1 in 7000 launches at n = 384
+            // let D read the row before the store, moving the last 32 d by
+            // up to 9e-2 -- the round-5 symptom, whose compiler barrier had
+            // only shifted its timing.)
+            if (role == 1 && q > 0 && s == ntp - 1)
+              df_wait(&sy.cnt[2][q - 1], unsigned(ntp + 1), sy, stall, timeout);
           }
           DF_ACC(1)
           auto wait_v = [&]() {

@@ -61,8 +61,14 @@ struct PivWs {
   double *Lpp;      // PB x PB  L rows of the panel's pivots (panel columns)
   double *Hk2;      // n x n  second buffer: the compacted Schur complements alternate
   int32_t *oidx;    // n  new position ps + x -> its compact index in the panel's H_k
+  // candidate block (piv_sel_kernel<SEL_SELECT / SEL_STEPS>)
+  int32_t *cand;    // SEL + 8: candidate rows, then [SEL] nset, [SEL+1] bp, [SEL+2] brow, [SEL+3] bo
+  double *cselv;    // 2: tau, bv (the selection's bound and step-0 maximum)
+  int32_t *cidx;    // n: compact index (next panel) -> candidate slot, or -1
+  double *Cc;       // SEL x SEL: H_k of the candidate pairs, by slot (both triangles)
 };
 constexpr int PPS = PB + 8;  // partial / broadcast record (doubles)
+constexpr int SEL_WS = 1024;  // = SEL (candidates), for the workspace layout above it
 static_assert(PGMAX * PPS % 256 == 0, "slot copy assumes whole rounds of 256 threads");
 
 // The candidate-set pivot order with compacted Schur complements (two n x n
@@ -104,6 +110,10 @@ void piv_layout(A &ar, int n, int k, PivWs *p) {
   take(q.Lpp, PB * PB);
   take2m(q.Hk2, compact_pivot(n) ? size_t(n) * n : size_t(1));
   take(q.oidx, n);
+  take(q.cand, SEL_WS + 8);
+  take(q.cselv, 2);
+  take(q.cidx, n);
+  take(q.Cc, compact_pivot(n) ? size_t(SEL_WS) * SEL_WS : size_t(1));
 }
 
 // B[t][c] = S[t] * Vh[t][c]    (gptq_utils.py:112)
@@ -564,7 +574,7 @@ __global__ __launch_bounds__(256) void piv_panel_kernel(int n, int k, int ps, in
 // Each panel's Schur update writes the next compacted block into the other
 // buffer (syrk_compact_kernel), so the update touches (n - ps)^2 entries
 // instead of n^2 and a pivot's row is contiguous.
-constexpr int SEL = 1024;         // candidates
+constexpr int SEL = SEL_WS;       // candidates
 constexpr int SEL_LDS_N = 8192;  // n up to which piv_sel_kernel stages diagonals in LDS
 
 #ifdef TG_SEL_PHASES
@@ -732,6 +742,23 @@ __device__ inline void hist_scan(const unsigned *hist, int target, int *out) {
   }
 }
 
+// Modes of piv_sel_kernel.  SEL_FULL: candidate selection, then the panel's
+// steps (pivot rows gathered from the compacted H_k).  The candidate-block
+// form (the default; TG_PIV_CC=0 keeps SEL_FULL) splits it around the
+// previous panel's Schur update: SEL_SELECT picks the candidates first and
+// maps their compact indices (w.cidx, tagged with the panel start), the
+// update then also writes H_k of every candidate pair into the SEL x SEL
+// block w.Cc (syrk_compact_p_kernel's epilogue, exact copies of the values it
+// stores), and SEL_STEPS runs the steps reading a pivot's row of candidate
+// entries as 8 KB contiguous from Cc instead of ~1024 scattered lines of H_k
+// (half of them column reads of the lower-triangle storage: the TA-bound
+// part of a step).  Same values, same operations: perm and R_x are
+// bit-identical.
+enum { SEL_FULL = 0, SEL_SELECT = 1, SEL_STEPS = 2 };
+constexpr int CC_TAG = 11;  // cidx = (panel start << CC_TAG) | slot
+static_assert((1 << CC_TAG) > SEL, "slot field");
+
+template <int MODE>
 __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
                                                       const double *__restrict__ Hc) {
   extern __shared__ int permL[];  // n: position -> row
@@ -746,7 +773,7 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ps = w.sstate[0];
   if (ps >= k) {
-    if (tid == 0) w.sstate[1] = 0;
+    if (tid == 0 && MODE != SEL_SELECT) w.sstate[1] = 0;
     return;
   }
   const int pe = min(ps + PB, k);
@@ -754,6 +781,24 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
   uint64_t selt_last = 0;
 #endif
   SELT(0)
+  int nset, bp, brow, bo;
+  double tau, bv;
+  const double *dS;
+  const int32_t *pS;
+  if constexpr (MODE == SEL_STEPS) {
+    // the selection SEL_SELECT made before the Schur update
+    for (int x = tid; x < n; x += STH) permL[x] = w.perm[x];
+    for (int c = tid; c < SEL; c += STH) cand[c] = w.cand[c];
+    nset = w.cand[SEL];
+    bp = w.cand[SEL + 1];
+    brow = w.cand[SEL + 2];
+    bo = w.cand[SEL + 3];
+    tau = w.cselv[0];
+    bv = w.cselv[1];
+    dS = w.dsc;
+    pS = w.pos;
+    __syncthreads();
+  } else {
   // Schur diagonals and positions: staged in LDS once for n <= SEL_LDS_N (the
   // selection passes below read them three times), else read from HBM/L2
   const bool staged = n <= SEL_LDS_N;
@@ -788,8 +833,8 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
   }
   __syncthreads();
   SELT(9)
-  const double *dS = staged ? dsh : w.dsc;
-  const int32_t *pS = staged ? posh : w.pos;
+  dS = staged ? dsh : w.dsc;
+  pS = staged ? posh : w.pos;
   // --- candidate set ---------------------------------------------------------
   // one sweep: count of unpivoted rows with positive keys + exponent histogram
   int valid = 0;
@@ -849,8 +894,10 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
   // compaction of the set, tau over the rest, full argmax for step 0 (branch-free;
   // membership kept as one bit per row of this thread: n <= 64 STH)
   int mine = 0;
-  double tau = -INFINITY, bv = -INFINITY;
-  int bp = n, brow = 0;
+  tau = -INFINITY;
+  bv = -INFINITY;
+  bp = n;
+  brow = 0;
   unsigned long long insm = 0ull;
   for (int r0 = tid, bi = 0; r0 < n; r0 += 8 * STH, bi += 8) {
     double dv[8];
@@ -909,11 +956,29 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
   }
   __syncthreads();
   SELT(12)
-  int nset = 0;
+  nset = 0;
 #pragma unroll
   for (int q = 0; q < STH / 64; ++q) nset += scnt[q];
-  int bo = bp - ps;  // compact index of the step-0 pivot (positions unchanged so far)
+  bo = bp - ps;  // compact index of the step-0 pivot (positions unchanged so far)
   block_argmax_sel(bv, bp, brow, bo, rec, reco);
+  if constexpr (MODE == SEL_SELECT) {
+    for (int c = tid; c < nset; c += STH) {
+      w.cand[c] = cand[c];
+      // compact index (this panel's numbering) -> slot, tagged with the panel
+      // start so entries of earlier panels never match (one store per entry)
+      w.cidx[pS[cand[c]] - ps] = (ps << CC_TAG) | c;
+    }
+    if (tid == 0) {
+      w.cand[SEL] = nset;
+      w.cand[SEL + 1] = bp;
+      w.cand[SEL + 2] = brow;
+      w.cand[SEL + 3] = bo;
+      w.cselv[0] = tau;
+      w.cselv[1] = bv;
+    }
+    return;
+  }
+  }  // MODE != SEL_STEPS
   int rc[CPT], posc[CPT], oc[CPT];
   double dc[CPT];
   bool done[CPT];
@@ -930,6 +995,7 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
     for (int l = 0; l < PB; ++l) lr[u][l] = 0.0;
   }
   int piv = brow, q = bp, opiv = bo;
+  int cpiv = -1;  // SEL_STEPS: the pivot's candidate slot (step 0: from H_k)
   double dpiv = bv;
   int tdone = 0;
   SELT(1)
@@ -949,7 +1015,8 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
         v = take ? dc[u] : v;
         p = take ? posc[u] : p;
         r = take ? rc[u] : r;
-        o = take ? oc[u] : o;
+        // SEL_STEPS: the candidate slot rides along above the compact index
+        o = take ? (MODE == SEL_STEPS ? oc[u] | ((tid + u * STH + 1) << 16) : oc[u]) : o;
       }
       SELT(4)
       block_argmax_sel(v, p, r, o, rec, reco);
@@ -959,12 +1026,19 @@ __global__ __launch_bounds__(STH) void piv_sel_kernel(int n, int k, PivWs w,
       dpiv = v;
       q = p;
       piv = r;
-      opiv = o;
+      opiv = MODE == SEL_STEPS ? (o & 0xffff) : o;
+      cpiv = MODE == SEL_STEPS ? (o >> 16) - 1 : -1;
     }
     double hv[CPT];
+    if (MODE == SEL_STEPS && cpiv >= 0) {  // uniform: the pivot's candidate row of Cc
+      const double *crow = w.Cc + size_t(cpiv) * SEL;
 #pragma unroll
-    for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
-      hv[u] = Hc[hk_at(opiv, oc[u], n)];  // unconditional; masked below
+      for (int u = 0; u < CPT; ++u) hv[u] = crow[tid + u * STH];
+    } else {
+#pragma unroll
+      for (int u = 0; u < CPT; ++u)  // H_k[piv][candidate], issued before the hand-off
+        hv[u] = Hc[hk_at(opiv, oc[u], n)];  // unconditional; masked below
+    }
 #pragma unroll
     for (int u = 0; u < CPT; ++u)
       if (rc[u] == piv) {
@@ -1190,10 +1264,13 @@ __global__ __launch_bounds__(256) void syrk_compact_kernel(int n, PivWs w,
 // tile is multiplied and written (its row / column indices one step earlier
 // still), so the memory pipe does not idle through each workgroup's MFMA,
 // epilogue and dispatch.  Same arithmetic per entry as syrk_compact_kernel.
+// cc: also write H_k of every pair of the next panel's candidates (w.cidx
+// entries tagged with this update's ps2) into w.Cc, both triangles, by slot
+// (piv_sel_kernel<SEL_STEPS>) -- copies of the values stored to Hn.
 __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
                                                                 const double *__restrict__ Hc,
                                                                 double *__restrict__ Hn,
-                                                                int mirror) {
+                                                                int mirror, int cc) {
   __shared__ double li[PB][64], lj[PB][64];
   __shared__ double tt[64][65];
   const int tid = threadIdx.x;
@@ -1238,9 +1315,22 @@ __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
   load_old(ro, co, old);
   const int G = int(gridDim.x);
   if (b + G < tiles) load_idx(b + G, ro, co);
+  const int ctag = ps2 << CC_TAG;
   for (; b < tiles; b += G) {
     int i0, j0;
     tile_ij(b, i0, j0);
+    // candidate slots of this thread's rows and columns (-1: not a candidate
+    // of the next panel); loads in flight through the tile's MFMA
+    int crs[2][4], ccs[2];
+    if (cc) {
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          crs[ib][q] = w.cidx[min(i0 + wm * 32 + ib * 16 + lk + 4 * q, nc - 1)];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) ccs[jb] = w.cidx[min(j0 + wn * 32 + jb * 16 + lr, nc - 1)];
+    }
     __syncthreads();  // the previous tile's reads of li, lj, tt are done
     double lv[8][2];
 #pragma unroll
@@ -1291,6 +1381,12 @@ __global__ __launch_bounds__(256, 2) void syrk_compact_p_kernel(int n, PivWs w,
           const int gi = i0 + rl, gj = j0 + cl;
           if (gi < nc && gj < nc && (mirror || gi >= gj)) Hn[size_t(gi) * n + gj] = acc[ib][jb][q];
           tt[cl][rl] = acc[ib][jb][q];
+          if (cc && gi < nc && gj < nc && gi >= gj && (crs[ib][q] & ~(SEL_WS * 2 - 1)) == ctag &&
+              (ccs[jb] & ~(SEL_WS * 2 - 1)) == ctag) {
+            const int a = crs[ib][q] & (SEL_WS * 2 - 1), c2 = ccs[jb] & (SEL_WS * 2 - 1);
+            w.Cc[size_t(a) * SEL + c2] = acc[ib][jb][q];
+            w.Cc[size_t(c2) * SEL + a] = acc[ib][jb][q];
+          }
         }
     if (i0 != j0 && mirror) {  // uniform: mirror rows j0 .. j0 + 63, columns i0 .. i0 + 63
       __syncthreads();
@@ -1894,9 +1990,14 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   TG_LAUNCHED();
   const size_t lds = sizeof(int) * size_t((n + 1) & ~1) +
                      (n <= SEL_LDS_N ? (sizeof(double) + sizeof(int)) * size_t(n) : 0);
-  if (lds > 48 * 1024)
-    TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel,
+  if (lds > 48 * 1024) {
+    TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel<SEL_FULL>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel<SEL_SELECT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+    TG_HIP(hipFuncSetAttribute((const void *)piv_sel_kernel<SEL_STEPS>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+  }
   // TG_SYR2K_PERSIST=0: one tile per workgroup (development switch, per call)
   const char *ps = getenv("TG_SYR2K_PERSIST");
   const bool persist = !(ps && ps[0] == '0');
@@ -1909,11 +2010,16 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   // compacted Schur complements alternate between the two buffers
   const double *hc = w.Hk;
   double *hn = w.Hk2;
-  auto schur_compact = [&](int rows) -> hipError_t {
+  // TG_PIV_CC=0: the steps gather pivot rows from H_k (SEL_FULL) instead of
+  // the candidate block (development switch, per call; the block needs the
+  // persistent Schur update)
+  const char *pc = getenv("TG_PIV_CC");
+  const bool ccb = persist && !(pc && pc[0] == '0');
+  auto schur_compact = [&](int rows, int cc = 0) -> hipError_t {
     const int nt = tg::cdiv(rows, 64);
     if (persist)
       hipLaunchKernelGGL(syrk_compact_p_kernel, dim3(std::min(nt * (nt + 1) / 2, 2 * ncu)),
-                         dim3(256), 0, st, n, w, hc, hn, mirror);
+                         dim3(256), 0, st, n, w, hc, hn, mirror, cc);
     else
       hipLaunchKernelGGL(syrk_compact_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, st, n, w, hc,
                          hn, mirror);
@@ -1923,7 +2029,11 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
     hn = t;
     return e;
   };
+  if (ccb) TG_HIP(hipMemsetAsync(w.cidx, 0xff, sizeof(int32_t) * size_t(n), st));  // no tags
   int done = 0;
+  // a panel's Schur update runs at the head of the next panel: with the
+  // candidate block, between that panel's selection and its steps
+  int pend_rows = 0;  // rows of the pending update (0: none)
   for (int round = 0;; ++round) {
     if (round > 4 * (k / PB + 2)) {
       tg::set_error("pivot order: no progress after %d rounds (%d of %d steps)", round, done, k);
@@ -1933,20 +2043,32 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
     // every panel starts at or after `done + p` steps: grids sized for that bound
     for (int p = 0; p < P; ++p) {
       const int rows = n - (done + p);
+      if (ccb && pend_rows > 0) {
+        auto tk = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n) * 2, 0.0);
+        hipLaunchKernelGGL(piv_sel_kernel<SEL_SELECT>, dim3(1), dim3(STH), lds, st, n, k, w, hc);
+        tg::prof_end(st, tk);
+        TG_LAUNCHED();
+        TG_HIP(schur_compact(pend_rows, 1));
+      } else if (pend_rows > 0) {
+        TG_HIP(schur_compact(pend_rows));
+      }
       auto tok = tg::prof_begin(st, tg::PROF_PIVSTEP, 8.0 * double(n) * PB * 3, 0.0);
-      hipLaunchKernelGGL(piv_sel_kernel, dim3(1), dim3(STH), lds, st, n, k, w, hc);
+      if (ccb && pend_rows > 0)
+        hipLaunchKernelGGL(piv_sel_kernel<SEL_STEPS>, dim3(1), dim3(STH), lds, st, n, k, w, hc);
+      else
+        hipLaunchKernelGGL(piv_sel_kernel<SEL_FULL>, dim3(1), dim3(STH), lds, st, n, k, w, hc);
       // one wave per workgroup: the gathers of the pivots' columns spread
       // over 4x the CUs of 256-thread groups (n = 12,288: -1.4 ms per solve)
       hipLaunchKernelGGL(piv_fill_kernel<64>, dim3(tg::cdiv(rows, 64)), dim3(64), 0, st, n, k, w, hc);
       tg::prof_end(st, tok);
       TG_LAUNCHED();
-      if (p + 1 < P) TG_HIP(schur_compact(rows));
+      pend_rows = rows;
     }
     int32_t h = 0;
     TG_HIP(hipMemcpyAsync(&h, w.sstate, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     TG_HIP(hipStreamSynchronize(st));
     if (h >= k) break;
-    TG_HIP(schur_compact(n - (done + P - 1)));  // the round's last panel
+    pend_rows = n - (done + P - 1);  // the round's last panel, updated at the next one's head
     done = h;
   }
   return 0;
@@ -2463,6 +2585,72 @@ extern "C" int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, in
                   h.info);
     return int(hipErrorUnknown);
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// The explicit-form U factor in column-sharded pieces (multi-GPU,
+// gptq_svd_amd.dist.u_factor_rx_sharded): rank r computes C[:, c0:c1] =
+// R11^-1 R12[:, c0:c1] (tg_urx_c), the ranks all-gather C, every rank forms
+// U11 = V^-1 from the whole C (tg_urx_u11: Z, N, one k x k Cholesky, the
+// triangular inverse -- replicated), then rank r its U12 columns V^-1 C[:,
+// c0:c1] (tg_urx_u12) and the ranks all-gather U12.  Every C and U12 entry
+// depends on its own column only (block back substitution, GEMMs with a
+// fixed k order per entry), so the gathered U equals tg_u_factor_rx's
+// explicit form bit for bit (tests/test_gpu_urx_sharded.py).  Workspace:
+// tg_ufactor_rx_workspace_size(n, k).  The small-m form (m * 16 <= k, the
+// near-full-rank layers) is not sharded: its C is a sliver.
+// ---------------------------------------------------------------------------
+extern "C" int tg_urx_c(void *stream, const double *Rx, int ldr, int n, int k, int c0, int c1,
+                        double *C, int ldc, void *ws, size_t ws_bytes) {
+  TG_ARG(Rx, 2, "null Rx");
+  TG_ARG(ldr >= n, 3, "ldr < n");
+  TG_ARG(k >= 1 && k <= n, 5, "k must be in [1, n]");
+  TG_ARG(c0 >= 0 && c0 <= c1 && c1 <= n - k, 6, "column range outside [0, n - k]");
+  TG_ARG(C || c1 == c0, 8, "null C");
+  TG_ARG(ldc >= c1 - c0, 9, "ldc < c1 - c0");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  double *S, *Y, *Bm, *A, *Tt, *Wb, *Rq;
+  int *info;
+  RefineWs rw{};
+  urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info, &Rq, &rw);
+  TG_WS(ar);
+  if (c1 == c0) return 0;
+  if (const int e = urx_diag_inverses(st, Rx, ldr, k, Y, Tt)) return e;
+  return trsm_upper_blocks(st, Rx, ldr, k, Rx + k + c0, c1 - c0, Y, k, A, C, ldc);
+}
+
+extern "C" int tg_urx_u11(void *stream, const double *Rx, int ldr, int n, int k, const double *C,
+                          int ldc, double *U, int ldu, void *ws, size_t ws_bytes) {
+  TG_ARG(Rx, 2, "null Rx");
+  TG_ARG(ldr >= n, 3, "ldr < n");
+  TG_ARG(k >= 1 && k <= n, 5, "k must be in [1, n]");
+  TG_ARG(C || n == k, 6, "null C");
+  TG_ARG(ldc >= n - k, 7, "ldc < n - k");
+  TG_ARG(U, 8, "null U");
+  TG_ARG(ldu >= n, 9, "ldu < n");
+  hipStream_t st = (hipStream_t)stream;
+  tg::Arena ar(ws, ws_bytes);
+  double *S, *Y, *Bm, *A, *Tt, *Wb, *Rq;
+  int *info;
+  RefineWs rw{};
+  urx_layout(ar, n, k, &S, &Y, &Bm, &A, &Tt, &Wb, &info, &Rq, &rw);
+  TG_WS(ar);
+  TG_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  return urx_u11_from_c(st, Rx, ldr, n, k, C, ldc, U, ldu, Y, S, A, Rq, Tt, Wb, info, rw);
+}
+
+extern "C" int tg_urx_u12(void *stream, const double *U, int ldu, int k, const double *C, int ldc,
+                          int ncols, double *out, int ldo) {
+  TG_ARG(U, 2, "null U");
+  TG_ARG(ldu >= k, 3, "ldu < k");
+  TG_ARG(k >= 1, 4, "k < 1");
+  TG_ARG(ncols >= 0, 7, "ncols < 0");
+  TG_ARG((C && out) || ncols == 0, 5, "null C / out");
+  TG_ARG(ldc >= ncols && ldo >= ncols, 6, "ldc / ldo < ncols");
+  if (ncols == 0) return 0;
+  TG_HIP(tg::dgemm_upper_a((hipStream_t)stream, k, ncols, k, 1.0, U, ldu, C, ldc, 0.0, out, ldo));
   return 0;
 }
 

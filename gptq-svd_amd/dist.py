@@ -110,3 +110,88 @@ def quantize_rows_sharded(W: torch.Tensor, U: torch.Tensor, perm: torch.Tensor, 
         Wq = torch.empty((0, n), dtype=W.dtype, device=W.device)
         codes = torch.empty((0, n), dtype=torch.uint8, device=W.device)
     return all_gather_rows(Wq, m, pg), all_gather_rows(codes, m, pg)
+
+
+def all_gather_cols(t: torch.Tensor, m: int, pg=None) -> torch.Tensor:
+    """Concatenate per-rank column shards (widths from shard_rows(m, ...))
+    along dim 1."""
+    world, _ = _world(pg)
+    if world == 1:
+        return t
+    return all_gather_rows(t.t().contiguous(), m, pg).t().contiguous()
+
+
+class UrxHip:
+    """The column-sharded pieces of the complement-path U factor on this
+    process's GPU (include/truncgptq.h tg_urx_c / tg_urx_u11 / tg_urx_u12)."""
+
+    def __init__(self):
+        from . import _lib
+        self.L = _lib
+
+    def small_m(self, k: int, m: int) -> bool:
+        import os
+        e = os.environ.get("TG_URX_SMALLM")  # the library's switch (factor.hip urx_small_m)
+        return e == "1" if e is not None else m * 16 <= k
+
+    def _ws(self, n, k, dev):
+        return self.L.workspace(self.L.lib.tg_ufactor_rx_workspace_size(n, k), dev)
+
+    def full(self, Rx: torch.Tensor, n: int, k: int) -> torch.Tensor:
+        L = self.L
+        U = torch.empty((k, n), dtype=torch.float64, device=Rx.device)
+        ws = self._ws(n, k, Rx.device)
+        L.call("tg_u_factor_rx", L.stream(), L.ptr(Rx), Rx.stride(0), n, k, L.ptr(U), n, L.ptr(ws),
+               ws.numel())
+        return U
+
+    def c_cols(self, Rx, n, k, c0, c1):
+        L = self.L
+        C = torch.empty((k, max(c1 - c0, 1)), dtype=torch.float64, device=Rx.device)
+        ws = self._ws(n, k, Rx.device)
+        L.call("tg_urx_c", L.stream(), L.ptr(Rx), Rx.stride(0), n, k, c0, c1, L.ptr(C),
+               C.stride(0), L.ptr(ws), ws.numel())
+        return C[:, : c1 - c0]
+
+    def u11(self, Rx, n, k, C):
+        L = self.L
+        C = C.contiguous()
+        U = torch.zeros((k, n), dtype=torch.float64, device=Rx.device)
+        ws = self._ws(n, k, Rx.device)
+        L.call("tg_urx_u11", L.stream(), L.ptr(Rx), Rx.stride(0), n, k, L.ptr(C),
+               max(C.stride(0), 1), L.ptr(U), n, L.ptr(ws), ws.numel())
+        return U
+
+    def u12(self, U, k, Cb):
+        L = self.L
+        Cb = Cb.contiguous()
+        w = Cb.shape[1]
+        out = torch.empty((k, max(w, 1)), dtype=torch.float64, device=U.device)
+        L.call("tg_urx_u12", L.stream(), L.ptr(U), U.stride(0), k, L.ptr(Cb), max(Cb.stride(0), 1),
+               w, L.ptr(out), out.stride(0))
+        return out[:, :w]
+
+
+def u_factor_rx_sharded(Rx: torch.Tensor, n: int, k: int, pg=None, ops=None) -> torch.Tensor:
+    """The complement-path U factor (tg_u_factor_rx, gptq_utils.py:118-124's
+    QR) with its column-parallel work split over the ranks of `pg`: rank r
+    forms C[:, cols_r] = R11^-1 R12[:, cols_r] (block back substitution), the
+    ranks all-gather C, every rank forms U11 = V^-1 from it (one k x k
+    Cholesky, replicated), rank r its U12 columns V^-1 C[:, cols_r], and the
+    ranks all-gather U12.  Every C / U12 column depends on its own input
+    column only, so U equals the one-process factor bit for bit
+    (tests/test_gpu_urx_sharded.py on the HIP path, tests/test_dist_urx.py on
+    gloo).  Collectives: two all-gathers of k x m doubles (1.2 GB each at
+    Llama-3-70B down_proj width with k = 21,402).  The small-m form (m * 16 <=
+    k: near-full-rank layers, where C is a sliver) and world size 1 run the
+    one-process call.  `ops`: the per-process pieces (default: UrxHip)."""
+    world, rank = _world(pg)
+    ops = ops if ops is not None else UrxHip()
+    m = n - k
+    if m <= 0 or ops.small_m(k, m):
+        return ops.full(Rx, n, k)
+    c0, c1 = shard_rows(m, world, rank)
+    C = all_gather_cols(ops.c_cols(Rx, n, k, c0, c1), m, pg)
+    U = ops.u11(Rx, n, k, C)
+    U[:, k:] = all_gather_cols(ops.u12(U, k, C[:, c0:c1]), m, pg)
+    return U

@@ -139,6 +139,23 @@ size_t tg_ufactor_rx_workspace_size(int n, int k);
 int tg_u_factor_rx(void *stream, const double *Rx, int ldr, int n, int k, double *U, int ldu,
                    void *ws, size_t ws_bytes);
 
+/* The same U factor (explicit form: m = n - k > k / 16) in column-sharded
+ * pieces for one process per GPU (gptq_svd_amd.dist.u_factor_rx_sharded; no
+ * reference counterpart: the reference is single-device, quantize.py:180-184).
+ * C = R11^-1 R12 (R11 = Rx[:, :k], R12 = Rx[:, k:]):
+ *   tg_urx_c:   C[:, c0:c1] into C (k x (c1 - c0), ld ldc);
+ *   tg_urx_u11: U[:, :k] = V^-1 from the whole C (k x (n - k), ld ldc);
+ *   tg_urx_u12: out (k x ncols, ld ldo) = U[:, :k] C_block.
+ * Each entry of C and U12 depends on its own column only, so gathering the
+ * ranks' blocks gives tg_u_factor_rx's U bit for bit.  Workspace:
+ * tg_ufactor_rx_workspace_size(n, k) for tg_urx_c / tg_urx_u11. */
+int tg_urx_c(void *stream, const double *Rx, int ldr, int n, int k, int c0, int c1, double *C,
+             int ldc, void *ws, size_t ws_bytes);
+int tg_urx_u11(void *stream, const double *Rx, int ldr, int n, int k, const double *C, int ldc,
+               double *U, int ldu, void *ws, size_t ws_bytes);
+int tg_urx_u12(void *stream, const double *U, int ldu, int k, const double *C, int ldc, int ncols,
+               double *out, int ldo);
+
 /* ---- A6: relative prediction error (log_quantization_error,
  * gptq_utils.py:275-291) ---------------------------------------------------
  * out[0] = ||W[:, perm] R^T||_F^2, out[1] = ||(W - Wq)[:, perm] R^T||_F^2
