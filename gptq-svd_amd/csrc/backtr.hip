@@ -406,14 +406,28 @@ static_assert(Q1RB >= 1 && Q1S % (16 * BW) == 0, "sub-chunk = whole 16-row block
 
 // Single-level panels (one compact-WY block of m rows, band.h SbPlan::single):
 // sub-chunks of Q1S rows, two phases with a grid barrier between them.
-// Phase A: sub-chunk I publishes P_I = Y_I^T Z_I (32 x k) to part[I].
+// Sub-chunks are aligned to absolute Z rows (sub-chunk j = rows [128 j,
+// 128 j + 128) clipped to the panel's rows), so q1_lds_kernel -- whose
+// workgroups hold fixed row ranges -- forms the same partials and sums them
+// in the same order: the two Q1 forms are bit-identical.
+// Phase A: sub-chunk I (the I-th at or below the panel) publishes
+// P_I = Y_I^T Z_I (32 x k) to part[I].
+__device__ inline void q1_sub_rows(const Q1Op &d, int I, int &g0, int &lo, int &hi) {
+  g0 = (d.r0 / Q1S + I) * Q1S;              // first Z row of the sub-chunk
+  lo = max(0, d.r0 - g0);                   // local rows [lo, hi) are the panel's
+  hi = min(Q1S, d.r0 + d.rows - g0);
+}
+__device__ inline int q1_nsub(const Q1Op &d) {
+  return (d.r0 + d.rows - 1) / Q1S - d.r0 / Q1S + 1;
+}
 template <int NCB>
 __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
                          SmQ1 &sm) {
   const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane >> 4, lc = lane & 15;
-  const int kb = I * Q1S, h = min(Q1S, d.rows - kb);
-  const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
+  int g0, lo, hi;
+  q1_sub_rows(d, I, g0, lo, hi);
+  const double *Y = a.Y + d.yoff + int64_t(g0 - d.r0) * SB_B;
   doublex4 Pa[2][NCB];
 #pragma unroll
   for (int ia = 0; ia < 2; ++ia)
@@ -424,22 +438,23 @@ __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
     double zl[4][NCB], ya[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * (16 * Q1RB) + rb * 16 + 4 * q + lr, rc = min(rl, h - 1);
+      const int rl = wid * (16 * Q1RB) + rb * 16 + 4 * q + lr, rc = min(max(rl, lo), hi - 1);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
-        zl[q][cb] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
+        zl[q][cb] = load_z(a, rz, int64_t(g0 + rc) * k + min(cb * 16 + lc, k - 1));
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia) ya[q][ia] = Y[int64_t(rc) * SB_B + ia * 16 + lc];
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int rl = wid * (16 * Q1RB) + rb * 16 + 4 * q + lr;
+      const bool act = rl >= lo && rl < hi;
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
-          const double zv = (rl < h && cb * 16 + lc < k) ? zl[q][cb] : 0.0;
-          const double yv = rl < h ? ya[q][ia] : 0.0;
+          const double zv = (act && cb * 16 + lc < k) ? zl[q][cb] : 0.0;
+          const double yv = act ? ya[q][ia] : 0.0;
           Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(yv, zv, Pa[ia][cb], 0, 0, 0);
         }
     }
@@ -468,18 +483,19 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
                          int nsub, SmQ1 &sm) {
   const int k = a.k, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane >> 4, lc = lane & 15;
-  const int kb = I * Q1S, h = min(Q1S, d.rows - kb);
-  const double *Y = a.Y + d.yoff + int64_t(kb) * SB_B;
-  double *Zs = a.Z + int64_t(d.r0 + kb) * k;
+  int g0, lo, hi;
+  q1_sub_rows(d, I, g0, lo, hi);
+  const double *Y = a.Y + d.yoff + int64_t(g0 - d.r0) * SB_B;
+  double *Zs = a.Z + int64_t(g0) * k;
   doublex4 F[Q1RB][NCB];
 #pragma unroll
   for (int rb = 0; rb < Q1RB; ++rb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int rl = wid * (16 * Q1RB) + rb * 16 + lr + 4 * q, rc = min(rl, h - 1);
+      const int rl = wid * (16 * Q1RB) + rb * 16 + lr + 4 * q, rc = min(max(rl, lo), hi - 1);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
-        F[rb][cb][q] = load_z(a, rz, int64_t(d.r0 + kb + rc) * k + min(cb * 16 + lc, k - 1));
+        F[rb][cb][q] = load_z(a, rz, int64_t(g0 + rc) * k + min(cb * 16 + lc, k - 1));
     }
   for (int idx = tid; idx < SB_B * SB_B; idx += 64 * BW) {
     double v = 0.0;
@@ -516,8 +532,8 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
 #pragma unroll
     for (int rb = 0; rb < Q1RB; ++rb) {
       const int rl = wid * (16 * Q1RB) + rb * 16 + lc;
-      const double yl = Y[int64_t(min(rl, h - 1)) * SB_B + k0 + lr];
-      const double ya = rl < h ? -yl : 0.0;
+      const double yl = Y[int64_t(min(max(rl, lo), hi - 1)) * SB_B + k0 + lr];
+      const double ya = (rl >= lo && rl < hi) ? -yl : 0.0;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm[cb], F[rb][cb], 0, 0, 0);
@@ -528,7 +544,7 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int rl = wid * (16 * Q1RB) + rb * 16 + lr + 4 * q;
-      if (rl >= h) continue;
+      if (rl < lo || rl >= hi) continue;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
         const int col = cb * 16 + lc;
@@ -677,7 +693,7 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
     for (int o = 0; o < a.nops; ++o) {
       BT_T(t0)
       const Q1Op d = a.ops[o];
-      const int nsub = (d.rows + Q1S - 1) / Q1S;
+      const int nsub = q1_nsub(d);
       for (int I = me; I < nsub; I += W) q1_big_a<NCB>(a, rz, d, I, sm.q1);
       BT_T(t1)
       grid_barrier(a, unsigned(W) * ++step);
@@ -753,7 +769,13 @@ __global__ __launch_bounds__(64 * BW) void bt_few_kernel(BtArgs a) {
 // with its previous chunk.  Same blocks, reflectors, T factors and MFMA
 // sequence as q2_block: Z is bit-identical to the level-by-level form.
 // ---------------------------------------------------------------------------
-constexpr int QW = 8;   // sweep groups (waves) per workgroup
+// TG_Q2L_QW (build-time): sweep groups (waves) per workgroup.  4 = one wave
+// per SIMD: a block's 80 FP64 MFMAs (64 cycles each) own their SIMD's
+// matrix pipe; at 8 two waves share it and the MFMA phase doubles
+#ifndef TG_Q2L_QW
+#define TG_Q2L_QW 4
+#endif
+constexpr int QW = TG_Q2L_QW;
 constexpr int RS = 16;  // chunk ring slots per workgroup
 
 struct Q2LArgs {
@@ -767,7 +789,7 @@ struct Q2LArgs {
 };
 
 template <int NCB>
-struct Q2LShared {
+struct Q2LShared {  // (QW = 4: 104 KB)
   double Zs[RS][32][16 * NCB + 1];  // chunk c in slot c % RS
   double Vs[QW][QB][SB_B + 1];
   unsigned done[QW];
@@ -820,6 +842,19 @@ __device__ inline void q2l_fetch(const Q2LArgs &a, int G2, int s, Q2Pre &p) {
 
 __device__ __forceinline__ int q2l_nb(int n, int G2) { return ntasks(n, G2 * QB); }
 
+// TG_Q2L_STATS (build-time): per-phase s_memtime cycles of every block,
+// summed over waves (wait for the group above / the ring slot, Z tile + V
+// staging, MFMA chain, stores + publish), read by the host after the launch
+#ifndef TG_Q2L_STATS
+#define TG_Q2L_STATS 0
+#endif
+#if TG_Q2L_STATS
+__device__ unsigned long long g_q2l_stats[8];
+#define Q2L_T(v) const uint64_t v = __builtin_amdgcn_s_memtime();
+#else
+#define Q2L_T(v)
+#endif
+
 template <int NCB>
 __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
   __shared__ Q2LShared<NCB> sm;
@@ -842,8 +877,12 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
   const int nbu = G2 + 1 < a.ng2 ? q2l_nb(n, G2 + 1) : 0;  // blocks of the group above
   Q2Pre pre;
   if (nb > 0) q2l_fetch(a, G2, 0, pre);
+#if TG_Q2L_STATS
+  uint64_t st[4] = {0, 0, 0, 0};
+#endif
   for (int s = 0; s < nb; ++s) {
     const int j0 = G2 * QB, c = G2 + s, rb0 = j0 + 1 + s * SB_B;
+    Q2L_T(t0)
     // (G2 + 1, s) -- or, for the last block, all of group G2 + 1
     if (nbu > 0) {
       const unsigned need = unsigned(min(s + 1, nbu));
@@ -858,9 +897,14 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
       const int prev = c + 1 - RS - G0;  // the lowest wave's block that released the slot
       if (prev >= 0) q2l_wait(&sm.done[0], unsigned(prev + 1), &sm.dead, a.stall, a.timeout);
     }
+    Q2L_T(t1)
     // Z tile: rows i < 32 from chunk c (LDS), i >= 32 from chunk c + 1 (LDS,
-    // or global for the top wave)
+    // or global for the top wave).  The block's 63 rows leave chunk c + 1's
+    // last row (i = 63) out; the top wave still carries it into the ring
+    // (x63, unchanged), since the blocks that take c + 1 as their first chunk
+    // update it
     doublex4 F[4][NCB];
+    double x63[NCB];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const bool gl = rb >= 2 && from_g;
@@ -879,6 +923,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
           else
             v = sm.Zs[sl][r][col];
           F[rb][cb][qq] = (ok && col < k) ? v : 0.0;
+          if (rb == 3 && qq == 3) x63[cb] = v;  // row i = 63 on lanes lr = 3
         }
       }
     }
@@ -894,6 +939,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
     // next block's reflectors: in flight through this block's arithmetic
     if (s + 1 < nb) q2l_fetch(a, G2, s + 1, pre);
     wave_sync();
+    Q2L_T(t2)
     auto yval = [&](int i, int cc) -> double {
       const int d = i - cc;
       return (d >= 0 && d < SB_B) ? Vs[cc][d] : 0.0;
@@ -946,9 +992,18 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
             F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][qq], F[rb][cb], 0, 0, 0);
         }
       }
+#if TG_Q2L_STATS
+    asm volatile("s_nop 0" : "+v"(F[3][0][3]));  // the chain's last MFMA issued
+#endif
+    Q2L_T(t3)
     // stores: the lowest wave hands its first chunk (and, at its last block,
     // the second) to global memory write-through; everything else to the ring
     const bool last = s + 1 == nb;
+    if (from_g && !(g == 0 && last) && lr == 3 && rb0 + 63 < n) {
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        if (cb * 16 + lc < k) sm.Zs[(c + 1) % RS][31][cb * 16 + lc] = x63[cb];
+    }
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) {
       const bool gl = g == 0 && (rb < 2 || last);
@@ -981,6 +1036,222 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     wave_sync();  // Vs reused by the next block
+#if TG_Q2L_STATS
+    const uint64_t t4 = __builtin_amdgcn_s_memtime();
+    st[0] += t1 - t0;
+    st[1] += t2 - t1;
+    st[2] += t3 - t2;
+    st[3] += t4 - t3;
+#endif
+  }
+#if TG_Q2L_STATS
+  if (lane == 0 && nb > 0) {
+    for (int x = 0; x < 4; ++x) atomicAdd(&g_q2l_stats[x], (unsigned long long)st[x]);
+    atomicAdd(&g_q2l_stats[4], (unsigned long long)nb);
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Q1 with Z resident in LDS (after q2_lds_kernel, the default for k <= 16 and
+// single-level panels; TG_BT_Q1_LDS=0 keeps bt_few_kernel's Q1).  Q1 is 127
+// panel steps (n = 4096), Z[r0:] -= Y (T (Y^T Z[r0:])) from the last panel to
+// the first; each step needs P = Y^T Z over every row at or below the
+// panel's, a reduction over the grid.  Here each workgroup holds Q1R rows of
+// Z in LDS for the whole launch: per step it forms the partials of its two
+// 128-row sub-chunks on MFMA, publishes them write-through (sc1) with one
+// arrival on a counter, waits for all W arrivals, sums the partials in
+// sub-chunk order and updates its rows -- one grid exchange per step instead
+// of bt_few's two barriers, and Z never re-read from L2.  Bit-identical to
+// bt_few's Q1 (q1_big_a / q1_big_b): the same absolute sub-chunks, each a sum
+// of eight 16-row MFMA partials in block order, the sub-chunk sum in the same
+// order (leading sub-chunks above the panel are skipped, as bt_few has none),
+// the same M = T P and Z -= Y M chains.  Partials are double-buffered by step
+// parity: a workgroup can be at most one step ahead of the slowest (the
+// arrival wait), so it never overwrites partials another is still summing.
+// ---------------------------------------------------------------------------
+constexpr int Q1W = 4;                 // waves per workgroup
+constexpr int Q1R = 256;               // Z rows per workgroup (64 per wave)
+constexpr int Q1SW = Q1R / Q1S;        // sub-chunks per workgroup
+static_assert(Q1S == 16 * BW, "a sub-chunk is bt_few's BW 16-row blocks");
+static_assert(Q1R == 2 * Q1S && Q1W == 4, "two sub-chunks of two waves' four blocks each");
+
+struct Q1LArgs {
+  double *Z;
+  int n, k;
+  const double *Y, *T;
+  const Q1Op *ops;
+  int nops;
+  double *part;     // 2 x (Q1SW W) x 512 partials (step parity, sub-chunk, 32 x 16)
+  unsigned *cnt;    // [0] arrivals (zeroed per call)
+  unsigned *stall;  // timeout flag
+  unsigned long long timeout;
+};
+
+struct Q1LShared {
+  double Zs[Q1R][17];
+  double Ys[Q1R][SB_B + 1];     // this step's Y rows (zero outside the panel)
+  double half[Q1SW][SB_B][17];  // each sub-chunk's sum over its first four blocks
+  double Ps[SB_B][17];
+  double Ts[SB_B][SB_B + 1];
+};
+
+// step d's Y rows R0 .. R0 + Q1R - 1 (0 outside the panel) and T into
+// registers: issued a step ahead, landed by the next step's staging
+struct Q1LPre {
+  double y[Q1R * SB_B / (64 * Q1W)];
+  double t[SB_B * SB_B / (64 * Q1W)];
+};
+__device__ __forceinline__ void q1l_fetch(const Q1LArgs &a, const Q1Op &d, int R0, Q1LPre &p) {
+  const int tid = threadIdx.x, col = tid & 31, rsub = tid >> 5;
+  const double *Y = a.Y + d.yoff;
+#pragma unroll
+  for (int u = 0; u < Q1R * SB_B / (64 * Q1W); ++u) {
+    const int row = R0 + u * (64 * Q1W / SB_B) + rsub;
+    // raw (clamped row): the mask waits for the load, so it is applied at staging
+    p.y[u] = Y[int64_t(min(max(row - d.r0, 0), d.rows - 1)) * SB_B + col];
+  }
+#pragma unroll
+  for (int u = 0; u < SB_B * SB_B / (64 * Q1W); ++u) p.t[u] = a.T[d.toff + tid + 64 * Q1W * u];
+}
+
+__global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
+  __shared__ Q1LShared sm;
+  const int n = a.n, k = a.k, tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane >> 4, lc = lane & 15;
+  const int W = int(gridDim.x), w = blockIdx.x, R0 = w * Q1R;
+  const int nsc = (n + Q1S - 1) / Q1S;  // sub-chunks holding rows of Z
+  for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
+    const int r = e >> 4, col = e & 15, row = R0 + r;
+    sm.Zs[r][col] = (row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
+  }
+  Q1LPre pre;
+  if (a.nops > 0) q1l_fetch(a, a.ops[0], R0, pre);
+  for (int o = 0; o < a.nops; ++o) {
+    const Q1Op d = a.ops[o];
+    const int rend = d.r0 + d.rows;
+#pragma unroll
+    for (int u = 0; u < Q1R * SB_B / (64 * Q1W); ++u) {
+      const int rl = u * (64 * Q1W / SB_B) + (tid >> 5), row = R0 + rl;
+      sm.Ys[rl][tid & 31] = (row >= d.r0 && row < rend) ? pre.y[u] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < SB_B * SB_B / (64 * Q1W); ++u) {
+      const int e = tid + 64 * Q1W * u;
+      sm.Ts[e >> 5][e & 31] = pre.t[u];
+    }
+    __syncthreads();
+    // the 16-row blocks' partials Y^T Z (rows outside the panel: 0)
+    doublex4 Pa[4][2];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int blk = wid * 4 + rb;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia) Pa[rb][ia] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = blk * 16 + 4 * q + lr, row = R0 + rl;
+        const bool act = row >= d.r0 && row < rend;
+        const double zv = act ? sm.Zs[rl][lc] : 0.0;
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia)
+          Pa[rb][ia] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.Ys[rl][ia * 16 + lc], zv, Pa[rb][ia],
+                                                            0, 0, 0);
+      }
+    }
+    // sub-chunk sums over its eight blocks in order (bt_few: wave b's block
+    // is block b): the even wave sums blocks 0..3, the odd wave continues
+    // with 4..7 and publishes write-through
+    const int sc = wid >> 1;
+    if ((wid & 1) == 0) {
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double v = 0.0;
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) v += Pa[rb][ia][q];
+          sm.half[sc][ia * 16 + lr + 4 * q][lc] = v;
+        }
+    }
+    __syncthreads();
+    if (wid & 1) {
+      double *mine = a.part + (size_t(o & 1) * Q1SW * W + size_t(w) * Q1SW + sc) * 512;
+#pragma unroll
+      for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = ia * 16 + lr + 4 * q;
+          double v = sm.half[sc][r][lc];
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) v += Pa[rb][ia][q];
+          __hip_atomic_store(&mine[r * 16 + lc], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores drained
+    __syncthreads();
+    // the next step's Y and T: in flight through the exchange below (issued
+    // after the drain, which would otherwise wait for them too)
+    if (o + 1 < a.nops) q1l_fetch(a, a.ops[o + 1], R0, pre);
+    if (wid == 0) {
+      tg::wave_arrive(a.cnt);
+      tg::spin_geq(a.cnt, unsigned(W) * unsigned(o + 1), a.stall, a.timeout);
+    }
+    __syncthreads();
+    // P = sum of the sub-chunk partials from the panel's first, in order:
+    // each thread's loads for a batch of 32 sub-chunks issued together
+    const double *all = a.part + size_t(o & 1) * Q1SW * W * 512;
+    const int j0 = d.r0 / Q1S;
+    for (int e = tid; e < 512; e += 64 * Q1W) {
+      double v = 0.0;
+      for (int jb = j0; jb < nsc; jb += 32) {
+        double t[32];
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+          t[b] = __hip_atomic_load(all + size_t(min(jb + b, nsc - 1)) * 512 + e, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+          if (jb + b < nsc) v += t[b];
+      }
+      sm.Ps[e >> 4][e & 15] = v;
+    }
+    __syncthreads();
+    // M = T P (T upper triangular), into half[0]
+    for (int e = tid; e < 512; e += 64 * Q1W) {
+      const int r = e >> 4, cc = e & 15;
+      double v = 0.0;
+      for (int x = r; x < SB_B; ++x) v += sm.Ts[r][x] * sm.Ps[x][cc];
+      sm.half[0][r][cc] = v;
+    }
+    __syncthreads();
+    // Z -= Y M on this wave's rows
+    doublex4 F[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) F[rb][q] = sm.Zs[wid * 64 + rb * 16 + lr + 4 * q][lc];
+#pragma unroll
+    for (int k0 = 0; k0 < SB_B; k0 += 4) {
+      const double bm = sm.half[0][k0 + lr][lc];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int rl = wid * 64 + rb * 16 + lc, row = R0 + rl;
+        const bool act = row >= d.r0 && row < rend;
+        const double ya = act ? -sm.Ys[rl][k0 + lr] : 0.0;
+        F[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm, F[rb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm.Zs[wid * 64 + rb * 16 + lr + 4 * q][lc] = F[rb][q];
+    __syncthreads();  // half, Ts, Ps, Ys reused by the next step
+  }
+  for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
+    const int r = e >> 4, col = e & 15, row = R0 + r;
+    if (row < n && col < k) a.Z[int64_t(row) * k + col] = sm.Zs[r][col];
   }
 }
 
@@ -997,15 +1268,17 @@ static size_t few_ops_bytes(const SbPlan &pl) {
   for (const SbPanel &P : pl.panels) c += size_t(P.nl);
   return (64 + c * sizeof(Q1Op) + 255) & ~size_t(255);
 }
-static int few_nsub(const SbPlan &pl) {
-  return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) : 0;
+static int few_nsub(const SbPlan &pl) {  // + 1: sub-chunks are row-aligned, not panel-aligned
+  return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) + 1 : 0;
 }
-static size_t few_part_bytes(const SbPlan &pl) {
-  return size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double);
+static size_t few_part_bytes(const SbPlan &pl, int n) {
+  if (!pl.single || pl.panels.empty()) return 0;
+  const size_t lds_form = size_t(2) * cdiv(n, Q1R) * Q1SW * 512 * sizeof(double);
+  return std::max(size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double), lds_form);
 }
 // + one progress word per Q2 sweep group (n / 32 + 1), 16-byte padded
 size_t sb_apply_few_scratch(const SbPlan &pl, int n) {
-  return few_ops_bytes(pl) + few_part_bytes(pl) + ((size_t(n / QB + 1) * 4 + 15) & ~size_t(15));
+  return few_ops_bytes(pl) + few_part_bytes(pl, n) + ((size_t(n / QB + 1) * 4 + 15) & ~size_t(15));
 }
 
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
@@ -1045,7 +1318,7 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.cnt = cnt;
   a.timeout = spin_timeout_ticks("TG_BT_TIMEOUT_TICKS");
   a.colflag = reinterpret_cast<unsigned *>(static_cast<char *>(dev) + few_ops_bytes(pl) +
-                                           few_part_bytes(pl));
+                                           few_part_bytes(pl, n));
   {
     const char *qw = getenv("TG_BT_Q2_WAVE");  // development switch, read per call
     a.q2_wave = (qw && qw[0] == '1') ? 1 : 0;
@@ -1069,10 +1342,41 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       if (e != hipSuccess) return e;
       Q2LArgs qa{Z, n, k, b.V2, b.T2, a.smax, a.ng2, a.colflag, cnt + 1, a.timeout};
       auto tq = prof_begin(st, PROF_Q2, 0.0, 0.0);
+#if TG_Q2L_STATS
+      {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_q2l_stats), z, sizeof(z), 0,
+                                     hipMemcpyHostToDevice, st);
+      }
+#endif
       hipLaunchKernelGGL(q2_lds_kernel<1>, dim3(Wq), dim3(64 * QW), 0, st, qa);
       prof_end(st, tq);
       if ((e = hipGetLastError()) != hipSuccess) return e;
+#if TG_Q2L_STATS
+      {
+        unsigned long long h[8];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_q2l_stats), sizeof(h));
+        const double nbk = double(h[4] ? h[4] : 1);
+        fprintf(stderr, "q2_lds n=%d: %llu blocks; cycles per block: wait %.0f, tile+V %.0f, "
+                "mfma %.0f, store+publish %.0f\n", n, h[4], h[0] / nbk, h[1] / nbk, h[2] / nbk,
+                h[3] / nbk);
+      }
+#endif
       a.nlev2 = 0;  // bt_few_kernel: Q1 only
+      // Q1 with Z in LDS as well (single-level plans; TG_BT_Q1_LDS=0: bt_few's)
+      const char *q1l = getenv("TG_BT_Q1_LDS");  // development switch, read per call
+      const int W1 = cdiv(n, Q1R);
+      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 &&
+          W1 <= xq.xcds * xq.cus_per_xcd) {
+        // partials in bt_few's sub-chunk partial area; arrivals in cnt[5]
+        Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, cnt + 5, cnt + 1, a.timeout};
+        auto t1 = prof_begin(st, PROF_Q1, 0.0, 0.0);
+        hipLaunchKernelGGL(q1_lds_kernel, dim3(W1), dim3(64 * Q1W), 0, st, la);
+        prof_end(st, t1);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        a.nops = 0;  // bt_few_kernel: nothing left
+      }
     }
   }
   // one wave per Q2 block of the widest level, one workgroup per TSQR chunk
@@ -1083,6 +1387,14 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   const XcdInfo xi = xcd_info();
   if (TG_BT_XCD) W = std::min(W, xi.cus_per_xcd);
   a.wexp = W;
+  if (a.nlev2 == 0 && a.nops == 0 && !a.q2_wave) {
+    // everything ran in the LDS-resident kernels: only the timeout flag to read
+    unsigned h2[2] = {0u, 0u};
+    e = hipMemcpyAsync(h2, cnt, sizeof(h2), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);  // also: ops read before it goes
+    *timed_out = h2[1] != 0u;
+    return e;
+  }
   auto tok = prof_begin(st, a.nlev2 > 0 ? PROF_Q2 : PROF_Q1, 0.0, 0.0);
   const int grid = TG_BT_XCD ? xi.xcds * W : W;  // XCD form: W land on each XCD
   if (a.q2_wave) {

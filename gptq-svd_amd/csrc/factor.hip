@@ -745,7 +745,8 @@ __device__ inline void hist_scan(const unsigned *hist, int target, int *out) {
 // Modes of piv_sel_kernel.  SEL_FULL: candidate selection, then the panel's
 // steps (pivot rows gathered from the compacted H_k).  The candidate-block
 // form (the default; TG_PIV_CC=0 keeps SEL_FULL) splits it around the
-// previous panel's Schur update: SEL_SELECT picks the candidates first and
+// previous panel's Schur update (TG_PIV_CC=1; measured no faster, see
+// DESIGN.md): SEL_SELECT picks the candidates first and
 // maps their compact indices (w.cidx, tagged with the panel start), the
 // update then also writes H_k of every candidate pair into the SEL x SEL
 // block w.Cc (syrk_compact_p_kernel's epilogue, exact copies of the values it
@@ -2010,11 +2011,13 @@ static int pivot_core_sel(hipStream_t st, PivWs &w, int n, int k) {
   // compacted Schur complements alternate between the two buffers
   const double *hc = w.Hk;
   double *hn = w.Hk2;
-  // TG_PIV_CC=0: the steps gather pivot rows from H_k (SEL_FULL) instead of
-  // the candidate block (development switch, per call; the block needs the
-  // persistent Schur update)
+  // TG_PIV_CC=1: the steps gather pivot rows from the candidate block instead
+  // of H_k (development switch, per call; the block needs the persistent
+  // Schur update).  Measured at n = 4096: the pivot class 9.0 -> 8.9 ms but
+  // the phase 10.6 -> 11.0 ms (the extra selection launch and the block's
+  // writes in every update), so it is off by default
   const char *pc = getenv("TG_PIV_CC");
-  const bool ccb = persist && !(pc && pc[0] == '0');
+  const bool ccb = persist && pc && pc[0] == '1';
   auto schur_compact = [&](int rows, int cc = 0) -> hipError_t {
     const int nt = tg::cdiv(rows, 64);
     if (persist)

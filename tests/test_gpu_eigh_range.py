@@ -255,3 +255,35 @@ def test_q2_lds_bit_identical(n, count, monkeypatch):
     ref = vectors("0")
     for _ in range(2):
         assert np.array_equal(vectors("1"), ref)
+
+
+@pytest.mark.parametrize("n,count", [(4096, 14), (4096, 1), (600, 14), (1000, 16), (4100, 14),
+                                     (4200, 14), (9000, 14)])
+def test_q1_lds_bit_identical(n, count, monkeypatch):
+    """The few-vector Q1 with Z resident in LDS (csrc/backtr.hip
+    q1_lds_kernel, the default after q2_lds_kernel on single-level plans: 256
+    Z rows per workgroup, one grid exchange of sub-chunk partials per panel
+    step) gives bt_few_kernel's Q1 (TG_BT_Q1_LDS=0) bit for bit, twice in a
+    row: both form the same row-aligned 128-row sub-chunk partials and sum
+    them in the same order.  n = 4100 / 4200: a last sub-chunk past the last
+    workgroup's first half / a partial last workgroup; n = 9000: 36
+    workgroups, more than one XCD's CUs."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 23)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def vectors(flag):
+        monkeypatch.setenv("TG_BT_Q1_LDS", flag)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - count, count,
+                 lib.ptr(V), n, lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    ref = vectors("0")
+    for _ in range(2):
+        assert np.array_equal(vectors("1"), ref)

@@ -62,8 +62,9 @@ def rel(a, b):
     {"TG_URX_SMALLM": "1"},
     {"TG_URX_INV": "1"},
     {"TG_SCHUR_MIRROR": "1"},
-    {"TG_PIV_CC": "0"},
+    {"TG_PIV_CC": "1"},
     {"TG_BT_Q2_LDS": "0"},
+    {"TG_BT_Q1_LDS": "0"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
     {"TG_ORTH_MGS": "1"},

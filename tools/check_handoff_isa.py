@@ -58,7 +58,7 @@ KERNELS = {
                  ("bt_few_kernelILi2ELb1E", True, False, True),
                  ("bt_few_kernelILi1ELb0E", True, False, True),
                  ("bt_few_kernelILi2ELb0E", True, False, True),
-                 ("q2_lds_kernelILi1E", False, False, True)],
+                 ("q2_lds_kernelILi1E", False, False, True), ("q1_lds_kernel", False, False, True)],
     # pqr: the hand-off words and payloads go through explicit address_space(1)
     # sc1 atomics (st_sc1 / ld_sc1); its flat accesses are the panel rows of
     # the launch's input and its outputs, reached through the LDS copy of the
