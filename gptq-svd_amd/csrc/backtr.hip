@@ -32,6 +32,7 @@ using tg::SB_B;
 using tg::SB_C;
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
+typedef double doublex2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
@@ -420,6 +421,22 @@ __device__ inline void q1_sub_rows(const Q1Op &d, int I, int &g0, int &lo, int &
 __device__ inline int q1_nsub(const Q1Op &d) {
   return (d.r0 + d.rows - 1) / Q1S - d.r0 / Q1S + 1;
 }
+// M = T P for the single-level Q1 (T 32 x 32 upper triangular, zeros below;
+// P 32 x 16 ncb), on FP64 MFMA: wave w < 2 ncb forms the 16 x 16 tile
+// (ia, cb) = (w & 1, w >> 1), k ascending in steps of 4.  bt_few_kernel and
+// q1_lds_kernel both use it, so their M (and Z) agree bit for bit.
+template <int TS, int PS>
+__device__ __forceinline__ doublex4 q1_tp_mfma(const double *T, const double *P, int w) {
+  const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
+  const int ia = w & 1, cb = w >> 1;
+  doublex4 acc = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < SB_B; k0 += 4)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(T[(ia * 16 + lc) * TS + k0 + lr],
+                                               P[(k0 + lr) * PS + cb * 16 + lc], acc, 0, 0, 0);
+  return acc;
+}
+
 template <int NCB>
 __device__ void q1_big_a(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op &d, int I,
                          SmQ1 &sm) {
@@ -513,16 +530,14 @@ __device__ void q1_big_b(const BtArgs &a, __amdgpu_buffer_rsrc_t rz, const Q1Op 
     sm.Ms[idx >> 5][idx & 31] = a.T[d.toff + idx];
   }
   __syncthreads();
-  double mval[2] = {0.0, 0.0};
-  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) {
-    const int r = idx >> 5, cc = idx & 31;
-    if (cc >= 16 * NCB) continue;
-    double v = 0.0;
-    for (int e = r; e < SB_B; ++e) v += sm.Ms[r][e] * sm.Ps[e][cc];
-    mval[t] = v;
-  }
+  // M = T P (q1_tp_mfma), over T in Ms once every wave is done reading it
+  doublex4 mt{};
+  if (wid < 2 * NCB) mt = q1_tp_mfma<SB_B + 1, SB_B + 1>(&sm.Ms[0][0], &sm.Ps[0][0], wid);
   __syncthreads();
-  for (int idx = tid, t = 0; idx < SB_B * SB_B; idx += 64 * BW, ++t) sm.Ms[idx >> 5][idx & 31] = mval[t];
+  if (wid < 2 * NCB) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sm.Ms[(wid & 1) * 16 + lr + 4 * q][(wid >> 1) * 16 + lc] = mt[q];
+  }
   __syncthreads();
 #pragma unroll
   for (int k0 = 0; k0 < SB_B; k0 += 4) {
@@ -1053,28 +1068,30 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Q1 with Z resident in LDS (after q2_lds_kernel, the default for k <= 16 and
-// single-level panels; TG_BT_Q1_LDS=0 keeps bt_few_kernel's Q1).  Q1 is 127
-// panel steps (n = 4096), Z[r0:] -= Y (T (Y^T Z[r0:])) from the last panel to
-// the first; each step needs P = Y^T Z over every row at or below the
-// panel's, a reduction over the grid.  Here each workgroup holds Q1R rows of
-// Z in LDS for the whole launch: per step it forms the partials of its two
-// 128-row sub-chunks on MFMA, publishes them write-through (sc1) with one
-// arrival on a counter, waits for all W arrivals, sums the partials in
-// sub-chunk order and updates its rows -- one grid exchange per step instead
-// of bt_few's two barriers, and Z never re-read from L2.  Bit-identical to
-// bt_few's Q1 (q1_big_a / q1_big_b): the same absolute sub-chunks, each a sum
-// of eight 16-row MFMA partials in block order, the sub-chunk sum in the same
-// order (leading sub-chunks above the panel are skipped, as bt_few has none),
-// the same M = T P and Z -= Y M chains.  Partials are double-buffered by step
-// parity: a workgroup can be at most one step ahead of the slowest (the
-// arrival wait), so it never overwrites partials another is still summing.
+// Q1 with Z resident in LDS (after q2_lds_kernel, the default for k <= 16,
+// single-level panels and n <= 32 x 128; TG_BT_Q1_LDS=0 keeps bt_few_kernel's
+// Q1).  Q1 is 127 panel steps (n = 4096), Z[r0:] -= Y (T (Y^T Z[r0:])) from
+// the last panel to the first; each step needs P = Y^T Z over every row at or
+// below the panel's, a reduction over the grid.  Here each workgroup holds
+// one 128-row sub-chunk of Z in LDS for the whole launch; per step it stages
+// the step's Y rows (prefetched into registers during the previous step's
+// exchange), forms its sub-chunk's partial on MFMA, publishes it (plain
+// stores in the one XCD's L2) with one arrival on a counter, waits for all W
+// arrivals, sums the partials in sub-chunk order (16-byte sc1 loads, all in
+// flight at once), forms M = T P on MFMA and updates its rows -- one grid
+// exchange per step instead of bt_few's two barriers, Z never re-read.
+// Bit-identical to bt_few's Q1 (q1_big_a / q1_big_b): the same row-aligned
+// sub-chunks, each the sum of eight 16-row MFMA partials in block order, the
+// sub-chunk sum in the same order (leading sub-chunks above the panel are
+// skipped, as bt_few has none), the same q1_tp_mfma and Z -= Y M chains.
+// Partials are double-buffered by step parity: a workgroup can be at most one
+// step ahead of the slowest (the arrival wait), so it never overwrites
+// partials another is still summing.
 // ---------------------------------------------------------------------------
 constexpr int Q1W = 4;                 // waves per workgroup
-constexpr int Q1R = 256;               // Z rows per workgroup (64 per wave)
-constexpr int Q1SW = Q1R / Q1S;        // sub-chunks per workgroup
-static_assert(Q1S == 16 * BW, "a sub-chunk is bt_few's BW 16-row blocks");
-static_assert(Q1R == 2 * Q1S && Q1W == 4, "two sub-chunks of two waves' four blocks each");
+constexpr int Q1R = Q1S;               // Z rows per workgroup: one sub-chunk (32 per wave)
+constexpr int Q1BW = Q1R / (16 * Q1W); // 16-row blocks per wave
+static_assert(Q1S == 16 * BW && Q1BW * Q1W == BW, "a sub-chunk is bt_few's BW 16-row blocks");
 
 struct Q1LArgs {
   double *Z;
@@ -1082,22 +1099,25 @@ struct Q1LArgs {
   const double *Y, *T;
   const Q1Op *ops;
   int nops;
-  double *part;     // 2 x (Q1SW W) x 512 partials (step parity, sub-chunk, 32 x 16)
+  double *part;     // 2 x W x 512 partials (step parity, sub-chunk, 32 x 16)
   unsigned *cnt;    // [0] arrivals (zeroed per call)
+  unsigned *elect;  // [0] XCD + 1, [1] tickets, [2] checked in, [3] not placed (zeroed)
   unsigned *stall;  // timeout flag
+  int nw;           // workers: cdiv(n, Q1R) (the grid is nw x XCDs)
   unsigned long long timeout;
 };
 
 struct Q1LShared {
   double Zs[Q1R][17];
-  double Ys[Q1R][SB_B + 1];     // this step's Y rows (zero outside the panel)
-  double half[Q1SW][SB_B][17];  // each sub-chunk's sum over its first four blocks
+  double Ys[Q1R][SB_B + 1];   // this step's Y rows (zero outside the panel)
+  double red[BW][SB_B][17];   // the sub-chunk's block partials (block = bt_few's wave)
   double Ps[SB_B][17];
   double Ts[SB_B][SB_B + 1];
+  double Ms[SB_B][17];
 };
 
-// step d's Y rows R0 .. R0 + Q1R - 1 (0 outside the panel) and T into
-// registers: issued a step ahead, landed by the next step's staging
+// step d's Y rows R0 .. R0 + Q1R - 1 (raw, clamped rows) and T into
+// registers: issued a step ahead, masked and staged at the next step
 struct Q1LPre {
   double y[Q1R * SB_B / (64 * Q1W)];
   double t[SB_B * SB_B / (64 * Q1W)];
@@ -1108,20 +1128,86 @@ __device__ __forceinline__ void q1l_fetch(const Q1LArgs &a, const Q1Op &d, int R
 #pragma unroll
   for (int u = 0; u < Q1R * SB_B / (64 * Q1W); ++u) {
     const int row = R0 + u * (64 * Q1W / SB_B) + rsub;
-    // raw (clamped row): the mask waits for the load, so it is applied at staging
     p.y[u] = Y[int64_t(min(max(row - d.r0, 0), d.rows - 1)) * SB_B + col];
   }
 #pragma unroll
   for (int u = 0; u < SB_B * SB_B / (64 * Q1W); ++u) p.t[u] = a.T[d.toff + tid + 64 * Q1W * u];
 }
 
+// Workers: the nw workgroups of one XCD (the first to arrive; tickets 0 ..
+// nw - 1), so every hand-off below stays in that XCD's L2 (the one-L2 form
+// of csrc/spin.h: plain stores, drained, then the arrival; sc1 loads).  Each
+// worker holds a fixed row block, so the kernel needs all nw: if fewer land
+// on the elected XCD (the dispatcher's placement is not guaranteed), every
+// worker leaves before touching Z and elect[3] tells the host to run
+// bt_few's Q1 instead.
+__device__ inline int q1l_elect(const Q1LArgs &a) {
+  __shared__ int sh_w;
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    unsigned expect = 0;
+    __hip_atomic_compare_exchange_strong((gu32 *)a.elect, &expect, x + 1, __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool mine = (expect == 0 ? x + 1 : expect) == x + 1;
+    int ticket = -1;
+    if (mine)
+      ticket = int(__hip_atomic_fetch_add((gu32 *)(a.elect + 1), 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ticket taken before checking in
+    __hip_atomic_fetch_add((gu32 *)(a.elect + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int me = ticket < a.nw ? ticket : -1;
+    if (me >= 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load((gu32 *)(a.elect + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 unsigned(a.nw) &&
+             __hip_atomic_load((gu32 *)(a.elect + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 gridDim.x) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+          tg::stall_set(a.stall);
+          break;
+        }
+      }
+      if (__hip_atomic_load((gu32 *)(a.elect + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+          unsigned(a.nw)) {
+        if (me == 0) tg::ctl_record(a.elect + 3, 1u);
+        me = -1;
+      }
+    }
+    sh_w = me;
+  }
+  __syncthreads();
+  return sh_w;
+}
+
+// TG_Q1L_STATS (build-time): s_memtime cycles per step of each phase, summed
+// over workers (stage Y/T, partials + drain, exchange, P sum, M, Z update)
+#ifndef TG_Q1L_STATS
+#define TG_Q1L_STATS 0
+#endif
+#if TG_Q1L_STATS
+__device__ unsigned long long g_q1l_stats[8];
+#define Q1L_T(v) const uint64_t v = __builtin_amdgcn_s_memtime();
+#else
+#define Q1L_T(v)
+#endif
+
 __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
   __shared__ Q1LShared sm;
+  const int w = q1l_elect(a);
+  if (w < 0) return;
+#if TG_Q1L_STATS
+  uint64_t st[6] = {0, 0, 0, 0, 0, 0};
+#endif
   const int n = a.n, k = a.k, tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane >> 4, lc = lane & 15;
-  const int W = int(gridDim.x), w = blockIdx.x, R0 = w * Q1R;
-  const int nsc = (n + Q1S - 1) / Q1S;  // sub-chunks holding rows of Z
+  const int W = a.nw, R0 = w * Q1R;
+  // the partials as a buffer: 16-byte sc1 loads of two entries
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      a.part, 0, int(size_t(2) * W * 512 * sizeof(double)), 0x00020000);
+  constexpr int SC1 = 16;  // cache policy bit of the L1-bypassing loads
   for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
     const int r = e >> 4, col = e & 15, row = R0 + r;
     sm.Zs[r][col] = (row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
@@ -1129,6 +1215,7 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
   Q1LPre pre;
   if (a.nops > 0) q1l_fetch(a, a.ops[0], R0, pre);
   for (int o = 0; o < a.nops; ++o) {
+    Q1L_T(t0)
     const Q1Op d = a.ops[o];
     const int rend = d.r0 + d.rows;
 #pragma unroll
@@ -1142,13 +1229,14 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
       sm.Ts[e >> 5][e & 31] = pre.t[u];
     }
     __syncthreads();
+    Q1L_T(t1)
     // the 16-row blocks' partials Y^T Z (rows outside the panel: 0)
-    doublex4 Pa[4][2];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const int blk = wid * 4 + rb;
+    for (int rb = 0; rb < Q1BW; ++rb) {
+      const int blk = wid * Q1BW + rb;
+      doublex4 Pa[2];
 #pragma unroll
-      for (int ia = 0; ia < 2; ++ia) Pa[rb][ia] = doublex4{0.0, 0.0, 0.0, 0.0};
+      for (int ia = 0; ia < 2; ++ia) Pa[ia] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rl = blk * 16 + 4 * q + lr, row = R0 + rl;
@@ -1156,41 +1244,29 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
         const double zv = act ? sm.Zs[rl][lc] : 0.0;
 #pragma unroll
         for (int ia = 0; ia < 2; ++ia)
-          Pa[rb][ia] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.Ys[rl][ia * 16 + lc], zv, Pa[rb][ia],
-                                                            0, 0, 0);
+          Pa[ia] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.Ys[rl][ia * 16 + lc], zv, Pa[ia], 0, 0, 0);
       }
-    }
-    // sub-chunk sums over its eight blocks in order (bt_few: wave b's block
-    // is block b): the even wave sums blocks 0..3, the odd wave continues
-    // with 4..7 and publishes write-through
-    const int sc = wid >> 1;
-    if ((wid & 1) == 0) {
 #pragma unroll
       for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double v = 0.0;
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb) v += Pa[rb][ia][q];
-          sm.half[sc][ia * 16 + lr + 4 * q][lc] = v;
-        }
+        for (int q = 0; q < 4; ++q) sm.red[blk][ia * 16 + lr + 4 * q][lc] = Pa[ia][q];
     }
     __syncthreads();
-    if (wid & 1) {
-      double *mine = a.part + (size_t(o & 1) * Q1SW * W + size_t(w) * Q1SW + sc) * 512;
+    // the sub-chunk partial (blocks in order, as bt_few sums its waves'),
+    // published to the one XCD's L2
+    {
+      double *mine = a.part + (size_t(o & 1) * W + w) * 512;
+      for (int e = tid; e < 512; e += 64 * Q1W) {
+        const int r = e >> 4, cc = e & 15;
+        double v = 0.0;
 #pragma unroll
-      for (int ia = 0; ia < 2; ++ia)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = ia * 16 + lr + 4 * q;
-          double v = sm.half[sc][r][lc];
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb) v += Pa[rb][ia][q];
-          __hip_atomic_store(&mine[r * 16 + lc], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int b = 0; b < BW; ++b) v += sm.red[b][r][cc];
+        mine[e] = v;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores drained
     __syncthreads();
+    Q1L_T(t2)
     // the next step's Y and T: in flight through the exchange below (issued
     // after the drain, which would otherwise wait for them too)
     if (o + 1 < a.nops) q1l_fetch(a, a.ops[o + 1], R0, pre);
@@ -1199,56 +1275,79 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
       tg::spin_geq(a.cnt, unsigned(W) * unsigned(o + 1), a.stall, a.timeout);
     }
     __syncthreads();
+    Q1L_T(t3)
     // P = sum of the sub-chunk partials from the panel's first, in order:
-    // each thread's loads for a batch of 32 sub-chunks issued together
-    const double *all = a.part + size_t(o & 1) * Q1SW * W * 512;
-    const int j0 = d.r0 / Q1S;
-    for (int e = tid; e < 512; e += 64 * Q1W) {
-      double v = 0.0;
-      for (int jb = j0; jb < nsc; jb += 32) {
-        double t[32];
+    // entries 2 tid, 2 tid + 1 of every sub-chunk, all loads in flight at once
+    {
+      const int j0 = d.r0 / Q1S;
+      double v0 = 0.0, v1 = 0.0;
+      for (int jb = j0; jb < W; jb += 32) {
+        doublex2 t[32];
 #pragma unroll
         for (int b = 0; b < 32; ++b)
-          t[b] = __hip_atomic_load(all + size_t(min(jb + b, nsc - 1)) * 512 + e, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+          t[b] = __builtin_bit_cast(
+              doublex2, __builtin_amdgcn_raw_buffer_load_b128(
+                            rp, int(((size_t(o & 1) * W + min(jb + b, W - 1)) * 512 + 2 * tid) * 8),
+                            0, SC1));
 #pragma unroll
         for (int b = 0; b < 32; ++b)
-          if (jb + b < nsc) v += t[b];
+          if (jb + b < W) {
+            v0 += t[b][0];
+            v1 += t[b][1];
+          }
       }
-      sm.Ps[e >> 4][e & 15] = v;
+      const int e = 2 * tid;
+      sm.Ps[e >> 4][e & 15] = v0;
+      sm.Ps[e >> 4][(e & 15) + 1] = v1;
     }
     __syncthreads();
-    // M = T P (T upper triangular), into half[0]
-    for (int e = tid; e < 512; e += 64 * Q1W) {
-      const int r = e >> 4, cc = e & 15;
-      double v = 0.0;
-      for (int x = r; x < SB_B; ++x) v += sm.Ts[r][x] * sm.Ps[x][cc];
-      sm.half[0][r][cc] = v;
+    Q1L_T(t4)
+    // M = T P (q1_tp_mfma: waves 0, 1; T upper triangular)
+    if (wid < 2) {
+      const doublex4 mt = q1_tp_mfma<SB_B + 1, 17>(&sm.Ts[0][0], &sm.Ps[0][0], wid);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm.Ms[wid * 16 + lr + 4 * q][lc] = mt[q];
     }
     __syncthreads();
+    Q1L_T(t5)
     // Z -= Y M on this wave's rows
-    doublex4 F[4];
+    doublex4 F[Q1BW];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < Q1BW; ++rb)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) F[rb][q] = sm.Zs[wid * 64 + rb * 16 + lr + 4 * q][lc];
+      for (int q = 0; q < 4; ++q) F[rb][q] = sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc];
 #pragma unroll
     for (int k0 = 0; k0 < SB_B; k0 += 4) {
-      const double bm = sm.half[0][k0 + lr][lc];
+      const double bm = sm.Ms[k0 + lr][lc];
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const int rl = wid * 64 + rb * 16 + lc, row = R0 + rl;
+      for (int rb = 0; rb < Q1BW; ++rb) {
+        const int rl = (wid * Q1BW + rb) * 16 + lc, row = R0 + rl;
         const bool act = row >= d.r0 && row < rend;
         const double ya = act ? -sm.Ys[rl][k0 + lr] : 0.0;
         F[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm, F[rb], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < Q1BW; ++rb)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sm.Zs[wid * 64 + rb * 16 + lr + 4 * q][lc] = F[rb][q];
-    __syncthreads();  // half, Ts, Ps, Ys reused by the next step
+      for (int q = 0; q < 4; ++q) sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc] = F[rb][q];
+    __syncthreads();  // Ms, Ts, Ps, Ys, red reused by the next step
+#if TG_Q1L_STATS
+    const uint64_t t6 = __builtin_amdgcn_s_memtime();
+    st[0] += t1 - t0;
+    st[1] += t2 - t1;
+    st[2] += t3 - t2;
+    st[3] += t4 - t3;
+    st[4] += t5 - t4;
+    st[5] += t6 - t5;
+#endif
   }
+#if TG_Q1L_STATS
+  if (tid == 0) {
+    for (int x = 0; x < 6; ++x) atomicAdd(&g_q1l_stats[x], (unsigned long long)st[x]);
+    atomicAdd(&g_q1l_stats[6], (unsigned long long)a.nops);
+  }
+#endif
   for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
     const int r = e >> 4, col = e & 15, row = R0 + r;
     if (row < n && col < k) a.Z[int64_t(row) * k + col] = sm.Zs[r][col];
@@ -1261,19 +1360,21 @@ namespace tg {
 
 int sb_smax(int n);
 
-// ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + 64 bytes of
-// device scratch (step counter + timeout flag first).
+// ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + 128 bytes of
+// device scratch (32 control words: step counter, timeout flag, bt_few's XCD
+// election [2..4], q1_lds arrivals [5], bt_few stats [8..23], q1_lds's XCD
+// election [24..27]).
 static size_t few_ops_bytes(const SbPlan &pl) {
   size_t c = 0;
   for (const SbPanel &P : pl.panels) c += size_t(P.nl);
-  return (64 + c * sizeof(Q1Op) + 255) & ~size_t(255);
+  return (128 + c * sizeof(Q1Op) + 255) & ~size_t(255);
 }
 static int few_nsub(const SbPlan &pl) {  // + 1: sub-chunks are row-aligned, not panel-aligned
   return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) + 1 : 0;
 }
 static size_t few_part_bytes(const SbPlan &pl, int n) {
   if (!pl.single || pl.panels.empty()) return 0;
-  const size_t lds_form = size_t(2) * cdiv(n, Q1R) * Q1SW * 512 * sizeof(double);
+  const size_t lds_form = size_t(2) * cdiv(n, Q1R) * 512 * sizeof(double);
   return std::max(size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double), lds_form);
 }
 // + one progress word per Q2 sweep group (n / 32 + 1), 16-byte padded
@@ -1292,8 +1393,8 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       ops.push_back(Q1Op{it->r0, L.rows, L.nc, l, int(L.yoff), int(L.toff)});
     }
   unsigned *cnt = static_cast<unsigned *>(dev);
-  Q1Op *dops = reinterpret_cast<Q1Op *>(static_cast<char *>(dev) + 64);
-  hipError_t e = hipMemsetAsync(cnt, 0, 64, st);
+  Q1Op *dops = reinterpret_cast<Q1Op *>(static_cast<char *>(dev) + 128);
+  hipError_t e = hipMemsetAsync(cnt, 0, 128, st);
   if (e != hipSuccess) return e;
   if (!ops.empty()) {
     e = hipMemcpyAsync(dops, ops.data(), ops.size() * sizeof(Q1Op), hipMemcpyHostToDevice, st);
@@ -1366,16 +1467,42 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       a.nlev2 = 0;  // bt_few_kernel: Q1 only
       // Q1 with Z in LDS as well (single-level plans; TG_BT_Q1_LDS=0: bt_few's)
       const char *q1l = getenv("TG_BT_Q1_LDS");  // development switch, read per call
+      // (its workers are the workgroups of one XCD: at most its CUs, n <= 4096)
       const int W1 = cdiv(n, Q1R);
-      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 &&
-          W1 <= xq.xcds * xq.cus_per_xcd) {
-        // partials in bt_few's sub-chunk partial area; arrivals in cnt[5]
-        Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, cnt + 5, cnt + 1, a.timeout};
+      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 && W1 <= xq.cus_per_xcd) {
+        // partials in bt_few's sub-chunk partial area; arrivals in cnt[5],
+        // the XCD election in cnt[24..27]
+        Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, cnt + 5, cnt + 24, cnt + 1, W1,
+                   a.timeout};
         auto t1 = prof_begin(st, PROF_Q1, 0.0, 0.0);
-        hipLaunchKernelGGL(q1_lds_kernel, dim3(W1), dim3(64 * Q1W), 0, st, la);
+        // TG_BT_Q1_LDS=2 (tests): a grid of W1 only, spread over the XCDs, so
+        // the election comes up short and the bt_few fallback runs
+        const int g1 = (q1l && q1l[0] == '2') ? W1 : W1 * xq.xcds;
+        hipLaunchKernelGGL(q1_lds_kernel, dim3(g1), dim3(64 * Q1W), 0, st, la);
         prof_end(st, t1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        a.nops = 0;  // bt_few_kernel: nothing left
+        // did the workers land on one XCD?  (the sync is the one the
+        // all-LDS path makes anyway to read the timeout flag)
+        unsigned h[28];
+        e = hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);  // also: ops read before they go
+        if (e != hipSuccess) return e;
+        *timed_out = h[1] != 0u;
+        if (*timed_out) return hipSuccess;
+#if TG_Q1L_STATS
+        {
+          unsigned long long q[8];
+          (void)hipMemcpyFromSymbol(q, HIP_SYMBOL(g_q1l_stats), sizeof(q));
+          const double ns = double(q[6] ? q[6] : 1);
+          fprintf(stderr, "q1_lds n=%d: %llu worker-steps; cycles per step: stage %.0f, partials %.0f, "
+                  "exchange %.0f, P sum %.0f, M %.0f, Z update %.0f\n", n, q[6], q[0] / ns, q[1] / ns,
+                  q[2] / ns, q[3] / ns, q[4] / ns, q[5] / ns);
+          const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          (void)hipMemcpyToSymbol(HIP_SYMBOL(g_q1l_stats), z, sizeof(z));
+        }
+#endif
+        if (h[27] == 0u) return hipSuccess;  // done: Q2 and Q1 both ran with Z in LDS
+        // not placed: Z untouched, bt_few_kernel's Q1 below
       }
     }
   }

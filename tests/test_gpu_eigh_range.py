@@ -257,17 +257,20 @@ def test_q2_lds_bit_identical(n, count, monkeypatch):
         assert np.array_equal(vectors("1"), ref)
 
 
-@pytest.mark.parametrize("n,count", [(4096, 14), (4096, 1), (600, 14), (1000, 16), (4100, 14),
-                                     (4200, 14), (9000, 14)])
+@pytest.mark.parametrize("n,count", [(4096, 14), (4096, 1), (600, 14), (1000, 16), (3000, 14),
+                                     (4000, 14), (4200, 14)])
 def test_q1_lds_bit_identical(n, count, monkeypatch):
     """The few-vector Q1 with Z resident in LDS (csrc/backtr.hip
-    q1_lds_kernel, the default after q2_lds_kernel on single-level plans: 256
-    Z rows per workgroup, one grid exchange of sub-chunk partials per panel
-    step) gives bt_few_kernel's Q1 (TG_BT_Q1_LDS=0) bit for bit, twice in a
-    row: both form the same row-aligned 128-row sub-chunk partials and sum
-    them in the same order.  n = 4100 / 4200: a last sub-chunk past the last
-    workgroup's first half / a partial last workgroup; n = 9000: 36
-    workgroups, more than one XCD's CUs."""
+    q1_lds_kernel, the default after q2_lds_kernel on single-level plans up
+    to n = 4096: one 128-row sub-chunk of Z per workgroup, the workgroups of
+    one XCD, one exchange of sub-chunk partials per panel step) gives
+    bt_few_kernel's Q1 (TG_BT_Q1_LDS=0) bit for bit, twice in a row: both
+    form the same row-aligned sub-chunk partials, sum them in the same order
+    and form M = T P with the same MFMA sequence.  TG_BT_Q1_LDS=2 launches
+    too few workgroups for one XCD, so the election fails and bt_few's Q1
+    runs instead: the same vectors again.  n = 3000 / 4000 / 600: a partial
+    last sub-chunk; n = 4096: all 32 CUs of the XCD; n = 4200: 33 sub-chunks,
+    more than one XCD's CUs (bt_few's Q1 only)."""
     from gptq_svd_amd import _lib as lib
     H = torch.from_numpy(_wishart(n, 23)).to(DEV)
     ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
@@ -287,3 +290,4 @@ def test_q1_lds_bit_identical(n, count, monkeypatch):
     ref = vectors("0")
     for _ in range(2):
         assert np.array_equal(vectors("1"), ref)
+    assert np.array_equal(vectors("2"), ref)
