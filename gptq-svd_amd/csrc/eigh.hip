@@ -1007,8 +1007,11 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
                                                        int first,
                                                        const double *__restrict__ w_asc,
                                                        const double *__restrict__ bnd, int iters,
+                                                       int refac,
                                                        Tri w) {
   extern __shared__ double2 rows[];  // rows[2i] = {1/pivot, du}, rows[2i+1] = {du2, x}
+  // after the rows: the interchange bits of each IFCH-step chunk
+  unsigned *swm = reinterpret_cast<unsigned *>(rows + 2 * size_t(n));
   const int jj = blockIdx.x, lane = threadIdx.x;
   const int gi = n - 1 - (first + jj);
   const double lam = w_asc[gi];
@@ -1022,6 +1025,7 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
     if (i < b0 || i >= b1) w.Z[size_t(i) * K + jj] = 0.0;
   d += b0;
   e += b0;
+  double *fz = w.Z + jj;  // multiplier f of block row i at fz[(b0 + i) K] until the last write
   for (int i = lane; i < m; i += 64) X(i) = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
   auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
   auto rcp2 = [](double b) {
@@ -1060,7 +1064,8 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
       // turning the selects into exec-mask branches.  a / b = q0 + r1 (a - b q0)
       // with r1 one Newton step from v_rcp_f64: the correction runs beside the
       // refinement, shortening the serial chain.
-      auto step = [&](double sub, double nd, double nu, double xnext, double2 &o0, double2 &o1) {
+      auto step = [&](double sub, double nd, double nu, double xnext, double2 &o0, double2 &o1,
+                      double &fo, unsigned &swb) {
         const uint64_t sw = __builtin_amdgcn_fcmp(fabs(cur_d), fabs(sub), 12);  // ULT
         const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(cur_d), tol, 4);       // OLT
         const double den = vsel(sw, sub, vsel(tiny, copysign(tol, cur_d), cur_d));
@@ -1073,43 +1078,100 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
         const double C = vsel(sw, cur_u, nd), D = vsel(sw, nd, cur_u);
         o0 = make_double2(fma(fma(-den, r1, 1.0), r1, r1), D);
         o1 = make_double2(vsel(sw, nu, 0.0), B);
-        xi = A - f * B;
+        xi = fma(-f, B, A);
         cur_d = C - f * D;
         cur_u = vsel(sw, -f * nu, nu);
+        fo = f;
+        swb = unsigned(sw & 1u);  // lane 0's interchange
       };
-      fetch(0, dn, en);
-      for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
-        const int cnt = min(IFCH, m - 1 - i0);
-        fetch(i0 + IFCH, pd, pe);  // next chunk in flight while this one runs
-        double xn[IFCH];
+      if (it == 0 || refac) {
+        // factor + forward substitution; the multipliers f go to Z's column
+        // (free until the final write) and the interchanges to LDS bit masks,
+        // so later iterations only substitute (the factors do not change)
+        fetch(0, dn, en);
+        for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
+          const int cnt = min(IFCH, m - 1 - i0);
+          fetch(i0 + IFCH, pd, pe);  // next chunk in flight while this one runs
+          double xn[IFCH], fo[IFCH];
+          unsigned msk = 0;
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
-        if (cnt == IFCH) {
-          // outputs leave in one batch after the chunk, off the chain
-          double2 o0[IFCH], o1[IFCH];
+          for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
+          if (cnt == IFCH) {
+            // outputs leave in one batch after the chunk, off the chain
+            double2 o0[IFCH], o1[IFCH];
 #pragma unroll
-          for (int u = 0; u < IFCH; ++u)
-            step(en[u], dn[u] - lam, u + 1 < IFCH ? en[u + 1] : pe[0], xn[u], o0[u], o1[u]);
+            for (int u = 0; u < IFCH; ++u) {
+              unsigned b;
+              step(en[u], dn[u] - lam, u + 1 < IFCH ? en[u + 1] : pe[0], xn[u], o0[u], o1[u], fo[u],
+                   b);
+              msk |= b << u;
+            }
+#pragma unroll
+            for (int u = 0; u < IFCH; ++u) {
+              rows[2 * (i0 + u)] = o0[u];
+              rows[2 * (i0 + u) + 1] = o1[u];
+              if (iters > 1) fz[size_t(b0 + i0 + u) * K] = fo[u];
+            }
+          } else {
+            for (int u = 0; u < cnt; ++u) {
+              double2 o0, o1;
+              unsigned b;
+              step(en[u], dn[u] - lam, eat(i0 + u + 1), xn[u], o0, o1, fo[0], b);
+              msk |= b << u;
+              rows[2 * (i0 + u)] = o0;
+              rows[2 * (i0 + u) + 1] = o1;
+              if (iters > 1) fz[size_t(b0 + i0 + u) * K] = fo[0];
+            }
+          }
+          swm[i0 / IFCH] = msk;
 #pragma unroll
           for (int u = 0; u < IFCH; ++u) {
-            rows[2 * (i0 + u)] = o0[u];
-            rows[2 * (i0 + u) + 1] = o1[u];
-          }
-        } else {
-          for (int u = 0; u < cnt; ++u) {
-            double2 o0, o1;
-            step(en[u], dn[u] - lam, eat(i0 + u + 1), xn[u], o0, o1);
-            rows[2 * (i0 + u)] = o0;
-            rows[2 * (i0 + u) + 1] = o1;
+            dn[u] = pd[u];
+            en[u] = pe[u];
           }
         }
+        rows[2 * (m - 1)] = make_double2(rcp2(clampp(cur_d)), 0.0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the f stores land before they are read back
+      } else {
+        // forward substitution with the stored factors: x_i = B, xi = A - f B
+        // with (A, B) = (xi, x_{i+1}) or swapped -- the same operations as the
+        // factoring pass, so the same values
+        double fc[IFCH], fp[IFCH];
+        auto ffetch = [&](int i0, double *a) {
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) {
-          dn[u] = pd[u];
-          en[u] = pe[u];
+          for (int u = 0; u < IFCH; ++u)
+            a[u] = fz[size_t(b0 + min(i0 + u + vz, max(m - 2, 0))) * K];
+        };
+        ffetch(0, fc);
+        for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
+          const int cnt = min(IFCH, m - 1 - i0);
+          ffetch(i0 + IFCH, fp);
+          const unsigned msk = swm[i0 / IFCH];
+          double xn[IFCH], xo[IFCH];
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
+          if (cnt == IFCH) {
+#pragma unroll
+            for (int u = 0; u < IFCH; ++u) {
+              const bool sw = (msk >> u) & 1u;
+              const double A = sw ? xi : xn[u], B = sw ? xn[u] : xi;
+              xo[u] = B;
+              xi = fma(-fc[u], B, A);
+            }
+#pragma unroll
+            for (int u = 0; u < IFCH; ++u) X(i0 + u) = xo[u];
+          } else {
+            for (int u = 0; u < cnt; ++u) {
+              const bool sw = (msk >> u) & 1u;
+              const double A = sw ? xi : xn[u], B = sw ? xn[u] : xi;
+              X(i0 + u) = B;
+              xi = fma(-fc[u], B, A);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) fc[u] = fp[u];
         }
       }
-      rows[2 * (m - 1)] = make_double2(rcp2(clampp(cur_d)), 0.0);
       rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
       // backward substitution with U (du of row m-1 and du2 of rows m-2, m-1 are 0)
       double xn1 = 0.0, xn2 = 0.0;
@@ -1627,13 +1689,16 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
   const char *ie = getenv("TG_INVIT_ITERS");
   const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
-  // few vectors: one LDS-resident wave per vector (4 doubles per row of T)
-  const size_t ilds = 4 * sizeof(double) * size_t(n);
+  // few vectors: one LDS-resident wave per vector (4 doubles per row of T,
+  // + one interchange mask per IFCH rows)
+  const size_t ilds = 4 * sizeof(double) * size_t(n) + 4 * size_t(tg::cdiv(n, IFCH));
   if (k <= 256 && ilds <= 160 * 1024 && !getenv("TG_INVIT_REG")) {
     TG_HIP(hipFuncSetAttribute((const void *)invit_lds_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(ilds)));
+    // TG_INVIT_REFACTOR=1 (tests): factor again in every iteration
+    const char *rf = getenv("TG_INVIT_REFACTOR");
     hipLaunchKernelGGL(invit_lds_kernel, dim3(k), dim3(64), ilds, st, w.d, w.es, n, k, first,
-                       w_asc, bnd, iters, w);
+                       w_asc, bnd, iters, (rf && rf[0] == '1') ? 1 : 0, w);
   } else {
     hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k,
                        first, w_asc, bnd, iters, w);

@@ -291,3 +291,34 @@ def test_q1_lds_bit_identical(n, count, monkeypatch):
     for _ in range(2):
         assert np.array_equal(vectors("1"), ref)
     assert np.array_equal(vectors("2"), ref)
+
+
+@pytest.mark.parametrize("n,count,kind,iters", [(4096, 14, "wishart", "2"), (600, 14, "wishart", "3"),
+                                                (700, 60, "blockdiag", "2"), (2048, 1, "wishart", "1")])
+def test_invit_factor_once_bit_identical(n, count, kind, iters, monkeypatch):
+    """Inverse iteration (csrc/eigh.hip invit_lds_kernel) factors T - lambda I
+    once and keeps the multipliers (in the vector's Z column) and the row
+    interchanges (LDS bit masks), so the later iterations only substitute:
+    the vectors equal those of a kernel that factors in every iteration
+    (TG_INVIT_REFACTOR=1) bit for bit -- 1, 2 and 3 iterations, and a
+    block-diagonal T (1x1 blocks: m = 1, no forward step)."""
+    from gptq_svd_amd import _lib as lib
+    H = _wishart(n, 31) if kind == "wishart" else _blockdiag(n, 31)
+    Hd = torch.from_numpy(H).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+    monkeypatch.setenv("TG_INVIT_ITERS", iters)
+
+    def vectors(refac):
+        monkeypatch.setenv("TG_INVIT_REFACTOR", refac)
+        A = Hd.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - count, count,
+                 lib.ptr(V), n, lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    ref = vectors("1")
+    assert np.array_equal(vectors("0"), ref)

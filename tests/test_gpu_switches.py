@@ -42,6 +42,7 @@ def rel(a, b):
     {"TG_PIVOT_OLD": "1"},
     {"TG_PIVOT_OLD": "1", "TG_PIVOT_STEPWISE": "1"},
     {"TG_INVIT_REG": "1"},
+    {"TG_INVIT_REFACTOR": "1"},
     {"TG_BT_MULTI": "1"},
     {"TG_BT_Q2_WAVE": "1"},
     {"TG_URX_TWOCHOL": "1"},
