@@ -898,6 +898,39 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
   for (int s = 0; s < nb; ++s) {
     const int j0 = G2 * QB, c = G2 + s, rb0 = j0 + 1 + s * SB_B;
     Q2L_T(t0)
+    // Off the chain, before the waits: this block's reflectors into LDS and
+    // from there the MFMA A operands of both V products into registers (the
+    // staircase selects included), T's into tv, and the next block's
+    // reflectors in flight -- none of it depends on Z.  After the waits only
+    // the Z tile, the 80 MFMAs and the stores remain.
+    double(*Vs)[SB_B + 1] = sm.Vs[g];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = lane + 64 * u, r = idx >> 5, d = idx & 31;
+      Vs[r][d] = refl_valid(n, j0 + r, s) ? pre.vv[u] : 0.0;
+    }
+    double tv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tv[u] = pre.tt[u];
+    if (s + 1 < nb) q2l_fetch(a, G2, s + 1, pre);
+    wave_sync();
+    auto yval = [&](int i, int cc) -> double {
+      const int d = i - cc;
+      return (d >= 0 && d < SB_B) ? Vs[cc][d] : 0.0;
+    };
+    double ya1[4][4][2], ya3[2][4][4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia) ya1[rb][qq][ia] = yval(rb * 16 + 4 * qq + lr, ia * 16 + lc);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) ya3[kb][qq][rb] = -yval(rb * 16 + lc, kb * 16 + 4 * qq + lr);
     // (G2 + 1, s) -- or, for the last block, all of group G2 + 1
     if (nbu > 0) {
       const unsigned need = unsigned(min(s + 1, nbu));
@@ -942,23 +975,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
         }
       }
     }
-    double(*Vs)[SB_B + 1] = sm.Vs[g];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int idx = lane + 64 * u, r = idx >> 5, d = idx & 31;
-      Vs[r][d] = refl_valid(n, j0 + r, s) ? pre.vv[u] : 0.0;
-    }
-    double tv[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) tv[u] = pre.tt[u];
-    // next block's reflectors: in flight through this block's arithmetic
-    if (s + 1 < nb) q2l_fetch(a, G2, s + 1, pre);
-    wave_sync();
     Q2L_T(t2)
-    auto yval = [&](int i, int cc) -> double {
-      const int d = i - cc;
-      return (d >= 0 && d < SB_B) ? Vs[cc][d] : 0.0;
-    };
     doublex4 Pa[2][NCB];
 #pragma unroll
     for (int ia = 0; ia < 2; ++ia)
@@ -967,18 +984,13 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int i = rb * 16 + 4 * qq + lr;
-        double ya[2];
-#pragma unroll
-        for (int ia = 0; ia < 2; ++ia) ya[ia] = yval(i, ia * 16 + lc);
+      for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
         for (int ia = 0; ia < 2; ++ia)
 #pragma unroll
           for (int cb = 0; cb < NCB; ++cb)
-            Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[ia], F[rb][cb][qq], Pa[ia][cb], 0,
-                                                              0, 0);
-      }
+            Pa[ia][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya1[rb][qq][ia], F[rb][cb][qq],
+                                                              Pa[ia][cb], 0, 0, 0);
     doublex4 Ma[2][NCB];
 #pragma unroll
     for (int ia = 0; ia < 2; ++ia)
@@ -997,16 +1009,13 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int kk = kb * 16 + 4 * qq + lr;
+      for (int qq = 0; qq < 4; ++qq)
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-          const double ya = -yval(rb * 16 + lc, kk);
+        for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
           for (int cb = 0; cb < NCB; ++cb)
-            F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, Ma[kb][cb][qq], F[rb][cb], 0, 0, 0);
-        }
-      }
+            F[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya3[kb][qq][rb], Ma[kb][cb][qq],
+                                                             F[rb][cb], 0, 0, 0);
 #if TG_Q2L_STATS
     asm volatile("s_nop 0" : "+v"(F[3][0][3]));  // the chain's last MFMA issued
 #endif
