@@ -141,6 +141,9 @@ hipError_t sb_apply_q2(hipStream_t st, int n, double *Z, int k, const double *V2
                        double *T2);
 // Q2 block T factors only (T2), for sb_apply_few.
 hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, double *T2);
+// side stream of the band reduction: fork after the work queued on st, join back into st
+hipError_t side_fork(hipStream_t st, hipStream_t *side);
+hipError_t side_join(hipStream_t st);
 // Z (n x k row-major, k <= 32) <- Q1 Q2 Z in one persistent launch (backtr.hip);
 // T2 must hold the Q2 T factors; dev: sb_apply_few_scratch bytes of device
 // scratch.  Syncs the stream (reads the barrier timeout flag).

@@ -718,6 +718,14 @@ struct XmArgs {
   // (what pair_part_kernel + pair_fin_kernel form otherwise); null: none
   const double *Ya, *Wa;
   double *PQ;
+  // fused W (no pair products; every workgroup resident): after M, every
+  // workgroup turns its rows of X into W = X - Y M / 2 in place (what
+  // w_update_kernel does, same operations): the last arriver publishes M
+  // write-through and raises *mflag to epoch, the others wait for it
+  int fuse_w;
+  unsigned *mflag, epoch;
+  unsigned *stall;  // timeout flag of the wait (the band reduction's, pq_ctl[0])
+  unsigned long long timeout;
 };
 // doubles of one block's partials: Y^T X, + the four pair products
 __host__ __device__ inline int xm_np(const XmArgs &g) { return g.Ya ? 5 : 1; }
@@ -908,6 +916,30 @@ __device__ __forceinline__ double xm_sum(const double *p, int z0, int z1, int e,
   return s;
 }
 
+// Fused W (XmArgs::fuse_w): wait until M is published, stage it, and turn
+// this block's rows of X into W = X - Y M / 2 in place -- per entry the fma
+// chain of w_update_kernel (l ascending from 0.0, then x - v / 2), so the
+// result is the same.  xs / ys: the block's X / Y rows in LDS; ms: 1024
+// doubles of LDS scratch.
+template <int NBC>
+__device__ __forceinline__ void xm_fused_w(const XmArgs &g, int r0, const double (*xs)[SB_B + 1],
+                                        const double (*ys)[SB_B + 1], double *ms) {
+  constexpr int RB = XR * NBC;
+  const int tid = threadIdx.x;
+  if (tid < 64) tg::spin_geq(g.mflag, g.epoch, g.stall, g.timeout);
+  __syncthreads();
+  for (int e = tid; e < SB_B * SB_B; e += 64 * XW)
+    ms[e] = __hip_atomic_load(&g.M[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int e = tid; e < RB * SB_B; e += 64 * XW) {
+    const int rr = e >> 5, c = e & 31;
+    double v = 0.0;
+#pragma unroll
+    for (int l = 0; l < SB_B; ++l) v = fma(ys[rr][l], ms[l * SB_B + c], v);
+    if (r0 + rr < g.m) g.X[int64_t(r0 + rr) * SB_B + c] = fma(-0.5, v, xs[rr][c]);
+  }
+}
+
 // NBC = 2 (m >= XM_WIDE, the HBM-resident trailing matrices): two
 // workgroups per CU -- 6 K steps in flight per wave (<= 128 registers) and
 // the Y / X rows of the block staged in the reduction buffer once it is free
@@ -920,9 +952,11 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   constexpr int RB = XR * NBC;                // rows of X per workgroup
   constexpr int DA = xm_depth<NBC>();
   __shared__ double red[XW][RB][SB_B + 1];   // the last workgroup reuses it for C, T
-  static_assert(XW >= 2, "xs and ys alias red[0] and red[1]");
-  double(*xs)[SB_B + 1] = red[0];
-  double(*ys)[SB_B + 1] = red[1];
+  // the block's X and Y rows in the last two slices (kept through the last
+  // arrivers' C / T / pair work in the first ones, for the fused W)
+  static_assert(XW >= 8, "xs and ys are red[XW - 2] and red[XW - 1]");
+  double(*xs)[SB_B + 1] = red[XW - 2];
+  double(*ys)[SB_B + 1] = red[XW - 1];
   __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform K loop
@@ -1074,7 +1108,11 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     s_last = __hip_atomic_fetch_add(&g.tick[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
              unsigned(z1 - z0 - 1);
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) {
+    if constexpr (NBC == 1)
+      if (g.fuse_w) xm_fused_w<NBC>(g, r0, xs, ys, &red[XW - 4][0][0]);
+    return;
+  }
   // Cs = C (Y^T X), then the pair sums P, Q, E1, E2 (pp); Ts = T
   double *Cs = &red[0][0][0], *Ts = Cs + 5 * SB_B * SB_B;
   static_assert(XW * XR * (SB_B + 1) >= 2 * SB_B * SB_B, "C and T fit in red");
@@ -1100,7 +1138,11 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
                                       __HIP_MEMORY_SCOPE_AGENT) == unsigned(NG - 1);
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) {
+      if constexpr (NBC == 1)
+        if (g.fuse_w) xm_fused_w<NBC>(g, r0, xs, ys, &red[XW - 4][0][0]);
+      return;
+    }
     for (int e = tid; e < ne; e += 64 * XW) Cs[e] = xm_sum(g.gpart, 0, NG, e, NP * 1024);
   }
   __syncthreads();
@@ -1108,7 +1150,21 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     const int a = e >> 5, c = e & 31;
     double v = 0.0;
     for (int k = 0; k <= a; ++k) v = fma(Ts[k * SB_B + a], Cs[k * SB_B + c], v);
-    g.M[e] = v;
+    if (NBC == 1 && g.fuse_w)
+      __hip_atomic_store(&g.M[e], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+    else
+      g.M[e] = v;
+  }
+  if (NBC == 1 && g.fuse_w) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's M stores drained
+    __syncthreads();
+    if (tid == 0) {
+      tg::ctl_reset(&g.tick[grp]);
+      if (NG > 1) tg::ctl_reset(&g.tick[NG]);
+      __hip_atomic_store(g.mflag, g.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (NBC == 1) xm_fused_w<NBC>(g, r0, xs, ys, &red[XW - 4][0][0]);
+    return;
   }
   if (pp) {
     // PQ[0 .. 2047] = {P, Q}; D = E1 P + E2 Q into C's slot (M is out);
@@ -1170,7 +1226,8 @@ __global__ __launch_bounds__(256) void w_update_kernel(const double *__restrict_
     v1 = fma(y[h].y, b.y, v1);
   }
   if (r < m)
-    reinterpret_cast<double2 *>(X + int64_t(r) * SB_B)[c2] = make_double2(x.x - 0.5 * v0, x.y - 0.5 * v1);
+    reinterpret_cast<double2 *>(X + int64_t(r) * SB_B)[c2] =
+        make_double2(fma(-0.5, v0, x.x), fma(-0.5, v1, x.y));
 }
 
 // A22 -= Y W^T + W Y^T on 64 x 64 lower tiles, mirrored (A22 stays bitwise
@@ -1704,6 +1761,25 @@ static hipError_t side_stream(SideStream *&out) {
   return hipSuccess;
 }
 
+// Fork work onto the side stream after everything queued on st so far, and
+// join it back (tg_eigh_vectors_range: the Q2 T factors beside inverse
+// iteration)
+hipError_t side_fork(hipStream_t st, hipStream_t *side) {
+  SideStream *ss = nullptr;
+  TG_CHK(side_stream(ss));
+  TG_CHK(hipEventRecord(ss->evj, st));
+  TG_CHK(hipStreamWaitEvent(ss->s, ss->evj, 0));
+  *side = ss->s;
+  return hipSuccess;
+}
+hipError_t side_join(hipStream_t st) {
+  SideStream *ss = nullptr;
+  TG_CHK(side_stream(ss));
+  TG_CHK(hipEventRecord(ss->evj, ss->s));
+  TG_CHK(hipStreamWaitEvent(st, ss->evj, 0));
+  return hipSuccess;
+}
+
 // One compact-WY block per panel (pqr.hip): panel QR, X = A22 YT, M, update.
 // (Measured and removed in round 3's clean-up, DESIGN.md §5: a look-ahead
 // with the next panel's QR on a side stream, +5 ms -- the QR's workgroups need
@@ -1719,18 +1795,55 @@ static int xm_nbc(int m) {
   const char *fx = getenv("TG_XM_NBC");  // development switch (1 | 2), read per call
   return fx ? (atoi(fx) == 2 ? 2 : 1) : (m >= XM_WIDE ? 2 : 1);
 }
-// Ya / Wa (panel pairs, NBC = 2 only): also form the pair products into PQ
+// X / M workgroups that fit the device at once (occupancy x CUs, cached)
+template <int NBC>
+static int xm_resident() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cached[dev] == 0) {
+    int ncu = 0, occ = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xm_kernel<NBC>, 64 * XW, 0) !=
+        hipSuccess)
+      occ = 0;
+    cached[dev] = std::max(0, ncu) * std::max(0, occ);
+    if (cached[dev] == 0) cached[dev] = -1;
+  }
+  return std::max(0, cached[dev]);
+}
+// Ya / Wa (panel pairs, NBC = 2 only): also form the pair products into PQ.
+// epoch > 0: fuse W = X - Y M / 2 into the launch when every workgroup fits
+// the device at once (they wait for M); returns *fused (false: the caller
+// runs w_update_kernel)
 static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const double *YT,
                             const double *Yp, const double *Tp, double *X, const SbBufs &b,
                             const double *Ya = nullptr, const double *Wa = nullptr,
-                            double *PQ = nullptr) {
+                            double *PQ = nullptr, unsigned epoch = 0, unsigned *mflag = nullptr,
+                            bool *fused = nullptr) {
   const int nbc = xm_nbc(m);
   if (Ya && nbc != 2) return hipErrorInvalidValue;
   const int G = cdiv(m, XR * nbc), np = Ya ? 5 : 1;
   const char *xs = getenv("TG_XM_ASM");  // development switch: 0 = compiler-scheduled loads
   const int asm_loads = !(xs && xs[0] == '0');
+  // TG_XM_FUSE_W=1 (development switch, per call): W inside the launch.  Measured
+  // 57.13 vs 56.82 ms per factorisation at n = 4096 and equal at 12,288
+  // (profiles/r06/env_ab_*.log): the wait for M costs what the separate
+  // w_update_kernel did, so the default keeps the separate kernel.
+  const char *fw = getenv("TG_XM_FUSE_W");
+  // (NBC = 1 only: at two workgroups per CU the fused tail spills xm_kernel<2>.
+  // Half the resident capacity, so that two processes sharing the device --
+  // the multi-rank tests -- can both have every workgroup of a launch
+  // resident at once: the waiting workgroups never block the ones that
+  // would publish M.)
+  const bool fuse = epoch > 0 && mflag && !Ya && nbc == 1 && (fw && fw[0] == '1') &&
+                    2 * G <= xm_resident<1>();
+  if (fused) *fused = fuse;
+  static const unsigned long long tmo_ticks = spin_timeout_ticks("TG_XM_TIMEOUT_TICKS");
   XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * np * 1024, b.M,
-            b.xm_tick, asm_loads, Ya, Wa, PQ};
+            b.xm_tick, asm_loads, Ya, Wa, PQ, fuse ? 1 : 0,
+            mflag, epoch, b.pq_ctl, tmo_ticks};
   if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
   else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
   return hipGetLastError();
@@ -1784,11 +1897,16 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     double *Yp = b.Y + P.L[0].yoff, *Tp = b.T + P.L[0].toff;
     TG_CHK(panel_qr(st, A, lda, P.p, P.r0, P.m, Yp, b.YT, Tp, b.pq_part, b.pq_bc,
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
-    TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b));
-    // W = X - Y M / 2 in place
-    hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
-    TG_CHK(hipGetLastError());
     const bool pair = pairs && pi + 1 < np && pl.panels[pi + 1].m >= pair_min;
+    // W = X - Y M / 2 in place: inside the X / M launch where it can be
+    // (panel a of a pair needs M only through W as well)
+    bool fused = false;
+    TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b, nullptr, nullptr, nullptr,
+                     unsigned(pi + 1), b.xm_tick + xm_tick_words(n) - 1, &fused));
+    if (!fused) {
+      hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
+      TG_CHK(hipGetLastError());
+    }
     if (!pair) {  // A22 -= Y W^T + W Y^T
       const int nt = cdiv(m, WT), tiles = nt * (nt + 1) / 2;
       auto tok = prof_begin(st, PROF_SBUPD, 12.0 * double(m) * m, 64.0 * double(m) * m);

@@ -1686,6 +1686,20 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   tg::sb_layout(ar, n, n, pl, &sb);
   TG_WS(ar);
   const double *bnd = w.scal;
+  // the few-vector back-transform's Q2 T factors depend only on the bulge
+  // reflectors: formed on the side stream beside inverse iteration (14
+  // one-wave workgroups) and the cluster checks, joined before the apply
+  const bool ts = two_stage(n);
+  const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
+  const bool few = ts && k <= 32 && !multi &&
+                   tg::sb_apply_few_scratch(pl, n) <= sizeof(double) * size_t(n) * tg::SB_B;
+  const char *tfs = getenv("TG_BT_TF_SIDE");  // development switch: 0 = in order, per call
+  const bool tf_side = few && !(tfs && tfs[0] == '0');
+  if (tf_side) {
+    hipStream_t side = nullptr;
+    TG_HIP(tg::side_fork(st, &side));
+    TG_HIP(tg::sb_q2_tfactors(side, n, sb.V2, sb.T2));
+  }
   auto itok = tg::prof_begin(st, tg::PROF_INVIT, 8.0 * 5 * 4 * double(n) * k, 0.0);
   const char *ie = getenv("TG_INVIT_ITERS");
   const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
@@ -1774,13 +1788,14 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
     }
   }
   // back-transformation Z <- Q Z, Q = H_0 H_1 ... H_{n-2}
-  const bool ts = two_stage(n);
   const int nref = ts ? 0 : n - 1;
   if (ts) {
-    // few vectors (the complement path's request): one persistent launch
-    const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
-    if (k <= 32 && !multi && tg::sb_apply_few_scratch(pl, n) <= sizeof(double) * size_t(n) * tg::SB_B) {
-      TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.T2));
+    // few vectors (the complement path's request): the LDS-resident kernels
+    if (few) {
+      if (tf_side)
+        TG_HIP(tg::side_join(st));  // the T factors
+      else
+        TG_HIP(tg::sb_q2_tfactors(st, n, sb.V2, sb.T2));
       bool tmo = false;
       TG_HIP(tg::sb_apply_few(st, n, w.Z, k, pl, sb, sb.X, &tmo));
       if (tmo) {

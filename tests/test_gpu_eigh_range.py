@@ -322,3 +322,29 @@ def test_invit_factor_once_bit_identical(n, count, kind, iters, monkeypatch):
 
     ref = vectors("1")
     assert np.array_equal(vectors("0"), ref)
+
+
+@pytest.mark.parametrize("n", [4096, 2000, 7000])
+def test_xm_fused_w_bit_identical(n, monkeypatch):
+    """W = X - Y M / 2 formed inside the X / M launch (csrc/band.hip
+    xm_fused_w, TG_XM_FUSE_W=1: every workgroup waits for the last arriver's
+    M, then updates its own rows; measured no faster, so opt-in) gives the
+    reduced band of w_update_kernel (the default) bit for bit: the same fma
+    chain per entry, so the eigenvalues agree exactly.  n = 2000: a ragged last row block; n = 7000: panels of both
+    X / M forms (16 and 32 columns per workgroup) and panel pairs."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 41)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def values(flag):
+        monkeypatch.setenv("TG_XM_FUSE_W", flag)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        torch.cuda.synchronize()
+        return w.cpu().numpy()
+
+    ref = values("0")
+    for _ in range(2):
+        assert np.array_equal(values("1"), ref)

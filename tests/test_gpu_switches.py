@@ -60,12 +60,14 @@ def rel(a, b):
     {"TG_XM_ASM": "0"},
     {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
+    {"TG_XM_FUSE_W": "1"},
     {"TG_URX_SMALLM": "1"},
     {"TG_URX_INV": "1"},
     {"TG_SCHUR_MIRROR": "1"},
     {"TG_PIV_CC": "1"},
     {"TG_BT_Q2_LDS": "0"},
     {"TG_BT_Q1_LDS": "0"},
+    {"TG_BT_TF_SIDE": "0"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
     {"TG_ORTH_MGS": "1"},
