@@ -460,10 +460,10 @@ def cpu_baseline(H, W, args):
                         f"factorisation {t1 - t0:.2f}s + quantize/pack {t2 - t1:.2f}s"))
 
 
-PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05",
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06",
                         "pmc_traffic.json")
 if not os.path.exists(PMC_FILE):  # until this round's profile is committed
-    PMC_FILE = PMC_FILE.replace("r05", "r04")
+    PMC_FILE = PMC_FILE.replace("r06", "r05")
 LATENCY_BOUND = {"bulge_chase", "tsqr_leaf"}
 BULGE_DG = 2  # csrc/bulge.hip TG_BULGE_DF_GSW: sweeps per workgroup of the dataflow kernel
 

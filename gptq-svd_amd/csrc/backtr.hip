@@ -1191,7 +1191,7 @@ __device__ inline int q1l_elect(const Q1LArgs &a) {
 }
 
 // TG_Q1L_STATS (build-time): s_memtime cycles per step of each phase, summed
-// over workers (stage Y/T, partials + drain, exchange, P sum, M, Z update)
+// over workers (stage Y/T + partials, drain, exchange, P sum + M + Z update)
 #ifndef TG_Q1L_STATS
 #define TG_Q1L_STATS 0
 #endif
@@ -1202,9 +1202,13 @@ __device__ unsigned long long g_q1l_stats[8];
 #define Q1L_T(v)
 #endif
 
+// L2 = false (n > 32 x 128 = 4096): the placement-independent form -- the
+// grid is the workers (all resident: one workgroup per CU), partials stored
+// write-through (sc1) and read sc1 (MI355X guide "Valid forms" row 1).
+template <bool L2>
 __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
   __shared__ Q1LShared sm;
-  const int w = q1l_elect(a);
+  const int w = L2 ? q1l_elect(a) : int(blockIdx.x);
   if (w < 0) return;
 #if TG_Q1L_STATS
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};
@@ -1227,120 +1231,130 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
     Q1L_T(t0)
     const Q1Op d = a.ops[o];
     const int rend = d.r0 + d.rows;
+    // a sub-chunk wholly above the panel neither contributes (the sum starts
+    // at the panel's sub-chunk) nor changes: it only keeps the step count
+    // (arrival + wait, so that it never runs more than a step ahead of the
+    // partials it will write once the panels reach it)
+    const bool live = R0 + Q1R > d.r0;  // uniform per workgroup
+    if (live) {
 #pragma unroll
-    for (int u = 0; u < Q1R * SB_B / (64 * Q1W); ++u) {
-      const int rl = u * (64 * Q1W / SB_B) + (tid >> 5), row = R0 + rl;
-      sm.Ys[rl][tid & 31] = (row >= d.r0 && row < rend) ? pre.y[u] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < SB_B * SB_B / (64 * Q1W); ++u) {
-      const int e = tid + 64 * Q1W * u;
-      sm.Ts[e >> 5][e & 31] = pre.t[u];
-    }
-    __syncthreads();
-    Q1L_T(t1)
-    // the 16-row blocks' partials Y^T Z (rows outside the panel: 0)
-#pragma unroll
-    for (int rb = 0; rb < Q1BW; ++rb) {
-      const int blk = wid * Q1BW + rb;
-      doublex4 Pa[2];
-#pragma unroll
-      for (int ia = 0; ia < 2; ++ia) Pa[ia] = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int rl = blk * 16 + 4 * q + lr, row = R0 + rl;
-        const bool act = row >= d.r0 && row < rend;
-        const double zv = act ? sm.Zs[rl][lc] : 0.0;
-#pragma unroll
-        for (int ia = 0; ia < 2; ++ia)
-          Pa[ia] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.Ys[rl][ia * 16 + lc], zv, Pa[ia], 0, 0, 0);
+      for (int u = 0; u < Q1R * SB_B / (64 * Q1W); ++u) {
+        const int rl = u * (64 * Q1W / SB_B) + (tid >> 5), row = R0 + rl;
+        sm.Ys[rl][tid & 31] = (row >= d.r0 && row < rend) ? pre.y[u] : 0.0;
       }
 #pragma unroll
-      for (int ia = 0; ia < 2; ++ia)
+      for (int u = 0; u < SB_B * SB_B / (64 * Q1W); ++u) {
+        const int e = tid + 64 * Q1W * u;
+        sm.Ts[e >> 5][e & 31] = pre.t[u];
+      }
+      __syncthreads();
+      // the 16-row blocks' partials Y^T Z (rows outside the panel: 0)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sm.red[blk][ia * 16 + lr + 4 * q][lc] = Pa[ia][q];
-    }
-    __syncthreads();
-    // the sub-chunk partial (blocks in order, as bt_few sums its waves'),
-    // published to the one XCD's L2
-    {
+      for (int rb = 0; rb < Q1BW; ++rb) {
+        const int blk = wid * Q1BW + rb;
+        doublex4 Pa[2];
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia) Pa[ia] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = blk * 16 + 4 * q + lr, row = R0 + rl;
+          const bool act = row >= d.r0 && row < rend;
+          const double zv = act ? sm.Zs[rl][lc] : 0.0;
+#pragma unroll
+          for (int ia = 0; ia < 2; ++ia)
+            Pa[ia] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm.Ys[rl][ia * 16 + lc], zv, Pa[ia], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sm.red[blk][ia * 16 + lr + 4 * q][lc] = Pa[ia][q];
+      }
+      __syncthreads();
+      // the sub-chunk partial (blocks in order, as bt_few sums its waves'),
+      // published to the one XCD's L2
       double *mine = a.part + (size_t(o & 1) * W + w) * 512;
       for (int e = tid; e < 512; e += 64 * Q1W) {
         const int r = e >> 4, cc = e & 15;
         double v = 0.0;
 #pragma unroll
         for (int b = 0; b < BW; ++b) v += sm.red[b][r][cc];
-        mine[e] = v;
+        if constexpr (L2)
+          mine[e] = v;  // stays in the one XCD's L2
+        else
+          __hip_atomic_store(&mine[e], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    Q1L_T(t1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores drained
     __syncthreads();
     Q1L_T(t2)
     // the next step's Y and T: in flight through the exchange below (issued
     // after the drain, which would otherwise wait for them too)
-    if (o + 1 < a.nops) q1l_fetch(a, a.ops[o + 1], R0, pre);
+    if (o + 1 < a.nops && R0 + Q1R > a.ops[o + 1].r0) q1l_fetch(a, a.ops[o + 1], R0, pre);
     if (wid == 0) {
       tg::wave_arrive(a.cnt);
       tg::spin_geq(a.cnt, unsigned(W) * unsigned(o + 1), a.stall, a.timeout);
     }
     __syncthreads();
     Q1L_T(t3)
-    // P = sum of the sub-chunk partials from the panel's first, in order:
-    // entries 2 tid, 2 tid + 1 of every sub-chunk, all loads in flight at once
-    {
-      const int j0 = d.r0 / Q1S;
-      double v0 = 0.0, v1 = 0.0;
-      for (int jb = j0; jb < W; jb += 32) {
-        doublex2 t[32];
+    if (live) {
+      // P = sum of the sub-chunk partials from the panel's first, in order:
+      // entries 2 tid, 2 tid + 1 of every sub-chunk, all loads in flight at once
+      {
+        const int j0 = d.r0 / Q1S;
+        double v0 = 0.0, v1 = 0.0;
+        for (int jb = j0; jb < W; jb += 32) {
+          doublex2 t[32];
 #pragma unroll
-        for (int b = 0; b < 32; ++b)
-          t[b] = __builtin_bit_cast(
-              doublex2, __builtin_amdgcn_raw_buffer_load_b128(
-                            rp, int(((size_t(o & 1) * W + min(jb + b, W - 1)) * 512 + 2 * tid) * 8),
-                            0, SC1));
+          for (int b = 0; b < 32; ++b)
+            t[b] = __builtin_bit_cast(
+                doublex2, __builtin_amdgcn_raw_buffer_load_b128(
+                              rp, int(((size_t(o & 1) * W + min(jb + b, W - 1)) * 512 + 2 * tid) * 8),
+                              0, SC1));
 #pragma unroll
-        for (int b = 0; b < 32; ++b)
-          if (jb + b < W) {
-            v0 += t[b][0];
-            v1 += t[b][1];
-          }
+          for (int b = 0; b < 32; ++b)
+            if (jb + b < W) {
+              v0 += t[b][0];
+              v1 += t[b][1];
+            }
+        }
+        const int e = 2 * tid;
+        sm.Ps[e >> 4][e & 15] = v0;
+        sm.Ps[e >> 4][(e & 15) + 1] = v1;
       }
-      const int e = 2 * tid;
-      sm.Ps[e >> 4][e & 15] = v0;
-      sm.Ps[e >> 4][(e & 15) + 1] = v1;
+      __syncthreads();
+      // M = T P (q1_tp_mfma: waves 0, 1; T upper triangular)
+      if (wid < 2) {
+        const doublex4 mt = q1_tp_mfma<SB_B + 1, 17>(&sm.Ts[0][0], &sm.Ps[0][0], wid);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sm.Ms[wid * 16 + lr + 4 * q][lc] = mt[q];
+      }
+      __syncthreads();
+      // Z -= Y M on this wave's rows
+      doublex4 F[Q1BW];
+#pragma unroll
+      for (int rb = 0; rb < Q1BW; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F[rb][q] = sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc];
+#pragma unroll
+      for (int k0 = 0; k0 < SB_B; k0 += 4) {
+        const double bm = sm.Ms[k0 + lr][lc];
+#pragma unroll
+        for (int rb = 0; rb < Q1BW; ++rb) {
+          const int rl = (wid * Q1BW + rb) * 16 + lc, row = R0 + rl;
+          const bool act = row >= d.r0 && row < rend;
+          const double ya = act ? -sm.Ys[rl][k0 + lr] : 0.0;
+          F[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm, F[rb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int rb = 0; rb < Q1BW; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc] = F[rb][q];
+      __syncthreads();  // Ms, Ts, Ps, Ys, red reused by the next step
     }
-    __syncthreads();
     Q1L_T(t4)
-    // M = T P (q1_tp_mfma: waves 0, 1; T upper triangular)
-    if (wid < 2) {
-      const doublex4 mt = q1_tp_mfma<SB_B + 1, 17>(&sm.Ts[0][0], &sm.Ps[0][0], wid);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sm.Ms[wid * 16 + lr + 4 * q][lc] = mt[q];
-    }
-    __syncthreads();
     Q1L_T(t5)
-    // Z -= Y M on this wave's rows
-    doublex4 F[Q1BW];
-#pragma unroll
-    for (int rb = 0; rb < Q1BW; ++rb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) F[rb][q] = sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc];
-#pragma unroll
-    for (int k0 = 0; k0 < SB_B; k0 += 4) {
-      const double bm = sm.Ms[k0 + lr][lc];
-#pragma unroll
-      for (int rb = 0; rb < Q1BW; ++rb) {
-        const int rl = (wid * Q1BW + rb) * 16 + lc, row = R0 + rl;
-        const bool act = row >= d.r0 && row < rend;
-        const double ya = act ? -sm.Ys[rl][k0 + lr] : 0.0;
-        F[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya, bm, F[rb], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int rb = 0; rb < Q1BW; ++rb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sm.Zs[(wid * Q1BW + rb) * 16 + lr + 4 * q][lc] = F[rb][q];
-    __syncthreads();  // Ms, Ts, Ps, Ys, red reused by the next step
 #if TG_Q1L_STATS
     const uint64_t t6 = __builtin_amdgcn_s_memtime();
     st[0] += t1 - t0;
@@ -1476,9 +1490,12 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       a.nlev2 = 0;  // bt_few_kernel: Q1 only
       // Q1 with Z in LDS as well (single-level plans; TG_BT_Q1_LDS=0: bt_few's)
       const char *q1l = getenv("TG_BT_Q1_LDS");  // development switch, read per call
-      // (its workers are the workgroups of one XCD: at most its CUs, n <= 4096)
+      // (n <= 4096: the workgroups of one XCD; larger n: one workgroup per CU
+      // of the device, placement-independent hand-offs)
       const int W1 = cdiv(n, Q1R);
-      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 && W1 <= xq.cus_per_xcd) {
+      const bool q1l2 = W1 <= xq.cus_per_xcd;
+      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 &&
+          (q1l2 || W1 <= xq.xcds * xq.cus_per_xcd)) {
         // partials in bt_few's sub-chunk partial area; arrivals in cnt[5],
         // the XCD election in cnt[24..27]
         Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, cnt + 5, cnt + 24, cnt + 1, W1,
@@ -1486,8 +1503,12 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
         auto t1 = prof_begin(st, PROF_Q1, 0.0, 0.0);
         // TG_BT_Q1_LDS=2 (tests): a grid of W1 only, spread over the XCDs, so
         // the election comes up short and the bt_few fallback runs
-        const int g1 = (q1l && q1l[0] == '2') ? W1 : W1 * xq.xcds;
-        hipLaunchKernelGGL(q1_lds_kernel, dim3(g1), dim3(64 * Q1W), 0, st, la);
+        if (q1l2) {
+          const int g1 = (q1l && q1l[0] == '2') ? W1 : W1 * xq.xcds;
+          hipLaunchKernelGGL(q1_lds_kernel<true>, dim3(g1), dim3(64 * Q1W), 0, st, la);
+        } else {
+          hipLaunchKernelGGL(q1_lds_kernel<false>, dim3(W1), dim3(64 * Q1W), 0, st, la);
+        }
         prof_end(st, t1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // did the workers land on one XCD?  (the sync is the one the
@@ -1503,9 +1524,9 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
           unsigned long long q[8];
           (void)hipMemcpyFromSymbol(q, HIP_SYMBOL(g_q1l_stats), sizeof(q));
           const double ns = double(q[6] ? q[6] : 1);
-          fprintf(stderr, "q1_lds n=%d: %llu worker-steps; cycles per step: stage %.0f, partials %.0f, "
-                  "exchange %.0f, P sum %.0f, M %.0f, Z update %.0f\n", n, q[6], q[0] / ns, q[1] / ns,
-                  q[2] / ns, q[3] / ns, q[4] / ns, q[5] / ns);
+          fprintf(stderr, "q1_lds n=%d: %llu worker-steps; cycles per step: stage + partials %.0f, "
+                  "drain %.0f, exchange %.0f, P sum + M + update %.0f\n", n, q[6], q[0] / ns,
+                  q[1] / ns, q[2] / ns, q[3] / ns + q[4] / ns + q[5] / ns);
           const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           (void)hipMemcpyToSymbol(HIP_SYMBOL(g_q1l_stats), z, sizeof(z));
         }

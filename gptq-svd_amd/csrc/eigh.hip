@@ -1001,7 +1001,11 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 // issue each, so row i keeps {1/pivot, du, du2, x} together (32 bytes) and
 // moves as two 16-byte accesses.  The whole wave rescales.  Same dgttrf
 // pivoting and substitution order as invit_kernel.
+// GR (n > 5120: the rows do not fit the LDS): the same kernel with the rows
+// in a per-vector slab of global memory (w.lu), the next chunk's rows
+// prefetched through each sweep so the chain still waits on no load.
 constexpr int IFCH = 16;
+template <bool GR>
 __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict__ d,
                                                        const double *__restrict__ e, int n, int k,
                                                        int first,
@@ -1009,10 +1013,11 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
                                                        const double *__restrict__ bnd, int iters,
                                                        int refac,
                                                        Tri w) {
-  extern __shared__ double2 rows[];  // rows[2i] = {1/pivot, du}, rows[2i+1] = {du2, x}
-  // after the rows: the interchange bits of each IFCH-step chunk
-  unsigned *swm = reinterpret_cast<unsigned *>(rows + 2 * size_t(n));
+  extern __shared__ double2 lds_rows[];  // rows[2i] = {1/pivot, du}, rows[2i+1] = {du2, x}
   const int jj = blockIdx.x, lane = threadIdx.x;
+  double2 *rows = GR ? reinterpret_cast<double2 *>(w.lu + size_t(jj) * 4 * size_t(n)) : lds_rows;
+  // after the LDS rows (or from the start): the interchange bits of each IFCH-step chunk
+  unsigned *swm = reinterpret_cast<unsigned *>(lds_rows + (GR ? 0 : 2 * size_t(n)));
   const int gi = n - 1 - (first + jj);
   const double lam = w_asc[gi];
   const int sl = w.slot[gi];
@@ -1059,6 +1064,11 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
           b[u] = eat(i);
         }
       };
+      // x of the rows after steps i0 .. i0 + IFCH - 1
+      auto xload = [&](int i0, double *a) {
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) a[u] = X(min(i0 + u + 1 + vz, m - 1));
+      };
       // one dgttrf step + forward substitution, branch-free.  Row interchange
       // when !(|cur_d| >= |sub|); lane masks + v_cndmask keep the compiler from
       // turning the selects into exec-mask branches.  a / b = q0 + r1 (a - b q0)
@@ -1089,13 +1099,14 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
         // (free until the final write) and the interchanges to LDS bit masks,
         // so later iterations only substitute (the factors do not change)
         fetch(0, dn, en);
+        double xn[IFCH], xp[IFCH];
+        xload(0, xn);
         for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
           const int cnt = min(IFCH, m - 1 - i0);
           fetch(i0 + IFCH, pd, pe);  // next chunk in flight while this one runs
-          double xn[IFCH], fo[IFCH];
+          xload(i0 + IFCH, xp);      // (rows this chunk does not write)
+          double fo[IFCH];
           unsigned msk = 0;
-#pragma unroll
-          for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
           if (cnt == IFCH) {
             // outputs leave in one batch after the chunk, off the chain
             double2 o0[IFCH], o1[IFCH];
@@ -1113,21 +1124,24 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
               if (iters > 1) fz[size_t(b0 + i0 + u) * K] = fo[u];
             }
           } else {
-            for (int u = 0; u < cnt; ++u) {
-              double2 o0, o1;
-              unsigned b;
-              step(en[u], dn[u] - lam, eat(i0 + u + 1), xn[u], o0, o1, fo[0], b);
-              msk |= b << u;
-              rows[2 * (i0 + u)] = o0;
-              rows[2 * (i0 + u) + 1] = o1;
-              if (iters > 1) fz[size_t(b0 + i0 + u) * K] = fo[0];
-            }
+#pragma unroll
+            for (int u = 0; u < IFCH; ++u)
+              if (u < cnt) {
+                double2 o0, o1;
+                unsigned b;
+                step(en[u], dn[u] - lam, eat(i0 + u + 1), xn[u], o0, o1, fo[0], b);
+                msk |= b << u;
+                rows[2 * (i0 + u)] = o0;
+                rows[2 * (i0 + u) + 1] = o1;
+                if (iters > 1) fz[size_t(b0 + i0 + u) * K] = fo[0];
+              }
           }
           swm[i0 / IFCH] = msk;
 #pragma unroll
           for (int u = 0; u < IFCH; ++u) {
             dn[u] = pd[u];
             en[u] = pe[u];
+            xn[u] = xp[u];
           }
         }
         rows[2 * (m - 1)] = make_double2(rcp2(clampp(cur_d)), 0.0);
@@ -1143,13 +1157,14 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
             a[u] = fz[size_t(b0 + min(i0 + u + vz, max(m - 2, 0))) * K];
         };
         ffetch(0, fc);
+        double xn[IFCH], xp[IFCH];
+        xload(0, xn);
         for (int i0 = 0; i0 < m - 1; i0 += IFCH) {
           const int cnt = min(IFCH, m - 1 - i0);
           ffetch(i0 + IFCH, fp);
+          xload(i0 + IFCH, xp);
           const unsigned msk = swm[i0 / IFCH];
-          double xn[IFCH], xo[IFCH];
-#pragma unroll
-          for (int u = 0; u < IFCH; ++u) xn[u] = X(min(i0 + u + 1, m - 1));
+          double xo[IFCH];
           if (cnt == IFCH) {
 #pragma unroll
             for (int u = 0; u < IFCH; ++u) {
@@ -1161,15 +1176,20 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
 #pragma unroll
             for (int u = 0; u < IFCH; ++u) X(i0 + u) = xo[u];
           } else {
-            for (int u = 0; u < cnt; ++u) {
-              const bool sw = (msk >> u) & 1u;
-              const double A = sw ? xi : xn[u], B = sw ? xn[u] : xi;
-              X(i0 + u) = B;
-              xi = fma(-fc[u], B, A);
-            }
+#pragma unroll
+            for (int u = 0; u < IFCH; ++u)
+              if (u < cnt) {
+                const bool sw = (msk >> u) & 1u;
+                const double A = sw ? xi : xn[u], B = sw ? xn[u] : xi;
+                X(i0 + u) = B;
+                xi = fma(-fc[u], B, A);
+              }
           }
 #pragma unroll
-          for (int u = 0; u < IFCH; ++u) fc[u] = fp[u];
+          for (int u = 0; u < IFCH; ++u) {
+            fc[u] = fp[u];
+            xn[u] = xp[u];
+          }
         }
       }
       rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
@@ -1182,6 +1202,17 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
         amax = fmax(amax, fabs(v));
         return v;
       };
+      if constexpr (GR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sweep's row stores
+      double2 q0[IFCH], q1[IFCH];  // the chunk below the current one, in flight
+      auto rload = [&](int i0, double2 *a, double2 *b) {
+#pragma unroll
+        for (int u = 0; u < IFCH; ++u) {
+          const int i = max(i0, 0) + u + vz;
+          a[u] = rows[2 * i];
+          b[u] = rows[2 * i + 1];
+        }
+      };
+      if (m - IFCH >= 0) rload(m - IFCH, q0, q1);
       for (int i1 = m; i1 > 0; i1 -= IFCH) {
         const int i0 = i1 - IFCH;
         if (i0 >= 0) {
@@ -1189,9 +1220,10 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
           double xv[IFCH];
 #pragma unroll
           for (int u = 0; u < IFCH; ++u) {
-            r0[u] = rows[2 * (i0 + u)];
-            r1[u] = rows[2 * (i0 + u) + 1];
+            r0[u] = q0[u];
+            r1[u] = q1[u];
           }
+          if (i0 - IFCH >= 0) rload(i0 - IFCH, q0, q1);
 #pragma unroll
           for (int u = IFCH - 1; u >= 0; --u) xv[u] = bstep(r0[u], r1[u]);
 #pragma unroll
@@ -1705,14 +1737,25 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   const int iters = ie ? std::max(1, std::min(5, atoi(ie))) : 2;
   // few vectors: one LDS-resident wave per vector (4 doubles per row of T,
   // + one interchange mask per IFCH rows)
-  const size_t ilds = 4 * sizeof(double) * size_t(n) + 4 * size_t(tg::cdiv(n, IFCH));
-  if (k <= 256 && ilds <= 160 * 1024 && !getenv("TG_INVIT_REG")) {
-    TG_HIP(hipFuncSetAttribute((const void *)invit_lds_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, int(ilds)));
-    // TG_INVIT_REFACTOR=1 (tests): factor again in every iteration
-    const char *rf = getenv("TG_INVIT_REFACTOR");
-    hipLaunchKernelGGL(invit_lds_kernel, dim3(k), dim3(64), ilds, st, w.d, w.es, n, k, first,
-                       w_asc, bnd, iters, (rf && rf[0] == '1') ? 1 : 0, w);
+  const size_t imask = 4 * size_t(tg::cdiv(n, IFCH));
+  const size_t ilds = 4 * sizeof(double) * size_t(n) + imask;
+  // TG_INVIT_REFACTOR=1 (tests): factor again in every iteration
+  const char *rf = getenv("TG_INVIT_REFACTOR");
+  const int refac = (rf && rf[0] == '1') ? 1 : 0;
+  // (n > 5120: the rows in a per-vector slab of w.lu, 4 n k <= 3 n^2 doubles)
+  const char *ig = getenv("TG_INVIT_GROWS");  // development switch: 1 = global rows at any n
+  const bool grows = ilds > 160 * 1024 || (ig && ig[0] == '1');
+  const char *ir = getenv("TG_INVIT_REG");  // development switch: 1 = the register kernel
+  if (k <= 256 && !(ir && ir[0] == '1')) {
+    if (grows) {
+      hipLaunchKernelGGL(invit_lds_kernel<true>, dim3(k), dim3(64), imask, st, w.d, w.es, n, k,
+                         first, w_asc, bnd, iters, refac, w);
+    } else {
+      TG_HIP(hipFuncSetAttribute((const void *)invit_lds_kernel<false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(ilds)));
+      hipLaunchKernelGGL(invit_lds_kernel<false>, dim3(k), dim3(64), ilds, st, w.d, w.es, n, k,
+                         first, w_asc, bnd, iters, refac, w);
+    }
   } else {
     hipLaunchKernelGGL(invit_kernel, dim3(tg::cdiv(k, 64)), dim3(64), 0, st, w.d, w.es, n, k,
                        first, w_asc, bnd, iters, w);

@@ -35,6 +35,7 @@ def _blockdiag(n, seed):
 @pytest.mark.parametrize("n,first,count,kind", [
     (600, 0, 14, "wishart"), (2048, 1500, 14, "wishart"), (2048, 0, 48, "wishart"),
     (4100, 3058, 14, "wishart"), (4100, 4099, 1, "wishart"), (1000, 0, 300, "wishart"),
+    (6000, 4500, 14, "wishart"),
     (700, 0, 20, "blockdiag"), (700, 640, 60, "blockdiag")])
 def test_few_vectors(n, first, count, kind):
     from gptq_svd_amd import _lib as lib
@@ -258,7 +259,7 @@ def test_q2_lds_bit_identical(n, count, monkeypatch):
 
 
 @pytest.mark.parametrize("n,count", [(4096, 14), (4096, 1), (600, 14), (1000, 16), (3000, 14),
-                                     (4000, 14), (4200, 14)])
+                                     (4000, 14), (4200, 14), (9000, 14)])
 def test_q1_lds_bit_identical(n, count, monkeypatch):
     """The few-vector Q1 with Z resident in LDS (csrc/backtr.hip
     q1_lds_kernel, the default after q2_lds_kernel on single-level plans up
@@ -269,8 +270,9 @@ def test_q1_lds_bit_identical(n, count, monkeypatch):
     and form M = T P with the same MFMA sequence.  TG_BT_Q1_LDS=2 launches
     too few workgroups for one XCD, so the election fails and bt_few's Q1
     runs instead: the same vectors again.  n = 3000 / 4000 / 600: a partial
-    last sub-chunk; n = 4096: all 32 CUs of the XCD; n = 4200: 33 sub-chunks,
-    more than one XCD's CUs (bt_few's Q1 only)."""
+    last sub-chunk; n = 4096: all 32 CUs of the XCD; n = 4200 / 9000: 33 / 71
+    sub-chunks, more than one XCD's CUs: the placement-independent form
+    (q1_lds_kernel<false>, write-through partials, one workgroup per CU)."""
     from gptq_svd_amd import _lib as lib
     H = torch.from_numpy(_wishart(n, 23)).to(DEV)
     ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
@@ -348,3 +350,30 @@ def test_xm_fused_w_bit_identical(n, monkeypatch):
     ref = values("0")
     for _ in range(2):
         assert np.array_equal(values("1"), ref)
+
+
+@pytest.mark.parametrize("n,count", [(4096, 14), (3001, 5)])
+def test_invit_global_rows_bit_identical(n, count, monkeypatch):
+    """Inverse iteration with the rows in a per-vector global slab (csrc/
+    eigh.hip invit_lds_kernel<true>, the default past n = 5120 where the
+    rows do not fit the LDS; TG_INVIT_GROWS=1 forces it) gives the LDS-row
+    kernel's vectors bit for bit (same operations; only where the rows live
+    and how far ahead they are fetched differ)."""
+    from gptq_svd_amd import _lib as lib
+    H = torch.from_numpy(_wishart(n, 43)).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def vectors(flag):
+        monkeypatch.setenv("TG_INVIT_GROWS", flag)
+        A = H.clone()
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        V = torch.empty((count, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - count, count,
+                 lib.ptr(V), n, lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    ref = vectors("0")
+    assert np.array_equal(vectors("1"), ref)

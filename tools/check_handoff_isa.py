@@ -6,11 +6,11 @@ The kernels hand data from one workgroup to another inside a launch in two
 forms (MI355X_MICROARCH.md § visibility):
 
 * write-through form (pqr_kernel, xm_kernel, the pivot kernels, the
-  boundary chunks of q2_lds_kernel): payload
+  boundary chunks of q2_lds_kernel, q1_lds_kernel<false>): payload
   stored `sc1`, every storing wave drains `vmcnt(0)`, one lane signals (an
   agent-scope atomic add or `sc1` store); the consumer polls the word and
   reads the payload with `sc1` loads -- the guide's "Valid forms" row 1;
-* one-L2 form (bulge_lds_kernel, bulge_df_kernel, bt_few_kernel, q1_lds_kernel):
+* one-L2 form (bulge_lds_kernel, bulge_df_kernel, bt_few_kernel, q1_lds_kernel<true>):
   the workers are the workgroups that landed on ONE XCD (HW_REG_XCC_ID
   election; the others exit before touching the data), the payload is
   stored plain (the lines stay in that XCD's L2, the point of coherence of
@@ -58,7 +58,8 @@ KERNELS = {
                  ("bt_few_kernelILi2ELb1E", True, False, True),
                  ("bt_few_kernelILi1ELb0E", True, False, True),
                  ("bt_few_kernelILi2ELb0E", True, False, True),
-                 ("q2_lds_kernelILi1E", False, False, True), ("q1_lds_kernel", True, False, True)],
+                 ("q2_lds_kernelILi1E", False, False, True), ("q1_lds_kernelILb1E", True, False, True),
+                 ("q1_lds_kernelILb0E", False, False, True)],
     # pqr: the hand-off words and payloads go through explicit address_space(1)
     # sc1 atomics (st_sc1 / ld_sc1); its flat accesses are the panel rows of
     # the launch's input and its outputs, reached through the LDS copy of the
