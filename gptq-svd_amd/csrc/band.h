@@ -56,6 +56,7 @@ struct SbBufs {
   double *pq_part, *pq_bc;
   unsigned *pq_ctl;       // [0] timeout flag, [1] M-kernel ticket, [4 + 4 i] panel i counters
   unsigned *xm_tick;      // X / M kernel tickets (band.hip xm_kernel), xm_tick_words(n)
+  double *xm_xpart;       // X / M K-split partial X blocks, xm_xpart_doubles(n)
 };
 
 int pqr_rows_per_thread(int m);
@@ -72,7 +73,13 @@ size_t sb2st_t2_count(int n);
 // control words: 4 + 4 per panel, padded to a multiple of 16 bytes
 inline size_t pq_ctl_words(int n) { return 4 + 4 * size_t(std::max(1, n / SB_B + 1)); }
 // X / M kernel: one ticket per group of 32 row blocks of 16 rows, + 1
-inline size_t xm_tick_words(int n) { return size_t(n) / 256 + 8; }
+// X / M control words: group tickets [0, n / 256 + 7), the fused-W flag at
+// n / 256 + 7, the K-split column-block tickets from n / 256 + 8 (n / 16 + 2)
+inline size_t xm_mflag_off(int n) { return size_t(n) / 256 + 7; }
+inline size_t xm_cbt_off(int n) { return size_t(n) / 256 + 8; }
+inline size_t xm_tick_words(int n) { return xm_cbt_off(n) + size_t(n) / 16 + 2; }
+// K-split partial X blocks: at most 8 splits of every 32-row block
+inline size_t xm_xpart_doubles(int n) { return 8 * (size_t(n) + 32) * 32; }
 
 template <class A>
 void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
@@ -118,6 +125,7 @@ void sb_layout(A &ar, int n, int kmax, const SbPlan &pl, SbBufs *bp) {
   else ar.template take<unsigned>(pq_ctl_words(n));
   if constexpr (std::is_same_v<A, Arena>) b.xm_tick = ar.template take<unsigned>(xm_tick_words(n));
   else ar.template take<unsigned>(xm_tick_words(n));
+  take(b.xm_xpart, xm_xpart_doubles(n));
 }
 
 // A (n x n symmetric, full storage, lda) -> band matrix of half-bandwidth

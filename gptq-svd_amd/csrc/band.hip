@@ -726,6 +726,13 @@ struct XmArgs {
   unsigned *mflag, epoch;
   unsigned *stall;  // timeout flag of the wait (the band reduction's, pq_ctl[0])
   unsigned long long timeout;
+  // K split: S workgroups per column block, each over kc rows of A22 (a
+  // multiple of 32); their partial X blocks meet in xpart (write-through) and
+  // the last of the S (ticket cbt[cb], reset by it) sums them in split order
+  // and goes on as the block's workgroup.  S = 1: no split.
+  int S, kc;
+  double *xpart;
+  unsigned *cbt;
 };
 // doubles of one block's partials: Y^T X, + the four pair products
 __host__ __device__ inline int xm_np(const XmArgs &g) { return g.Ya ? 5 : 1; }
@@ -885,8 +892,8 @@ __device__ __forceinline__ void xm_drain_slot(XmStep<NBC> &f) {
 // m - 1's value is the load's second element
 template <int NBC>
 __device__ __forceinline__ void xm_mma(const XmStep<NBC> &f, const bool (&cok)[NBC], bool sh,
-                                       int k0, doublex4 (&acc)[NBC][2], int m) {
-  const bool kok = k0 + ((threadIdx.x & 63) >> 4) < m;
+                                       int k0, doublex4 (&acc)[NBC][2], int kend) {
+  const bool kok = k0 + ((threadIdx.x & 63) >> 4) < kend;  // rows of this workgroup's K range
 #pragma unroll
   for (int c = 0; c < NBC; ++c) {
     double v = xm_b<NBC>(f, c);
@@ -960,8 +967,11 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform K loop
-  const int r0 = blockIdx.x * RB;
-  const int G = int(gridDim.x), NG = (G + XG - 1) / XG;
+  // column block cb, K split ks (the S splits of a block are adjacent)
+  const int cb = int(blockIdx.x) / g.S, ks = int(blockIdx.x) - cb * g.S;
+  const int r0 = cb * RB;
+  const int G = int(gridDim.x) / g.S, NG = (G + XG - 1) / XG;
+  const int kbeg = ks * g.kc, kend = min(g.m, kbeg + g.kc);
   constexpr int YPT = RB * SB_B / (64 * XW);  // Y values per thread
   double yv[YPT];
 #pragma unroll
@@ -969,8 +979,8 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31, row = r0 + rr;
     yv[u] = row < g.m ? g.Y[int64_t(row) * SB_B + c] : 0.0;
   }
-  // wave w takes the K steps w, w + XW, ... (4 rows of A22 each)
-  const int KS = 4 * XW, kb = 4 * wid;
+  // wave w takes the K steps w, w + XW, ... (4 rows of A22 each) of the range
+  const int KS = 4 * XW, kb = kbeg + 4 * wid;
   int colc[NBC];
   bool cok[NBC];
   // packed pair (m - 1, m) of an odd m: loaded as (m - 2, m - 1), see xm_mma
@@ -992,8 +1002,8 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   for (int c = 0; c < NBC; ++c)
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[c][i] = doublex4{0.0, 0.0, 0.0, 0.0};
-  if (kb < g.m && g.asm_loads) {
-    const int nit = (g.m - kb + KS - 1) / KS;
+  if (kb < kend && g.asm_loads) {
+    const int nit = (kend - kb + KS - 1) / KS;
     XmStep<NBC> f[DA];
 #pragma unroll
     for (int u = 0; u < DA; ++u) xm_load_asm<NBC>(g, colc, kb + KS * u, f[u]);
@@ -1002,14 +1012,14 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
       for (int u = 0; u < DA; ++u) {
         const int k0 = kb + KS * (it + u);
         xm_wait_slot<NBC, DA>(f[u]);
-        xm_mma<NBC>(f[u], cok, csh, k0, acc, g.m);
+        xm_mma<NBC>(f[u], cok, csh, k0, acc, kend);
         xm_load_asm<NBC>(g, colc, k0 + KS * DA, f[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < DA; ++u) xm_drain_slot<NBC>(f[u]);
-  } else if (kb < g.m) {
-    const int nit = (g.m - kb + KS - 1) / KS;
+  } else if (kb < kend) {
+    const int nit = (kend - kb + KS - 1) / KS;
     XmStep<NBC> f[DA];
 #pragma unroll
     for (int u = 0; u < DA; ++u) xm_load<NBC>(g, colc, kb + KS * u, f[u]);
@@ -1023,7 +1033,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
         // then the load of step it + u + DA into the freed slot): the
         // machine scheduler otherwise sinks prefetches next to their uses
         const int k0 = kb + KS * (it + u);
-        xm_mma<NBC>(f[u], cok, csh, k0, acc, g.m);
+        xm_mma<NBC>(f[u], cok, csh, k0, acc, kend);
         __builtin_amdgcn_sched_barrier(0);
         xm_load<NBC>(g, colc, k0 + KS * DA, f[u]);
         __builtin_amdgcn_sched_barrier(0);
@@ -1051,8 +1061,39 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
     double x = 0.0;
 #pragma unroll
     for (int w = 0; w < XW; ++w) x += red[w][rr][c];
-    if (r0 + rr < g.m) g.X[int64_t(r0 + rr) * SB_B + c] = x;
-    xv[u] = r0 + rr < g.m ? x : 0.0;
+    xv[u] = x;
+  }
+  if (g.S > 1) {
+    // this split's partial X block, write-through; the last of the block's
+    // S splits sums them in split order and goes on
+    double *mine = g.xpart + (size_t(cb) * g.S + ks) * (RB * SB_B);
+#pragma unroll
+    for (int u = 0; u < YPT; ++u)
+      __hip_atomic_store(&mine[tid + u * 64 * XW], xv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      s_last = __hip_atomic_fetch_add(&g.cbt[cb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               unsigned(g.S - 1);
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) tg::ctl_reset(&g.cbt[cb]);
+    const double *blk = g.xpart + size_t(cb) * g.S * (RB * SB_B);
+#pragma unroll
+    for (int u = 0; u < YPT; ++u) {
+      const int e = tid + u * 64 * XW;
+      double x = 0.0;
+      for (int z = 0; z < g.S; ++z)
+        x += __hip_atomic_load(&blk[size_t(z) * (RB * SB_B) + e], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      xv[u] = x;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < YPT; ++u) {
+    const int e = tid + u * 64 * XW, rr = e >> 5, c = e & 31;
+    if (r0 + rr < g.m) g.X[int64_t(r0 + rr) * SB_B + c] = xv[u];
+    xv[u] = r0 + rr < g.m ? xv[u] : 0.0;
   }
   __syncthreads();  // red is free: its first two slices take the block's X and Y rows
 #pragma unroll
@@ -1079,7 +1120,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   }
   __syncthreads();
   // this block's Y_zᵀ X_z (and the pair products), write-through, then the group ticket
-  double *mypart = g.part + size_t(blockIdx.x) * NP * 1024;
+  double *mypart = g.part + size_t(cb) * NP * 1024;
   for (int e = tid; e < SB_B * SB_B; e += 64 * XW) {
     const int a = e >> 5, c = e & 31;
     double p = 0.0;
@@ -1103,7 +1144,7 @@ __global__ __launch_bounds__(64 * XW, NBC == 2 ? TG_XM_MINW2 : 1) void xm_kernel
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int grp = blockIdx.x / XG, z0 = grp * XG, z1 = min(G, z0 + XG);
+  const int grp = cb / XG, z0 = grp * XG, z1 = min(G, z0 + XG);
   if (tid == 0)
     s_last = __hip_atomic_fetch_add(&g.tick[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
              unsigned(z1 - z0 - 1);
@@ -1817,14 +1858,33 @@ static int xm_resident() {
 // epoch > 0: fuse W = X - Y M / 2 into the launch when every workgroup fits
 // the device at once (they wait for M); returns *fused (false: the caller
 // runs w_update_kernel)
+// K splits per column block (TG_XM_KSPLIT=s forces s, 1 = none, 0 = the
+// default; read per call): the column-block grid alone leaves CUs idle once m / (16 NBC) is
+// below the device's workgroup slots, and at m / 32 = 192 .. 384 blocks of
+// the HBM-resident NBC = 2 launches it puts two blocks on some CUs and one on
+// others.  Splitting K brings the grid to about three rounds of 512
+// workgroups (two per CU on 256 CUs) -- a function of m only, so the
+// results do not depend on the device.
+// Measured (profiles/r06/env_ab_*_ksplit.log): n = 12,288 392.8 -> 389.7 ms
+// (the NBC = 2 launches 244 -> 226 us), but n = 4096 56.96 -> 58.30 ms (the
+// 16-column launches are MALL-resident and their extra partial hand-off
+// costs more than the balance gains), so only the 32-column form splits.
+static int xm_ksplit(int m, int G, int nbc) {
+  const char *e = getenv("TG_XM_KSPLIT");  // 0 / unset: the default below
+  int S = (e && atoi(e) > 0) ? atoi(e) : (nbc == 1 || G >= 1536 ? 1 : cdiv(1536, G));
+  S = std::max(1, std::min(8, S));
+  while (S > 1 && cdiv(m, S) < 4 * 32) --S;  // at least 128 rows per split
+  return S;
+}
 static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const double *YT,
                             const double *Yp, const double *Tp, double *X, const SbBufs &b,
-                            const double *Ya = nullptr, const double *Wa = nullptr,
-                            double *PQ = nullptr, unsigned epoch = 0, unsigned *mflag = nullptr,
-                            bool *fused = nullptr) {
+                            int n, const double *Ya = nullptr, const double *Wa = nullptr,
+                            double *PQ = nullptr, unsigned epoch = 0, bool *fused = nullptr) {
   const int nbc = xm_nbc(m);
   if (Ya && nbc != 2) return hipErrorInvalidValue;
   const int G = cdiv(m, XR * nbc), np = Ya ? 5 : 1;
+  const int S = xm_ksplit(m, G, nbc), kc = cdiv(cdiv(m, S), 32) * 32;
+  unsigned *mflag = b.xm_tick + xm_mflag_off(n);
   const char *xs = getenv("TG_XM_ASM");  // development switch: 0 = compiler-scheduled loads
   const int asm_loads = !(xs && xs[0] == '0');
   // TG_XM_FUSE_W=1 (development switch, per call): W inside the launch.  Measured
@@ -1837,15 +1897,15 @@ static hipError_t launch_xm(hipStream_t st, double *A22, int lda, int m, const d
   // the multi-rank tests -- can both have every workgroup of a launch
   // resident at once: the waiting workgroups never block the ones that
   // would publish M.)
-  const bool fuse = epoch > 0 && mflag && !Ya && nbc == 1 && (fw && fw[0] == '1') &&
-                    2 * G <= xm_resident<1>();
+  const bool fuse = epoch > 0 && !Ya && nbc == 1 && (fw && fw[0] == '1') &&
+                    2 * G * S <= xm_resident<1>();
   if (fused) *fused = fuse;
   static const unsigned long long tmo_ticks = spin_timeout_ticks("TG_XM_TIMEOUT_TICKS");
   XmArgs xa{A22, int64_t(lda), m, YT, Yp, Tp, X, b.U, b.U + size_t(G) * np * 1024, b.M,
             b.xm_tick, asm_loads, Ya, Wa, PQ, fuse ? 1 : 0,
-            mflag, epoch, b.pq_ctl, tmo_ticks};
-  if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G), dim3(64 * XW), 0, st, xa);
-  else hipLaunchKernelGGL(xm_kernel<1>, dim3(G), dim3(64 * XW), 0, st, xa);
+            mflag, epoch, b.pq_ctl, tmo_ticks, S, kc, b.xm_xpart, b.xm_tick + xm_cbt_off(n)};
+  if (nbc == 2) hipLaunchKernelGGL(xm_kernel<2>, dim3(G * S), dim3(64 * XW), 0, st, xa);
+  else hipLaunchKernelGGL(xm_kernel<1>, dim3(G * S), dim3(64 * XW), 0, st, xa);
   return hipGetLastError();
 }
 
@@ -1901,8 +1961,8 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
     // W = X - Y M / 2 in place: inside the X / M launch where it can be
     // (panel a of a pair needs M only through W as well)
     bool fused = false;
-    TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b, nullptr, nullptr, nullptr,
-                     unsigned(pi + 1), b.xm_tick + xm_tick_words(n) - 1, &fused));
+    TG_CHK(launch_xm(st, A22, lda, m, b.YT, Yp, Tp, Xa, b, n, nullptr, nullptr, nullptr,
+                     unsigned(pi + 1), &fused));
     if (!fused) {
       hipLaunchKernelGGL(w_update_kernel, dim3(cdiv(m, WU_R)), dim3(256), 0, st, Yp, Xa, m, b.M);
       TG_CHK(hipGetLastError());
@@ -1934,7 +1994,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
                     b.pq_ctl + 4 + 4 * pi, b.pq_ctl));
     if (xm_nbc(mb) == 2 && !pair_side) {
       // X_raw, M_raw and the corrections' products in one launch
-      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b, Ya, Wa, b.G));
+      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b, n, Ya, Wa, b.G));
     } else {
       // the corrections' products depend only on panel b's QR and panel a's
       // Y / W: a side stream forms them while X_raw streams the matrix
@@ -1948,7 +2008,7 @@ static hipError_t sy2sb_single(hipStream_t st, double *A, int lda, int n, const 
       hipLaunchKernelGGL(pair_fin_kernel, dim3(1), dim3(1024), 0, ss->s, b.Gr, nblk, Tb, b.G);
       TG_CHK(hipGetLastError());
       TG_CHK(hipEventRecord(ss->ev1[0], ss->s));
-      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b));  // X_raw, M_raw
+      TG_CHK(launch_xm(st, A22b, lda, mb, b.YT, Yb, Tb, Xb, b, n));  // X_raw, M_raw
       TG_CHK(hipStreamWaitEvent(st, ss->ev1[0], 0));
     }
     hipLaunchKernelGGL(w_update2_kernel, dim3(cdiv(mb, WU_R)), dim3(256), 0, st, Yb, Xb, mb, b.M,

@@ -377,3 +377,40 @@ def test_invit_global_rows_bit_identical(n, count, monkeypatch):
 
     ref = vectors("0")
     assert np.array_equal(vectors("1"), ref)
+
+
+@pytest.mark.parametrize("n", [4096, 2000, 7000, 9001])
+def test_xm_ksplit(n, monkeypatch):
+    """The X / M kernel with K split over several workgroups per column
+    block (csrc/band.hip xm_ksplit: by default the 32-column form's grid is
+    brought to ~1536 workgroups; TG_XM_KSPLIT=3 forces three splits of every
+    launch; partial X blocks summed in split order by the last of a block's
+    splits): eigenvalues equal LAPACK's and the unsplit kernel's
+    (TG_XM_KSPLIT=1) to 1e-12 ||H||, and repeat bit for bit.  n = 7000 /
+    9001: the 32-column form, panel pairs, an odd width; n = 2000 / 4096:
+    the 16-column form (forced splits only)."""
+    from gptq_svd_amd import _lib as lib
+    H = _wishart(n, 47)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+
+    def values(split):
+        if split is None:
+            monkeypatch.delenv("TG_XM_KSPLIT", raising=False)
+        else:
+            monkeypatch.setenv("TG_XM_KSPLIT", split)
+        A = torch.from_numpy(H).to(DEV)
+        w = torch.empty(n, dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws),
+                 ws.numel())
+        torch.cuda.synchronize()
+        return np.sort(w.cpu().numpy())
+
+    got = values(None)
+    assert np.array_equal(values(None), got)
+    nrm = np.abs(got).max()
+    ref = np.linalg.eigvalsh(H)
+    assert np.abs(got - ref).max() <= 1e-12 * nrm
+    forced = values("3")
+    assert np.array_equal(values("3"), forced)
+    assert np.abs(forced - ref).max() <= 1e-12 * nrm
+    assert np.abs(got - values("1")).max() <= 1e-12 * nrm

@@ -61,6 +61,8 @@ def rel(a, b):
     {"TG_XM_ASM": "0", "TG_XM_NBC": "2"},
     {"TG_XM_NBC": "2"},
     {"TG_XM_FUSE_W": "1"},
+    {"TG_XM_KSPLIT": "1"},
+    {"TG_XM_KSPLIT": "3"},
     {"TG_URX_SMALLM": "1"},
     {"TG_URX_INV": "1"},
     {"TG_SCHUR_MIRROR": "1"},
