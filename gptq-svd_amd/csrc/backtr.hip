@@ -798,9 +798,10 @@ struct Q2LArgs {
   int n, k;
   const double *V2, *T2;
   int smax, ng2;
-  unsigned *gprog;  // [ng2]: blocks done by each workgroup's lowest group (zeroed)
+  unsigned *gprog;  // [slabs x ng2]: blocks done by each group, per column slab (zeroed)
   unsigned *stall;  // set on a timed-out wait (the host reports it)
   unsigned long long timeout;
+  int slab0;        // first column slab of this launch (slab = slab0 + blockIdx.y)
 };
 
 template <int NCB>
@@ -873,17 +874,23 @@ __device__ unsigned long long g_q2l_stats[8];
 template <int NCB>
 __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
   __shared__ Q2LShared<NCB> sm;
-  const int n = a.n, k = a.k, tid = threadIdx.x, lane = tid & 63;
+  constexpr int KC = 16 * NCB;
+  // column slab slab0 + blockIdx.y: columns KC slab .. of Z (ld a.k), its own
+  // progress words (the columns are independent: each slab is a back-transform
+  // of its own, the same arithmetic as a call with those columns alone)
+  const int slab = a.slab0 + int(blockIdx.y), ld = a.k;
+  double *const Zb = a.Z + KC * slab;
+  unsigned *const gprog = a.gprog + size_t(slab) * a.ng2;
+  const int n = a.n, k = min(KC, a.k - KC * slab), tid = threadIdx.x, lane = tid & 63;
   const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = blockIdx.x, G0 = w * QW, G2 = G0 + g;
   const int gtop = min(QW, a.ng2 - G0) - 1;  // highest wave with a sweep group
   const int lr = lane >> 4, lc = lane & 15;
-  constexpr int KC = 16 * NCB;
   // this workgroup's own chunks G0 .. G0 + QW - 1 from Z (no higher group touches them)
   for (int e = tid; e < QW * 32 * KC; e += 64 * QW) {
     const int q = e / (32 * KC), r = (e / KC) % 32, col = e % KC;
     const int c = G0 + q, row = 32 * c + 1 + r;
-    sm.Zs[c % RS][r][col] = (row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
+    sm.Zs[c % RS][r][col] = (row < n && col < k) ? Zb[int64_t(row) * ld + col] : 0.0;
   }
   if (tid < QW) sm.done[tid] = 0u;
   if (tid == 0) sm.dead = 0u;
@@ -935,7 +942,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
     if (nbu > 0) {
       const unsigned need = unsigned(min(s + 1, nbu));
       if (g < gtop) q2l_wait(&sm.done[g + 1], need, &sm.dead, a.stall, a.timeout);
-      else if (!q2l_get(&sm.dead) && !tg::spin_geq(a.gprog + G2 + 1, need, a.stall, a.timeout))
+      else if (!q2l_get(&sm.dead) && !tg::spin_geq(gprog + G2 + 1, need, a.stall, a.timeout))
         sm.dead = 1u;
     }
     // the top wave brings chunk c + 1 into the ring: its slot held chunk
@@ -966,7 +973,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
           const int col = cb * 16 + lc;
           double v;
           if (gl)
-            v = __hip_atomic_load(&a.Z[int64_t(min(row, n - 1)) * k + min(col, k - 1)],
+            v = __hip_atomic_load(&Zb[int64_t(min(row, n - 1)) * ld + min(col, k - 1)],
                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
             v = sm.Zs[sl][r][col];
@@ -1041,7 +1048,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
           const int col = cb * 16 + lc;
           if (col >= k) continue;
           if (gl)
-            __hip_atomic_store((gu64 *)&a.Z[int64_t(row) * k + col],
+            __hip_atomic_store((gu64 *)&Zb[int64_t(row) * ld + col],
                                __double_as_longlong(F[rb][cb][qq]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
           else
@@ -1056,7 +1063,7 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
     if (g == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
-        __hip_atomic_store((gu32 *)(a.gprog + G2), unsigned(s + 1), __ATOMIC_RELAXED,
+        __hip_atomic_store((gu32 *)(gprog + G2), unsigned(s + 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     wave_sync();  // Vs reused by the next block
@@ -1077,18 +1084,21 @@ __global__ __launch_bounds__(64 * QW, 1) void q2_lds_kernel(Q2LArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Q1 with Z resident in LDS (after q2_lds_kernel, the default for k <= 16,
-// single-level panels and n <= 32 x 128; TG_BT_Q1_LDS=0 keeps bt_few_kernel's
-// Q1).  Q1 is 127 panel steps (n = 4096), Z[r0:] -= Y (T (Y^T Z[r0:])) from
-// the last panel to the first; each step needs P = Y^T Z over every row at or
-// below the panel's, a reduction over the grid.  Here each workgroup holds
-// one 128-row sub-chunk of Z in LDS for the whole launch; per step it stages
-// the step's Y rows (prefetched into registers during the previous step's
-// exchange), forms its sub-chunk's partial on MFMA, publishes it (plain
-// stores in the one XCD's L2) with one arrival on a counter, waits for all W
-// arrivals, sums the partials in sub-chunk order (16-byte sc1 loads, all in
-// flight at once), forms M = T P on MFMA and updates its rows -- one grid
-// exchange per step instead of bt_few's two barriers, Z never re-read.
+// Q1 with Z resident in LDS (after q2_lds_kernel, the default for k <= 16 and
+// single-level panels; TG_BT_Q1_LDS=0 keeps bt_few_kernel's Q1).  Q1 is 127
+// panel steps (n = 4096), Z[r0:] -= Y (T (Y^T Z[r0:])) from the last panel to
+// the first; each step needs P = Y^T Z over every row at or below the panel's,
+// a reduction over the grid.  Here each workgroup holds one 128-row sub-chunk
+// of Z in LDS for the whole launch; per step it stages the step's Y rows
+// (prefetched into registers during the previous step's exchange), forms its
+// sub-chunk's partial on MFMA, publishes it with one arrival on a counter,
+// waits for all W arrivals, sums the partials in sub-chunk order (16-byte sc1
+// loads, all in flight at once), forms M = T P on MFMA and updates its rows --
+// one grid exchange per step instead of bt_few's two barriers, Z never
+// re-read.  A sub-chunk wholly above the panel only keeps the step count.
+// n <= 32 x 128: the workgroups of one XCD, plain partial stores in its L2
+// (L2 = true); larger n: one workgroup per CU anywhere, write-through
+// partials (L2 = false).
 // Bit-identical to bt_few's Q1 (q1_big_a / q1_big_b): the same row-aligned
 // sub-chunks, each the sum of eight 16-row MFMA partials in block order, the
 // sub-chunk sum in the same order (leading sub-chunks above the panel are
@@ -1114,6 +1124,7 @@ struct Q1LArgs {
   unsigned *stall;  // timeout flag
   int nw;           // workers: cdiv(n, Q1R) (the grid is nw x XCDs)
   unsigned long long timeout;
+  int slab0;        // (L2 = false) first 16-column slab of this launch: slab0 + blockIdx.y
 };
 
 struct Q1LShared {
@@ -1213,17 +1224,23 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
 #if TG_Q1L_STATS
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  const int n = a.n, k = a.k, tid = threadIdx.x, lane = tid & 63;
+  const int W = a.nw, R0 = w * Q1R;
+  // (L2 = false) column slab slab0 + blockIdx.y: Z columns 16 slab .. (ld
+  // a.k), its own arrival counter and partials (the launch's blockIdx.y-th)
+  const int ys = L2 ? 0 : int(blockIdx.y), slab = L2 ? 0 : a.slab0 + ys, ld = a.k;
+  double *const Zb = a.Z + 16 * slab;
+  double *const part = a.part + size_t(ys) * 2 * W * 512;
+  unsigned *const cnt = a.cnt + 16 * slab;
+  const int n = a.n, k = min(16, a.k - 16 * slab), tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane >> 4, lc = lane & 15;
-  const int W = a.nw, R0 = w * Q1R;
   // the partials as a buffer: 16-byte sc1 loads of two entries
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-      a.part, 0, int(size_t(2) * W * 512 * sizeof(double)), 0x00020000);
+      part, 0, int(size_t(2) * W * 512 * sizeof(double)), 0x00020000);
   constexpr int SC1 = 16;  // cache policy bit of the L1-bypassing loads
   for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
     const int r = e >> 4, col = e & 15, row = R0 + r;
-    sm.Zs[r][col] = (row < n && col < k) ? a.Z[int64_t(row) * k + col] : 0.0;
+    sm.Zs[r][col] = (row < n && col < k) ? Zb[int64_t(row) * ld + col] : 0.0;
   }
   Q1LPre pre;
   if (a.nops > 0) q1l_fetch(a, a.ops[0], R0, pre);
@@ -1272,7 +1289,7 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
       __syncthreads();
       // the sub-chunk partial (blocks in order, as bt_few sums its waves'),
       // published to the one XCD's L2
-      double *mine = a.part + (size_t(o & 1) * W + w) * 512;
+      double *mine = part + (size_t(o & 1) * W + w) * 512;
       for (int e = tid; e < 512; e += 64 * Q1W) {
         const int r = e >> 4, cc = e & 15;
         double v = 0.0;
@@ -1292,8 +1309,8 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
     // after the drain, which would otherwise wait for them too)
     if (o + 1 < a.nops && R0 + Q1R > a.ops[o + 1].r0) q1l_fetch(a, a.ops[o + 1], R0, pre);
     if (wid == 0) {
-      tg::wave_arrive(a.cnt);
-      tg::spin_geq(a.cnt, unsigned(W) * unsigned(o + 1), a.stall, a.timeout);
+      tg::wave_arrive(cnt);
+      tg::spin_geq(cnt, unsigned(W) * unsigned(o + 1), a.stall, a.timeout);
     }
     __syncthreads();
     Q1L_T(t3)
@@ -1373,7 +1390,7 @@ __global__ __launch_bounds__(64 * Q1W) void q1_lds_kernel(Q1LArgs a) {
 #endif
   for (int e = tid; e < Q1R * 16; e += 64 * Q1W) {
     const int r = e >> 4, col = e & 15, row = R0 + r;
-    if (row < n && col < k) a.Z[int64_t(row) * k + col] = sm.Zs[r][col];
+    if (row < n && col < k) Zb[int64_t(row) * ld + col] = sm.Zs[r][col];
   }
 }
 
@@ -1383,32 +1400,66 @@ namespace tg {
 
 int sb_smax(int n);
 
-// ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + 128 bytes of
-// device scratch (32 control words: step counter, timeout flag, bt_few's XCD
-// election [2..4], q1_lds arrivals [5], bt_few stats [8..23], q1_lds's XCD
-// election [24..27]).
+// ops: host-built step list; dev: >= ops.size() * sizeof(Q1Op) + FEW_HDR
+// bytes of device scratch (control words: step counter, timeout flag, bt_few's
+// XCD election [2..4], q1_lds arrivals [5], bt_few stats [8..23], q1_lds's XCD
+// election [24..27], the column slabs' q1_lds arrivals [64 + 16 s]).
+constexpr int FEW_HDR = 1024;
+constexpr int FEW_SLABS = 8;  // 16-column slabs of the LDS-resident kernels: k <= 128
+static_assert(64 + 16 * FEW_SLABS <= FEW_HDR / 4, "slab counters fit the header");
 static size_t few_ops_bytes(const SbPlan &pl) {
   size_t c = 0;
   for (const SbPanel &P : pl.panels) c += size_t(P.nl);
-  return (128 + c * sizeof(Q1Op) + 255) & ~size_t(255);
+  return (FEW_HDR + c * sizeof(Q1Op) + 255) & ~size_t(255);
 }
 static int few_nsub(const SbPlan &pl) {  // + 1: sub-chunks are row-aligned, not panel-aligned
   return pl.single && !pl.panels.empty() ? cdiv(pl.panels[0].m, Q1S) + 1 : 0;
 }
-static size_t few_part_bytes(const SbPlan &pl, int n) {
+// Column slabs (k > 16: TG_BT_SLABS=0 keeps bt_few for k = 17 .. 32): both
+// LDS kernels take 16 columns a workgroup, slabs side by side in blockIdx.y,
+// as many a launch as leave every workgroup a CU of its own (their spins need
+// all resident); q1_lds's at most Q1_SLABS at once (partials per slab)
+constexpr int Q1_SLABS = 3;
+static int xcd_all_cus() {
+  const XcdInfo x = xcd_info();
+  return x.xcds * x.cus_per_xcd;
+}
+static bool few_slabs(int k) {
+  if (k <= 16) return false;
+  const char *e = getenv("TG_BT_SLABS");  // development switch, read per call
+  return !(e && e[0] == '0');
+}
+static int q1_conc(int n, int k) {
+  if (!few_slabs(k)) return 1;
+  return std::max(1, std::min({cdiv(k, 16), Q1_SLABS, xcd_all_cus() / std::max(1, cdiv(n, Q1R))}));
+}
+static size_t few_part_bytes(const SbPlan &pl, int n, int k) {
   if (!pl.single || pl.panels.empty()) return 0;
-  const size_t lds_form = size_t(2) * cdiv(n, Q1R) * 512 * sizeof(double);
+  const size_t lds_form = size_t(q1_conc(n, k)) * 2 * cdiv(n, Q1R) * 512 * sizeof(double);
   return std::max(size_t(few_nsub(pl)) * SB_B * SB_B * sizeof(double), lds_form);
 }
-// + one progress word per Q2 sweep group (n / 32 + 1), 16-byte padded
-size_t sb_apply_few_scratch(const SbPlan &pl, int n) {
-  return few_ops_bytes(pl) + few_part_bytes(pl, n) + ((size_t(n / QB + 1) * 4 + 15) & ~size_t(15));
+// + one progress word per Q2 sweep group (n / 32 + 1) and column slab, 16-byte padded
+size_t sb_apply_few_scratch(const SbPlan &pl, int n, int k) {
+  const size_t slabs = few_slabs(k) ? size_t(cdiv(k, 16)) : 1;
+  return few_ops_bytes(pl) + few_part_bytes(pl, n, k) +
+         ((size_t(n / QB + 1) * slabs * 4 + 15) & ~size_t(15));
+}
+// can sb_apply_few take k columns?  k <= 32 always (bt_few_kernel); up to 128
+// when the LDS-resident kernels fit (single-level plans, n / 128 workgroups <= CUs)
+bool sb_apply_few_ok(const SbPlan &pl, int n, int k) {
+  if (k < 1) return false;
+  if (k <= 32) return true;
+  const int cus = xcd_all_cus();
+  return few_slabs(k) && k <= 16 * FEW_SLABS && pl.single && n > 2 &&
+         cdiv(cdiv(n - 2, QB), QW) <= cus && cdiv(n, Q1R) <= cus;
 }
 
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                         const SbBufs &b, void *dev, bool *timed_out) {
   *timed_out = false;
-  if (k < 1 || k > 32) return hipErrorInvalidValue;
+  if (!sb_apply_few_ok(pl, n, k)) return hipErrorInvalidValue;
+  const bool slabs = few_slabs(k);
+  const int nslab = slabs ? cdiv(k, 16) : 1;
   std::vector<Q1Op> ops;
   for (auto it = pl.panels.rbegin(); it != pl.panels.rend(); ++it)
     for (int l = it->nl - 1; l >= 0; --l) {
@@ -1416,8 +1467,8 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       ops.push_back(Q1Op{it->r0, L.rows, L.nc, l, int(L.yoff), int(L.toff)});
     }
   unsigned *cnt = static_cast<unsigned *>(dev);
-  Q1Op *dops = reinterpret_cast<Q1Op *>(static_cast<char *>(dev) + 128);
-  hipError_t e = hipMemsetAsync(cnt, 0, 128, st);
+  Q1Op *dops = reinterpret_cast<Q1Op *>(static_cast<char *>(dev) + FEW_HDR);
+  hipError_t e = hipMemsetAsync(cnt, 0, FEW_HDR, st);
   if (e != hipSuccess) return e;
   if (!ops.empty()) {
     e = hipMemcpyAsync(dops, ops.data(), ops.size() * sizeof(Q1Op), hipMemcpyHostToDevice, st);
@@ -1442,7 +1493,7 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   a.cnt = cnt;
   a.timeout = spin_timeout_ticks("TG_BT_TIMEOUT_TICKS");
   a.colflag = reinterpret_cast<unsigned *>(static_cast<char *>(dev) + few_ops_bytes(pl) +
-                                           few_part_bytes(pl, n));
+                                           few_part_bytes(pl, n, k));
   {
     const char *qw = getenv("TG_BT_Q2_WAVE");  // development switch, read per call
     a.q2_wave = (qw && qw[0] == '1') ? 1 : 0;
@@ -1458,13 +1509,17 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
   {
     const char *ql = getenv("TG_BT_Q2_LDS");  // development switch, read per call
     const int Wq = cdiv(a.ng2, QW);
-    // (k <= 16: one 16-column block; with two, registers spill at the
-    // 256-VGPR cap of two waves per SIMD, so k = 17 .. 32 keeps bt_few's Q2)
-    if (!(ql && ql[0] == '0') && !a.q2_wave && a.nlev2 > 0 && k <= 16 &&
-        Wq <= xq.xcds * xq.cus_per_xcd) {
-      e = hipMemsetAsync(a.colflag, 0, ((size_t(a.ng2) * 4 + 15) & ~size_t(15)), st);
+    // (one 16-column block a workgroup: with two, registers spill at the
+    // 256-VGPR cap of two waves per SIMD; k > 16 in column slabs, or with
+    // TG_BT_SLABS=0 bt_few's Q2 for k = 17 .. 32)
+    const bool q2l = !(ql && ql[0] == '0') && !a.q2_wave && a.nlev2 > 0 && (k <= 16 || slabs) &&
+                     Wq <= xq.xcds * xq.cus_per_xcd;
+    if (!q2l && k > 32) return hipErrorInvalidValue;
+    if (q2l) {
+      e = hipMemsetAsync(a.colflag, 0, ((size_t(a.ng2) * nslab * 4 + 15) & ~size_t(15)), st);
       if (e != hipSuccess) return e;
-      Q2LArgs qa{Z, n, k, b.V2, b.T2, a.smax, a.ng2, a.colflag, cnt + 1, a.timeout};
+      Q2LArgs qa{Z, n, k, b.V2, b.T2, a.smax, a.ng2, a.colflag, cnt + 1, a.timeout, 0};
+      const int c2 = std::max(1, std::min(nslab, xq.xcds * xq.cus_per_xcd / Wq));
       auto tq = prof_begin(st, PROF_Q2, 0.0, 0.0);
 #if TG_Q2L_STATS
       {
@@ -1473,9 +1528,12 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
                                      hipMemcpyHostToDevice, st);
       }
 #endif
-      hipLaunchKernelGGL(q2_lds_kernel<1>, dim3(Wq), dim3(64 * QW), 0, st, qa);
+      for (qa.slab0 = 0; qa.slab0 < nslab; qa.slab0 += c2) {
+        hipLaunchKernelGGL(q2_lds_kernel<1>, dim3(Wq, std::min(c2, nslab - qa.slab0)), dim3(64 * QW),
+                           0, st, qa);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+      }
       prof_end(st, tq);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
 #if TG_Q2L_STATS
       {
         unsigned long long h[8];
@@ -1493,24 +1551,33 @@ hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &p
       // (n <= 4096: the workgroups of one XCD; larger n: one workgroup per CU
       // of the device, placement-independent hand-offs)
       const int W1 = cdiv(n, Q1R);
-      const bool q1l2 = W1 <= xq.cus_per_xcd;
-      if (!(q1l && q1l[0] == '0') && a.single && a.nops > 0 &&
-          (q1l2 || W1 <= xq.xcds * xq.cus_per_xcd)) {
-        // partials in bt_few's sub-chunk partial area; arrivals in cnt[5],
-        // the XCD election in cnt[24..27]
-        Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, cnt + 5, cnt + 24, cnt + 1, W1,
-                   a.timeout};
+      const bool q1l2 = W1 <= xq.cus_per_xcd && k <= 16;  // (column slabs: the other form)
+      const bool q1 = !(q1l && q1l[0] == '0') && a.single && a.nops > 0 &&
+                      (q1l2 || W1 <= xq.xcds * xq.cus_per_xcd);
+      if (!q1 && k > 32) return hipErrorInvalidValue;
+      if (q1) {
+        // partials in bt_few's sub-chunk partial area; arrivals in cnt[5]
+        // (column slabs: cnt[64 + 16 s]), the XCD election in cnt[24..27]
+        Q1LArgs la{Z, n, k, b.Y, b.T, dops, a.nops, a.part, q1l2 ? cnt + 5 : cnt + 64, cnt + 24,
+                   cnt + 1, W1, a.timeout, 0};
         auto t1 = prof_begin(st, PROF_Q1, 0.0, 0.0);
         // TG_BT_Q1_LDS=2 (tests): a grid of W1 only, spread over the XCDs, so
         // the election comes up short and the bt_few fallback runs
         if (q1l2) {
           const int g1 = (q1l && q1l[0] == '2') ? W1 : W1 * xq.xcds;
           hipLaunchKernelGGL(q1_lds_kernel<true>, dim3(g1), dim3(64 * Q1W), 0, st, la);
+          if ((e = hipGetLastError()) != hipSuccess) return e;
         } else {
-          hipLaunchKernelGGL(q1_lds_kernel<false>, dim3(W1), dim3(64 * Q1W), 0, st, la);
+          // slabs a launch: each its own arrival counter, partials reused by
+          // the next launch (stream order)
+          const int c1 = q1_conc(n, k);
+          for (la.slab0 = 0; la.slab0 < nslab; la.slab0 += c1) {
+            hipLaunchKernelGGL(q1_lds_kernel<false>, dim3(W1, std::min(c1, nslab - la.slab0)),
+                               dim3(64 * Q1W), 0, st, la);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+          }
         }
         prof_end(st, t1);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
         // did the workers land on one XCD?  (the sync is the one the
         // all-LDS path makes anyway to read the timeout flag)
         unsigned h[28];

@@ -152,10 +152,12 @@ hipError_t sb_q2_tfactors(hipStream_t st, int n, const double *V2, double *T2);
 // side stream of the band reduction: fork after the work queued on st, join back into st
 hipError_t side_fork(hipStream_t st, hipStream_t *side);
 hipError_t side_join(hipStream_t st);
-// Z (n x k row-major, k <= 32) <- Q1 Q2 Z in one persistent launch (backtr.hip);
-// T2 must hold the Q2 T factors; dev: sb_apply_few_scratch bytes of device
-// scratch.  Syncs the stream (reads the barrier timeout flag).
-size_t sb_apply_few_scratch(const SbPlan &pl, int n);
+// Z (n x k row-major) <- Q1 Q2 Z with Z resident on chip (backtr.hip): k <= 32,
+// or up to 128 in 16-column slabs when sb_apply_few_ok; T2 must hold the Q2 T
+// factors; dev: sb_apply_few_scratch bytes of device scratch.  Syncs the
+// stream (reads the barrier timeout flag).
+bool sb_apply_few_ok(const SbPlan &pl, int n, int k);
+size_t sb_apply_few_scratch(const SbPlan &pl, int n, int k);
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
                         const SbBufs &b, void *dev, bool *timed_out);
 // Z (n x k row-major) <- Q1 Z.

@@ -1723,8 +1723,8 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   // one-wave workgroups) and the cluster checks, joined before the apply
   const bool ts = two_stage(n);
   const bool multi = getenv("TG_BT_MULTI") != nullptr;  // read per call (tests set it)
-  const bool few = ts && k <= 32 && !multi &&
-                   tg::sb_apply_few_scratch(pl, n) <= sizeof(double) * size_t(n) * tg::SB_B;
+  const bool few = ts && !multi && tg::sb_apply_few_ok(pl, n, k) &&
+                   tg::sb_apply_few_scratch(pl, n, k) <= sizeof(double) * size_t(n) * tg::SB_B;
   const char *tfs = getenv("TG_BT_TF_SIDE");  // development switch: 0 = in order, per call
   const bool tf_side = few && !(tfs && tfs[0] == '0');
   if (tf_side) {

@@ -414,3 +414,46 @@ def test_xm_ksplit(n, monkeypatch):
     assert np.array_equal(values("3"), forced)
     assert np.abs(forced - ref).max() <= 1e-12 * nrm
     assert np.abs(got - values("1")).max() <= 1e-12 * nrm
+
+
+@pytest.mark.parametrize("n,count", [(4096, 40), (3000, 24), (2048, 128), (9000, 43), (4100, 70)])
+def test_few_slabs(n, count, monkeypatch):
+    """Few-vector back-transform in 16-column slabs (csrc/backtr.hip
+    sb_apply_few, k = 17 .. 128: q2_lds_kernel and q1_lds_kernel<false> with
+    the slabs side by side in blockIdx.y, as many a launch as leave every
+    workgroup a CU): the eigenpair bars of test_few_vectors, and every slab
+    equals a call for its columns alone bit for bit (inverse iteration is per
+    vector; each slab is the same arithmetic as a k <= 16 call).  Up to 32
+    columns, also bt_few_kernel's vectors (TG_BT_SLABS=0) to 1e-12.  n = 2048,
+    128: 8 slabs, Q1 in launches of 3; n = 9000, 43: a partial last slab,
+    71 workgroups a slab; n = 4100: a ragged last sub-chunk."""
+    from gptq_svd_amd import _lib as lib
+    H = _wishart(n, 53)
+    Hd = torch.from_numpy(H).to(DEV)
+    ws = lib.workspace(lib.lib.tg_eigh_workspace_size(n), torch.device(DEV))
+    A = Hd.clone()
+    w = torch.empty(n, dtype=torch.float64, device=DEV)
+    lib.call("tg_eigh_values", lib.stream(), lib.ptr(A), n, n, lib.ptr(w), lib.ptr(ws), ws.numel())
+    first = n - count
+
+    def vectors(f, c):
+        V = torch.empty((c, n), dtype=torch.float64, device=DEV)
+        lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), f, c, lib.ptr(V), n,
+                 lib.ptr(ws), ws.numel())
+        torch.cuda.synchronize()
+        return V.cpu().numpy()
+
+    Vh = vectors(first, count)
+    assert np.array_equal(vectors(first, count), Vh)
+    lam_desc = w.cpu().numpy()[::-1]
+    lam = lam_desc[first:]
+    nrm = np.abs(lam_desc).max()
+    resid = np.linalg.norm(Vh @ H - lam[:, None] * Vh, axis=1).max()
+    assert resid <= 1e-10 * nrm, resid
+    assert np.abs(Vh @ Vh.T - np.eye(count)).max() <= 1e-10
+    for s in range(0, count, 16):
+        c = min(16, count - s)
+        assert np.array_equal(vectors(first + s, c), Vh[s:s + c]), s
+    if count <= 32:
+        monkeypatch.setenv("TG_BT_SLABS", "0")
+        assert np.abs(vectors(first, count) - Vh).max() <= 1e-12
