@@ -1445,13 +1445,20 @@ size_t sb_apply_few_scratch(const SbPlan &pl, int n, int k) {
          ((size_t(n / QB + 1) * slabs * 4 + 15) & ~size_t(15));
 }
 // can sb_apply_few take k columns?  k <= 32 always (bt_few_kernel); up to 128
-// when the LDS-resident kernels fit (single-level plans, n / 128 workgroups <= CUs)
+// when the LDS-resident kernels fit (single-level plans, n / 128 workgroups <=
+// CUs) in at most 4 launches of the two: each launch is a chain of n / 32
+// dependent steps whatever its slabs, so past that the level-by-level
+// sb_apply_q2 / sb_apply_q1 are faster (measured: n = 28,672, k = 102 in 7 + 7
+// launches 201.7 ms against 109.5 ms; n = 4096, k = 100 in 1 + 3: 7.9 against
+// 11.1 ms; n = 14,336, k = 51 in 2 + 2: 29.4 against 39.9 ms)
 bool sb_apply_few_ok(const SbPlan &pl, int n, int k) {
   if (k < 1) return false;
   if (k <= 32) return true;
-  const int cus = xcd_all_cus();
-  return few_slabs(k) && k <= 16 * FEW_SLABS && pl.single && n > 2 &&
-         cdiv(cdiv(n - 2, QB), QW) <= cus && cdiv(n, Q1R) <= cus;
+  const int cus = xcd_all_cus(), wq = cdiv(cdiv(n - 2, QB), QW), w1 = cdiv(n, Q1R);
+  if (!few_slabs(k) || k > 16 * FEW_SLABS || !pl.single || n <= 2 || wq > cus || w1 > cus)
+    return false;
+  const int ns = cdiv(k, 16);
+  return cdiv(ns, cus / wq) + cdiv(ns, q1_conc(n, k)) <= 4;
 }
 
 hipError_t sb_apply_few(hipStream_t st, int n, double *Z, int k, const SbPlan &pl,
