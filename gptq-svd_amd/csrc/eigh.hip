@@ -1005,8 +1005,52 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 // in a per-vector slab of global memory (w.lu), the next chunk's rows
 // prefetched through each sweep so the chain still waits on no load.
 constexpr int IFCH = 16;
+// TG_INVIT_STATS (build-time): s_memrealtime stamps of vector 0's passes
+// (start, then per iteration: forward done, backward done, rescaled), printed
+// by the host after the launch
+#ifndef TG_INVIT_STATS
+#define TG_INVIT_STATS 0
+#endif
+#if TG_INVIT_STATS
+__device__ unsigned long long g_invit_stats[16];
+#define INVIT_T(slot)                                                              \
+  if (jj == 0 && lane == 0) g_invit_stats[slot] = __builtin_amdgcn_s_memrealtime();
+#else
+#define INVIT_T(slot)
+#endif
+// Two waves (128 threads; TG_INVIT_ONEWAVE builds: 64, the chain and the
+// factor rows on one wave): in a factoring pass wave 0 runs only the pivot
+// chain (cur_d, cur_u -> interchange, multiplier f) and hands each chunk's f,
+// pivot and cur_u to wave 1 through an LDS ring (workgroup acquire / release),
+// which forms the factor rows, the multipliers' copies and the forward
+// substitution from them with the same operations -- the chain no longer
+// issues them (measured per vector at n = 4096: the factoring pass was 580 us,
+// 340 cycles a step, for a dependent chain of ~10 operations).
+constexpr int IXS = 4;  // chunk slots of the ring
+// TG_INVIT_ONEWAVE=1 (build-time, A/B): the round-6 one-wave kernel (64
+// threads, the factoring pass on lane 0 alone); with both forms compiled in,
+// the kernel spills (the two waves' blocks and the one-wave step share its
+// register budget)
+#ifndef TG_INVIT_ONEWAVE
+#define TG_INVIT_ONEWAVE 0
+#endif
+struct InvitXch {
+  double2 fd[IXS][IFCH];  // (f, pivot) of each step
+  double2 cn[IXS][IFCH];  // (cur_u before the step, d - lambda of the next row)
+  double nu[IXS][IFCH];   // e of the next row (0 past the block)
+  unsigned msk[IXS];
+  unsigned pub, con;  // chunks published by wave 0 / consumed by wave 1
+};
+__device__ __forceinline__ void ixs_wait(const unsigned *p, unsigned v) {
+  // both waves are resident (one workgroup): the other always progresses
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
+    __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void ixs_put(unsigned *p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 template <bool GR>
-__global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict__ d,
+__global__ __launch_bounds__(128) void invit_lds_kernel(const double *__restrict__ d,
                                                        const double *__restrict__ e, int n, int k,
                                                        int first,
                                                        const double *__restrict__ w_asc,
@@ -1014,7 +1058,9 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
                                                        int refac,
                                                        Tri w) {
   extern __shared__ double2 lds_rows[];  // rows[2i] = {1/pivot, du}, rows[2i+1] = {du2, x}
-  const int jj = blockIdx.x, lane = threadIdx.x;
+  __shared__ InvitXch xc;
+  const int jj = blockIdx.x, lane = threadIdx.x;  // lane < 64: wave 0
+  const bool two = !TG_INVIT_ONEWAVE && blockDim.x > 64;
   double2 *rows = GR ? reinterpret_cast<double2 *>(w.lu + size_t(jj) * 4 * size_t(n)) : lds_rows;
   // after the LDS rows (or from the start): the interchange bits of each IFCH-step chunk
   unsigned *swm = reinterpret_cast<unsigned *>(lds_rows + (GR ? 0 : 2 * size_t(n)));
@@ -1026,12 +1072,14 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
   const size_t K = size_t(k);
   double *rw = reinterpret_cast<double *>(rows);
   auto X = [&](int i) -> double & { return rw[4 * i + 3]; };
-  for (int i = lane; i < n; i += 64)
-    if (i < b0 || i >= b1) w.Z[size_t(i) * K + jj] = 0.0;
+  if (lane < 64)
+    for (int i = lane; i < n; i += 64)
+      if (i < b0 || i >= b1) w.Z[size_t(i) * K + jj] = 0.0;
   d += b0;
   e += b0;
   double *fz = w.Z + jj;  // multiplier f of block row i at fz[(b0 + i) K] until the last write
-  for (int i = lane; i < m; i += 64) X(i) = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
+  if (lane < 64)
+    for (int i = lane; i < m; i += 64) X(i) = hash_unit(uint32_t(b0 + i), uint32_t(first + jj)) + 0.25;
   auto clampp = [&](double v) { return fabs(v) < tol ? (v < 0.0 ? -tol : tol) : v; };
   auto rcp2 = [](double b) {
     double r = __builtin_amdgcn_rcp(b);
@@ -1043,32 +1091,126 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
     const double v = e[max(min(i, m - 2), 0)];
     return i < m - 1 ? v : 0.0;
   };
+  // a zero the compiler cannot prove uniform: d and e then arrive by vector
+  // loads (vmcnt), not scalar ones, so waiting on the chain's LDS traffic
+  // (lgkmcnt) does not also wait on the prefetch.  Set afresh (opaque) in each
+  // block that fetches, so no block's addresses are hoisted out of the
+  // iteration loop and held across the others.
+  int vz = 0;
+  auto opaque_zero = [&]() { asm volatile("v_mov_b32 %0, 0" : "=v"(vz)); };
+  // chunk c covers steps i0..i0+IFCH-1: dn[u] = d[i0+u+1], en[u] = e[i0+u]
+  // (e[i0+u+1] is en[u+1], or the next chunk's en[0])
+  auto fetch = [&](int i0, double *a, double *b) {
+#pragma unroll
+    for (int u = 0; u < IFCH; ++u) {
+      const int i = i0 + u + vz;
+      a[u] = d[min(i + 1, m - 1)];
+      b[u] = eat(i);
+    }
+  };
+  // x of the rows after steps i0 .. i0 + IFCH - 1
+  auto xload = [&](int i0, double *a) {
+#pragma unroll
+    for (int u = 0; u < IFCH; ++u) a[u] = X(min(i0 + u + 1 + vz, m - 1));
+  };
   __syncthreads();
+  INVIT_T(0)
   for (int it = 0; it < iters; ++it) {
     double amax = 0.0;
-    if (lane == 0) {
-      double cur_d = d[0] - lam, cur_u = eat(0), xi = X(0);
-      // chunk c covers steps i0..i0+IFCH-1: dn[u] = d[i0+u+1], en[u] = e[i0+u]
-      // (e[i0+u+1] is en[u+1], or the next chunk's en[0])
-      double dn[IFCH], en[IFCH], pd[IFCH], pe[IFCH];
-      // a zero the compiler cannot prove uniform: d and e then arrive by vector
-      // loads (vmcnt), not scalar ones, so waiting on the chain's LDS traffic
-      // (lgkmcnt) does not also wait on the prefetch
-      int vz;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-      auto fetch = [&](int i0, double *a, double *b) {
+    const bool fac2 = two && (it == 0 || refac);
+    if (fac2) {
+      if (lane == 0) {
+        xc.pub = 0u;
+        xc.con = 0u;
+      }
+      __syncthreads();
+      if (lane == 0) {
+        // wave 0: the pivot chain; each step's f, pivot, cur_u and inputs go
+        // straight to the ring slot (no wait: wave 1 reads them a chunk later)
+        opaque_zero();
+        double cur_d = d[0] - lam, cur_u = eat(0);
+        double dn[IFCH], en[IFCH], pd[IFCH], pe[IFCH];
+        fetch(0, dn, en);
+        for (int c = 0, i0 = 0; i0 < m - 1; ++c, i0 += IFCH) {
+          const int cnt = min(IFCH, m - 1 - i0);
+          fetch(i0 + IFCH, pd, pe);
+          const int sl = c % IXS;
+          if (c >= IXS) ixs_wait(&xc.con, unsigned(c - IXS + 1));
+          unsigned msk = 0;
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) {
-          const int i = i0 + u + vz;
-          a[u] = d[min(i + 1, m - 1)];
-          b[u] = eat(i);
+          for (int u = 0; u < IFCH; ++u)
+            if (cnt == IFCH || u < cnt) {
+              const double sub = en[u], nd = dn[u] - lam;
+              const double nu = cnt == IFCH ? (u + 1 < IFCH ? en[u + 1] : pe[0]) : eat(i0 + u + 1);
+              const uint64_t sw = __builtin_amdgcn_fcmp(fabs(cur_d), fabs(sub), 12);  // ULT
+              const uint64_t tiny = __builtin_amdgcn_fcmp(fabs(cur_d), tol, 4);       // OLT
+              const double den = vsel(sw, sub, vsel(tiny, copysign(tol, cur_d), cur_d));
+              const double num = vsel(sw, cur_d, sub);
+              const double r0 = __builtin_amdgcn_rcp(den);
+              const double q0 = num * r0, ee = fma(-den, r0, 1.0);
+              const double res = fma(-den, q0, num), r1 = fma(r0, ee, r0);
+              const double f = fma(r1, res, q0);
+              const double C = vsel(sw, cur_u, nd), D = vsel(sw, nd, cur_u);
+              xc.fd[sl][u] = make_double2(f, den);
+              xc.cn[sl][u] = make_double2(cur_u, nd);
+              xc.nu[sl][u] = nu;
+              cur_d = C - f * D;
+              cur_u = vsel(sw, -f * nu, nu);
+              msk |= unsigned(sw & 1u) << u;
+            }
+          xc.msk[sl] = msk;
+          ixs_put(&xc.pub, unsigned(c + 1));
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) {
+            dn[u] = pd[u];
+            en[u] = pe[u];
+          }
         }
-      };
-      // x of the rows after steps i0 .. i0 + IFCH - 1
-      auto xload = [&](int i0, double *a) {
+        rows[2 * (m - 1)] = make_double2(rcp2(clampp(cur_d)), 0.0);
+      } else if (lane == 64) {
+        // wave 1: the factor rows, the multipliers' copies (Z's column) and the
+        // forward substitution, chunk by chunk behind the chain -- the
+        // operations of the one-wave step, on the chain's values
+        opaque_zero();
+        double xi = X(0);
+        double xn[IFCH], xp[IFCH];
+        xload(0, xn);
+        for (int c = 0, i0 = 0; i0 < m - 1; ++c, i0 += IFCH) {
+          const int cnt = min(IFCH, m - 1 - i0);
+          xload(i0 + IFCH, xp);  // (rows this chunk does not write)
+          const int sl = c % IXS;
+          ixs_wait(&xc.pub, unsigned(c + 1));
+          const unsigned msk = xc.msk[sl];
 #pragma unroll
-        for (int u = 0; u < IFCH; ++u) a[u] = X(min(i0 + u + 1 + vz, m - 1));
-      };
+          for (int u = 0; u < IFCH; ++u)
+            if (cnt == IFCH || u < cnt) {
+              const double2 fd = xc.fd[sl][u], cn = xc.cn[sl][u];
+              const double nu = xc.nu[sl][u];
+              const uint64_t sw = ((msk >> u) & 1u) ? ~0ull : 0ull;
+              const double f = fd.x, den = fd.y;
+              const double r0 = __builtin_amdgcn_rcp(den);
+              const double ee = fma(-den, r0, 1.0), r1 = fma(r0, ee, r0);
+              const double A = vsel(sw, xi, xn[u]), B = vsel(sw, xn[u], xi);
+              const double D = vsel(sw, cn.y, cn.x);
+              rows[2 * (i0 + u)] = make_double2(fma(fma(-den, r1, 1.0), r1, r1), D);
+              rows[2 * (i0 + u) + 1] = make_double2(vsel(sw, nu, 0.0), B);
+              if (iters > 1) fz[size_t(b0 + i0 + u) * K] = f;
+              xi = fma(-f, B, A);
+            }
+          ixs_put(&xc.con, unsigned(c + 1));
+          swm[c] = msk;
+#pragma unroll
+          for (int u = 0; u < IFCH; ++u) xn[u] = xp[u];
+        }
+        rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the f (and GR: row) stores
+      }
+      __syncthreads();
+    }
+    if (lane == 0) {
+      opaque_zero();
+      double cur_d = d[0] - lam, cur_u = eat(0), xi = X(0);
+      double dn[IFCH], en[IFCH], pd[IFCH], pe[IFCH];
       // one dgttrf step + forward substitution, branch-free.  Row interchange
       // when !(|cur_d| >= |sub|); lane masks + v_cndmask keep the compiler from
       // turning the selects into exec-mask branches.  a / b = q0 + r1 (a - b q0)
@@ -1094,7 +1236,9 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
         fo = f;
         swb = unsigned(sw & 1u);  // lane 0's interchange
       };
-      if (it == 0 || refac) {
+      if (fac2) {
+        // (the two waves factored and substituted above)
+      } else if (TG_INVIT_ONEWAVE && (it == 0 || refac)) {
         // factor + forward substitution; the multipliers f go to Z's column
         // (free until the final write) and the interchanges to LDS bit masks,
         // so later iterations only substitute (the factors do not change)
@@ -1192,7 +1336,8 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
           }
         }
       }
-      rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
+      if (!fac2) rows[2 * (m - 1) + 1] = make_double2(0.0, xi);
+      INVIT_T(1 + 3 * it)
       // backward substitution with U (du of row m-1 and du2 of rows m-2, m-1 are 0)
       double xn1 = 0.0, xn2 = 0.0;
       auto bstep = [&](double2 r0, double2 r1) {
@@ -1233,22 +1378,26 @@ __global__ __launch_bounds__(64) void invit_lds_kernel(const double *__restrict_
         }
       }
     }
+    INVIT_T(2 + 3 * it)
     __syncthreads();
-    amax = __shfl(amax, 0);
-    const double sc = amax > 0.0 ? 1.0 / amax : 1.0;
-    double nrm = 0.0;
-    for (int i = lane; i < m; i += 64) {
-      const double v = X(i) * sc;
-      nrm += v * v;
-      X(i) = v;
-    }
-    if (it == iters - 1) {
+    if (lane < 64) {  // wave 0 rescales
+      amax = __shfl(amax, 0);
+      const double sc = amax > 0.0 ? 1.0 / amax : 1.0;
+      double nrm = 0.0;
+      for (int i = lane; i < m; i += 64) {
+        const double v = X(i) * sc;
+        nrm += v * v;
+        X(i) = v;
+      }
+      if (it == iters - 1) {
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o);
-      const double inv = 1.0 / sqrt(nrm);
-      for (int i = lane; i < m; i += 64) w.Z[size_t(b0 + i) * K + jj] = X(i) * inv;
+        for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o);
+        const double inv = 1.0 / sqrt(nrm);
+        for (int i = lane; i < m; i += 64) w.Z[size_t(b0 + i) * K + jj] = X(i) * inv;
+      }
     }
     __syncthreads();
+    INVIT_T(3 + 3 * it)
   }
 }
 
@@ -1744,16 +1893,17 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   const int refac = (rf && rf[0] == '1') ? 1 : 0;
   // (n > 5120: the rows in a per-vector slab of w.lu, 4 n k <= 3 n^2 doubles)
   const char *ig = getenv("TG_INVIT_GROWS");  // development switch: 1 = global rows at any n
-  const bool grows = ilds > 160 * 1024 || (ig && ig[0] == '1');
+  const bool grows = ilds + sizeof(InvitXch) > 160 * 1024 || (ig && ig[0] == '1');
+  const int ith = TG_INVIT_ONEWAVE ? 64 : 128;
   const char *ir = getenv("TG_INVIT_REG");  // development switch: 1 = the register kernel
   if (k <= 256 && !(ir && ir[0] == '1')) {
     if (grows) {
-      hipLaunchKernelGGL(invit_lds_kernel<true>, dim3(k), dim3(64), imask, st, w.d, w.es, n, k,
+      hipLaunchKernelGGL(invit_lds_kernel<true>, dim3(k), dim3(ith), imask, st, w.d, w.es, n, k,
                          first, w_asc, bnd, iters, refac, w);
     } else {
       TG_HIP(hipFuncSetAttribute((const void *)invit_lds_kernel<false>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(ilds)));
-      hipLaunchKernelGGL(invit_lds_kernel<false>, dim3(k), dim3(64), ilds, st, w.d, w.es, n, k,
+      hipLaunchKernelGGL(invit_lds_kernel<false>, dim3(k), dim3(ith), ilds, st, w.d, w.es, n, k,
                          first, w_asc, bnd, iters, refac, w);
     }
   } else {
@@ -1762,6 +1912,16 @@ extern "C" int tg_eigh_vectors_range(void *stream, int n, const double *w_asc, i
   }
   tg::prof_end(st, itok);
   TG_LAUNCHED();
+#if TG_INVIT_STATS
+  {
+    unsigned long long h[16];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_invit_stats), sizeof(h));
+    fprintf(stderr, "invit n=%d k=%d (vector 0, us):", n, k);
+    for (int q = 1; q <= 3 * iters; ++q) fprintf(stderr, " %.1f", (h[q] - h[q - 1]) / 100.0);
+    fprintf(stderr, "\n");
+  }
+#endif
   {
     const char *ot = getenv("TG_INVIT_ORTOL");
     const double ortol = ot ? atof(ot) : 1e-6;

@@ -3,7 +3,10 @@ path's request) under environment variants, interleaved rep by rep in one
 process (development tool):
     N=4096,12288 K=16,24,43 REPS=6 python tools/few_time.py TG_BT_SLABS=1 TG_BT_SLABS=0 TG_BT_MULTI=1
 Prints the median and min ms per (n, k, variant) and the largest difference
-of each variant's vectors from the first variant's."""
+of each variant's vectors from the first variant's.  FIRST=f: eigenpairs
+f .. f + k - 1 (descending) instead of the last k (FIRST=3058 at n = 4096 is
+the bench's complement request: the smallest nonzero eigenvalues of the
+rank-3072 H)."""
 import os
 import statistics
 import sys
@@ -35,6 +38,7 @@ def main(variants):
         torch.cuda.synchronize()
         for k in [int(x) for x in os.environ.get("K", "16").split(",")]:
             V = torch.empty((k, n), dtype=torch.float64, device=dev)
+            first = int(os.environ["FIRST"]) if "FIRST" in os.environ else n - k
             times = {v: [] for v in variants}
             outs = {}
             for r in range(reps + 1):
@@ -46,7 +50,7 @@ def main(variants):
                         os.environ[key] = val
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                    lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), n - k, k,
+                    lib.call("tg_eigh_vectors_range", lib.stream(), n, lib.ptr(w), first, k,
                              lib.ptr(V), n, lib.ptr(ws), ws.numel())
                     torch.cuda.synchronize()
                     if r:
