@@ -1458,18 +1458,24 @@ constexpr int NU = 64;
 // U[i][l] X[l][:] from its rows i < l (U's diagonal held apart as 1/U_ll, so
 // the stored column has zeros at i >= l).  Broadcast rows double-buffered:
 // one barrier per step.
-template <int NWV>
-__global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restrict__ U, int ldu,
-                                                                int p, int pb,
-                                                                double *__restrict__ Wout,
-                                                                int *__restrict__ info) {
+struct PotrfSm {
+  double rowb[2][NU];
+  double ut[NU][NU + 2];  // ut[l][i] = U[i][l] for i < l (0 elsewhere); then W = U11^-T
+  double rinv[NU];
+};
+// The factor and the inverse of one diagonal block by the four waves of the
+// calling workgroup (the steps described above): U11 ends in a[] (row RW g +
+// q, column c, upper), W = U11^-T in sm.ut (ut[r][c] = W[r][c], lower), and
+// the return value says a pivot of the block's pb rows was not positive.
+// INV = false: the factor only (sm.ut then holds U's strict upper part).
+// (Two pivots per barrier -- every thread forming the second pivot's row
+// from the first's with the owner's fma, bit-identical -- measured no
+// faster: the pivots' rsq / Newton chain, not the barriers, sets the pace.)
+template <int NWV, bool INV>
+__device__ __forceinline__ bool potrf_inv_block(const double *__restrict__ base, int ldu, int pb,
+                                                PotrfSm &sm, double (&a)[NU / NWV]) {
   constexpr int RW = NU / NWV;  // rows per wave
-  __shared__ double rowb[2][NU];
-  __shared__ double ut[NU][NU + 2];  // ut[l][i] = U[i][l] for i < l (0 elsewhere); then W staging
-  __shared__ double rinv[NU];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  double a[RW];
-  double *base = U + size_t(p) * ldu + p;
   {
     const int cc = min(c, pb - 1);
 #pragma unroll
@@ -1483,12 +1489,12 @@ __global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restri
 #pragma unroll
   for (int j = 0; j < NU; ++j) {
     const int gj = j / RW, qj = j % RW;
-    if (g == gj) rowb[j & 1][c] = c >= j ? a[qj] : 0.0;
+    if (g == gj) sm.rowb[j & 1][c] = c >= j ? a[qj] : 0.0;
     __syncthreads();
-    const double d = rowb[j & 1][j];
-    const double vc = rowb[j & 1][c];
+    const double d = sm.rowb[j & 1][j];
+    const double vc = sm.rowb[j & 1][c];
     double rv[RW];
-    const double2 *r2 = reinterpret_cast<const double2 *>(&rowb[j & 1][RW * g]);
+    const double2 *r2 = reinterpret_cast<const double2 *>(&sm.rowb[j & 1][RW * g]);
 #pragma unroll
     for (int q = 0; q < RW / 2; ++q) {
       const double2 t = r2[q];
@@ -1509,10 +1515,59 @@ __global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restri
     for (int q = 0; q < RW; ++q) a[q] = fma(-rv[q], f, a[q]);  // rows <= j: rv = 0 or reset below
     if (g == gj) {
       a[qj] = c > j ? ujc : (c == j ? piv : 0.0);
-      ut[c][j] = c > j ? ujc : 0.0;  // column c of U at row j (diagonal apart)
+      sm.ut[c][j] = c > j ? ujc : 0.0;  // column c of U at row j (diagonal apart)
     }
-    if (c == j && g == 0) rinv[j] = inv;
+    if (c == j && g == 0) sm.rinv[j] = inv;
   }
+  if constexpr (INV) {
+    // X = U^-1: s = I, then for l = 63 .. 0: X[l] = s[l] / U_ll (owner), s[i] -= U[i][l] X[l]
+    double x[RW];
+#pragma unroll
+    for (int q = 0; q < RW; ++q) x[q] = (RW * g + q == c) ? 1.0 : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int l = NU - 1; l >= 0; --l) {
+      const int gl = l / RW, ql = l % RW;
+      if (g == gl) {
+        x[ql] *= sm.rinv[l];
+        sm.rowb[l & 1][c] = x[ql];
+      }
+      __syncthreads();
+      const double xl = sm.rowb[l & 1][c];
+      double uv[RW];
+      const double2 *u2 = reinterpret_cast<const double2 *>(&sm.ut[l][RW * g]);
+#pragma unroll
+      for (int q = 0; q < RW / 2; ++q) {
+        const double2 t = u2[q];
+        uv[2 * q] = t.x;
+        uv[2 * q + 1] = t.y;
+      }
+#pragma unroll
+      for (int q = 0; q < RW; ++q) x[q] = fma(-uv[q], xl, x[q]);  // U[i][l] = 0 for i >= l
+    }
+    __syncthreads();  // ut is reused as the W buffer
+    // W = X^T (lower): ut[c][r] = X[r][c]
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int r = RW * g + q;
+      sm.ut[c][r] = (r < pb && c < pb) ? x[q] : 0.0;
+    }
+    __syncthreads();
+  }
+  return bad;
+}
+
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restrict__ U, int ldu,
+                                                                int p, int pb,
+                                                                double *__restrict__ Wout,
+                                                                int *__restrict__ info) {
+  constexpr int RW = NU / NWV;
+  __shared__ PotrfSm sm;
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  double a[RW];
+  double *base = U + size_t(p) * ldu + p;
+  const bool bad = potrf_inv_block<NWV, true>(base, ldu, pb, sm, a);
   if (threadIdx.x == 0 && bad) atomicAdd(info, 1);
   // U block (upper) back in place
 #pragma unroll
@@ -1520,42 +1575,81 @@ __global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restri
     const int r = RW * g + q;
     if (r < pb && c < pb) base[size_t(r) * ldu + c] = c >= r ? a[q] : 0.0;
   }
-  // X = U^-1: s = I, then for l = 63 .. 0: X[l] = s[l] / U_ll (owner), s[i] -= U[i][l] X[l]
-#pragma unroll
-  for (int q = 0; q < RW; ++q) a[q] = (RW * g + q == c) ? 1.0 : 0.0;
-  __syncthreads();
-#pragma unroll
-  for (int l = NU - 1; l >= 0; --l) {
-    const int gl = l / RW, ql = l % RW;
-    if (g == gl) {
-      a[ql] *= rinv[l];
-      rowb[l & 1][c] = a[ql];
-    }
-    __syncthreads();
-    const double xl = rowb[l & 1][c];
-    double uv[RW];
-    const double2 *u2 = reinterpret_cast<const double2 *>(&ut[l][RW * g]);
-#pragma unroll
-    for (int q = 0; q < RW / 2; ++q) {
-      const double2 t = u2[q];
-      uv[2 * q] = t.x;
-      uv[2 * q + 1] = t.y;
-    }
-#pragma unroll
-    for (int q = 0; q < RW; ++q) a[q] = fma(-uv[q], xl, a[q]);  // U[i][l] = 0 for i >= l
-  }
-  __syncthreads();  // ut is reused as the W staging buffer
-  // W = X^T (lower) through LDS for coalesced rows: wt[c][r] = X[r][c]
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
     const int r = RW * g + q;
-    ut[c][r] = (r < pb && c < pb) ? a[q] : 0.0;
+    Wout[r * NU + c] = sm.ut[r][c];
+  }
+}
+
+// Fused panel step of chol_upper_rows (TG_CHOL_FUSED, the default): workgroup
+// t factors the panel's diagonal block itself (every workgroup the same
+// operations on the same block, so the same U11 and W in each) and forms its
+// 64-column tile of the panel rows, P = W G12[:, tile], on FP64 MFMA, in
+// place -- one launch where the potrf kernel, a GEMM launch and the gap
+// between them were.  U11 is NOT written here (another workgroup may still
+// be reading the block): chol_diag_kernel factors every panel's block again
+// at the end (the blocks stay as they were factored: no later step of the
+// factorisation writes them) and writes U11 and the pivot count.
+__global__ __launch_bounds__(256) void chol_panel_kernel(double *__restrict__ U, int ldu, int p,
+                                                         int pb, int c0, int n) {
+  constexpr int RW = NU / 4;
+  __shared__ PotrfSm sm;
+  __shared__ double gs[NU][NU + 1];  // the tile of G12 (row l, column j)
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6, lr = lane >> 4, lc = lane & 15;
+  const int col0 = c0 + NU * int(blockIdx.x);
+  // the tile first (its loads in flight through the factorisation)
+  double tv[NU * NU / 256];
+#pragma unroll
+  for (int u = 0; u < NU * NU / 256; ++u) {
+    const int e = tid + 256 * u, r = e >> 6, cc = e & 63;
+    tv[u] = U[size_t(p + min(r, pb - 1)) * ldu + min(col0 + cc, n - 1)];
+  }
+  double a[RW];
+  (void)potrf_inv_block<4, true>(U + size_t(p) * ldu + p, ldu, pb, sm, a);
+#pragma unroll
+  for (int u = 0; u < NU * NU / 256; ++u) {
+    const int e = tid + 256 * u, r = e >> 6, cc = e & 63;
+    gs[r][cc] = (r < pb) ? tv[u] : 0.0;
   }
   __syncthreads();
+  // wave g: rows 16 g .. 16 g + 15 of P, four 16-column blocks, K = 64
+  doublex4 acc[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < NU; k0 += 4) {
+    const double av = sm.ut[16 * g + lc][k0 + lr];  // W[row][k]
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, gs[k0 + lr][16 * cb + lc], acc[cb], 0, 0, 0);
+  }
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * g + lr + 4 * q, cc = col0 + 16 * cb + lc;
+      if (r < pb && cc < n) U[size_t(p + r) * ldu + cc] = acc[cb][q];
+    }
+}
+
+// U11 of every panel of chol_upper_rows' fused form (one workgroup each, the
+// panels' blocks as they were factored) and the count of non-positive pivots.
+__global__ __launch_bounds__(256) void chol_diag_kernel(double *__restrict__ U, int ldu, int k,
+                                                        int *__restrict__ info) {
+  constexpr int RW = NU / 4;
+  __shared__ PotrfSm sm;
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int p = NU * int(blockIdx.x), pb = min(NU, k - p);
+  double a[RW];
+  double *base = U + size_t(p) * ldu + p;
+  const bool bad = potrf_inv_block<4, false>(base, ldu, pb, sm, a);
+  if (threadIdx.x == 0 && bad) atomicAdd(info, 1);
+  __syncthreads();  // every wave's reads of the block are done
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
     const int r = RW * g + q;
-    Wout[r * NU + c] = ut[r][c];
+    if (r < pb && c < pb) base[size_t(r) * ldu + c] = c >= r ? a[q] : 0.0;
   }
 }
 
@@ -1617,20 +1711,31 @@ hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, dou
                            int *info) {
   // (a depth-1 look-ahead on a side stream measured +0.4 ms: the event
   // waits cost more than the overlap; removed)
+  // TG_CHOL_FUSED=0: the potrf kernel and a GEMM launch per panel (the
+  // panel's U11 written at once) instead of chol_panel_kernel + chol_diag_kernel
+  const char *cf = getenv("TG_CHOL_FUSED");  // development switch, read per call
+  const bool fused = !(cf && cf[0] == '0');
   for (int s0 = 0; s0 < k; s0 += CS) {
     const int se = std::min(k, s0 + CS);
     for (int p = s0; p < se; p += NU) {
       const int pb = std::min(NU, se - p);
-      launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
       const int c0 = p + pb;
-      if (c0 < n) {
-        // in place: one 64-row tile covers the panel's rows, so each workgroup
-        // reads its columns of G12 fully before writing them
-        double *P = U + size_t(p) * ldu + c0;
-        e = tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
-        if (e != hipSuccess) return e;
+      hipError_t e = hipSuccess;
+      if (fused) {
+        if (c0 < n)
+          hipLaunchKernelGGL(chol_panel_kernel, dim3(tg::cdiv(n - c0, NU)), dim3(256), 0, st, U, ldu,
+                             p, pb, c0, n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+      } else {
+        launch_potrf_inv(st, U, ldu, p, pb, Wb, info);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (c0 < n) {
+          // in place: one 64-row tile covers the panel's rows, so each workgroup
+          // reads its columns of G12 fully before writing them
+          double *P = U + size_t(p) * ldu + c0;
+          e = tg::dgemm(st, false, false, pb, n - c0, pb, 1.0, Wb, NU, P, ldu, 0.0, P, ldu);
+          if (e != hipSuccess) return e;
+        }
       }
       if (c0 < se) {  // the rest of the strip
         const double *P = U + size_t(p) * ldu + c0;
@@ -1648,6 +1753,10 @@ hipError_t chol_upper_rows(hipStream_t st, double *U, int ldu, int k, int n, dou
                              U + size_t(se) * ldu + se, ldu);
       if (e != hipSuccess) return e;
     }
+  }
+  if (fused && k > 0) {
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(tg::cdiv(k, NU)), dim3(256), 0, st, U, ldu, k, info);
+    return hipGetLastError();
   }
   return hipSuccess;
 }

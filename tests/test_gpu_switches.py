@@ -71,6 +71,7 @@ def rel(a, b):
     {"TG_BT_Q1_LDS": "0"},
     {"TG_BT_TF_SIDE": "0"},
     {"TG_BT_SLABS": "0"},
+    {"TG_CHOL_FUSED": "0"},
     {"TG_BISECT_NOGRID": "1"},
     {"TG_BISECT_CHUNK": "1"},
     {"TG_ORTH_MGS": "1"},
