@@ -159,6 +159,7 @@ struct BlockArgs {
   int m, bw;
   float minq, maxq;
   int code_off;
+  int dbl;  // two diagonal corr buffers (block_smem(bw, true)): the grid has <= 1 workgroup per CU
 };
 
 template <bool GATHER>
@@ -184,7 +185,8 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
   const int bwp = a.bw + 1;             // odd row stride: lane-per-row access is conflict-free
   float *Wb = smem;                      // [RW][bwp]
   float *el = Wb + RW * bwp;             // [2][RW][P+1] panel errors, parity by panel
-  float *cp = el + 2 * RW * (P + 1);     // [P][P]   corr panel
+  float *cpb = el + 2 * RW * (P + 1);    // [1 + dbl][P][P] corr diagonal panel block(s)
+  float *cq = cpb + (a.dbl ? 2 : 1) * P * P;  // [P][P] corr[p0 + cc][p0 + P + j]: the next panel's columns
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * RW;
 
@@ -193,50 +195,70 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
     const int row = r0 + rr;
     Wb[rr * bwp + c] = row < a.m ? a.W[size_t(row) * a.ldw + c] : 0.0f;
   }
-  auto load_cp = [&](int q0) {
-    const int qw = min(P, a.bw - q0);
-    for (int idx = tid; idx < P * P; idx += blockDim.x) {
-      const int cc = idx / P, j = idx % P;
-      cp[idx] = (cc < qw && j < qw) ? a.corr[size_t(q0 + cc) * a.ldcorr + q0 + j] : 0.0f;
+  // corr[q0 + cc][c0 + j] (cc, j < P, zero outside the block) of 1024 entries:
+  // this thread's share of them (threads t0, t0 + nt, ...) into registers
+  constexpr int NS = (P * P + 191) / 192;
+  auto corr_fetch = [&](int q0, int c0, int t0, int nt, float (&v)[NS]) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int idx = t0 + nt * u, cc = idx / P, j = idx % P;
+      const bool ok = idx < P * P && q0 + cc < a.bw && c0 + j < a.bw;
+      v[u] = ok ? a.corr[size_t(q0 + cc) * a.ldcorr + c0 + j] : 0.0f;
     }
   };
-  // rows rr0, rr0 + rstep, ... of column j get panel q0's errors e, in order
-  auto apply_col = [&](const float *e, int q0, int j, int rr0, int rstep) {
-    float cv[P];
+  auto corr_store = [&](float *dst, int t0, int nt, const float (&v)[NS]) {
 #pragma unroll
-    for (int cc = 0; cc < P; ++cc) cv[cc] = a.corr[size_t(q0 + cc) * a.ldcorr + j];
-#pragma unroll 2
-    for (int rr = rr0; rr < RW; rr += rstep) {
-      float w = Wb[rr * bwp + j];
-#pragma unroll
-      for (int cc = 0; cc < P; ++cc) {
-        const float d = e[rr * (P + 1) + cc] * cv[cc];
-        w = w - d;
-      }
-      Wb[rr * bwp + j] = w;
+    for (int u = 0; u < NS; ++u) {
+      const int idx = t0 + nt * u;
+      if (idx < P * P) dst[idx] = v[u];
     }
   };
-  load_cp(0);
+  {
+    float v[NS];
+    for (int t0 = tid; t0 < 192; t0 += blockDim.x) {  // (threads < 192)
+      corr_fetch(0, 0, t0, 192, v);
+      corr_store(cpb, t0, 192, v);
+    }
+  }
+  // the chain's scales / zeros of a panel (lane rr < RW of wave 0)
+  auto sz_fetch = [&](int p0, float (&sv)[P], float (&zv)[P]) {
+    const int rr = tid, row = r0 + rr, pw = min(P, a.bw - p0);
+#pragma unroll
+    for (int t = 0; t < P; ++t) {
+      if (t < pw) load_sz<GATHER>(a, row, p0 + t, sv[t], zv[t]);
+      else { sv[t] = 1.0f; zv[t] = 0.0f; }
+    }
+  };
+  float sv[P], zv[P];
+  if (tid < RW) sz_fetch(0, sv, zv);
   __syncthreads();
 
-  // Look-ahead: while wave 0 runs panel p's column chain, waves 1-3 apply
-  // panel p-1's errors to the columns after panel p; then all threads apply
-  // panel p's errors to panel p+1's columns.  Every element still receives
-  // the panels' updates in panel order, cc ascending within a panel, so the
-  // result is the same bit for bit.
+  // Per panel p: wave 0 runs panel p's column chain (one lane per row);
+  // waves 1-3 fetch the corr blocks the next steps need (the off-diagonal
+  // block for the update of panel p+1's columns, into LDS before the barrier;
+  // the next diagonal block for panel p+1's chain, into LDS after it, once
+  // the chain is done with cp -- one buffer each keeps two workgroups per CU
+  // at bw = 1024, the occupancy the 12,288-row layers need; with at most one
+  // workgroup per CU anyway, dbl: two diagonal buffers by panel parity, the
+  // next one stored before the barrier) and apply panel p-1's errors to the
+  // columns after panel p, each thread's next column's corr loads in flight
+  // while it updates the current one; then all threads apply panel p's errors
+  // to panel p+1's columns from LDS.  Every element still receives the
+  // panels' updates in panel order, cc ascending within a panel, each as the
+  // separately rounded mul and sub: the result is the same bit for bit.
   for (int p0 = 0, it = 0; p0 < a.bw; p0 += P, ++it) {
     const int pw = min(P, a.bw - p0);
     float *elc = el + (it & 1) * RW * (P + 1);
     const float *elp = el + ((it + 1) & 1) * RW * (P + 1);
+    const bool more = p0 + pw < a.bw;  // uniform
+    const float *cp = cpb + (a.dbl ? (it & 1) * P * P : 0);
+    float *cpn = cpb + (a.dbl ? ((it + 1) & 1) * P * P : 0);  // panel p+1's
+    float vp[NS];  // waves 1-3: their share of panel p+1's diagonal corr block
     if (tid < RW) {  // sequential column chain: one lane per row
       const int rr = tid, row = r0 + rr;
-      float wv[P], sv[P], zv[P];
+      float wv[P];
 #pragma unroll
-      for (int t = 0; t < P; ++t) {
-        wv[t] = t < pw ? Wb[rr * bwp + p0 + t] : 0.0f;
-        if (t < pw) load_sz<GATHER>(a, row, p0 + t, sv[t], zv[t]);
-        else { sv[t] = 1.0f; zv[t] = 0.0f; }
-      }
+      for (int t = 0; t < P; ++t) wv[t] = t < pw ? Wb[rr * bwp + p0 + t] : 0.0f;
 #pragma unroll
       for (int cc = 0; cc < P; ++cc) {
         if (cc < pw) {
@@ -268,17 +290,66 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
           }
         }
       }
-    } else if (tid >= 64 && p0 > 0) {
-      // deferred trailing update of panel p-1: the columns after panel p
-      for (int j = p0 + P + (tid - 64); j < a.bw; j += blockDim.x - 64)
-        apply_col(elp, p0 - P, j, 0, 1);
+      if (more) sz_fetch(p0 + P, sv, zv);  // the next panel's, in flight through the barrier
+    } else if (tid >= 64) {
+      const int t0 = tid - 64;
+      float vq[NS];
+      if (more) {
+        corr_fetch(p0, p0 + P, t0, 192, vq);      // off-diagonal block (p, p+1)
+        corr_fetch(p0 + P, p0 + P, t0, 192, vp);  // diagonal block of panel p+1
+      }
+      if (p0 > 0) {
+        // deferred trailing update of panel p-1: the columns after panel p
+        const int q0 = p0 - P;
+        int j = p0 + P + t0;
+        float cv[P];
+        if (j < a.bw) {
+#pragma unroll
+          for (int cc = 0; cc < P; ++cc) cv[cc] = a.corr[size_t(q0 + cc) * a.ldcorr + j];
+        }
+        for (; j < a.bw; j += 192) {
+          float cn[P];
+          const int jn = min(j + 192, a.bw - 1);  // clamped: the last prefetch is unused
+#pragma unroll
+          for (int cc = 0; cc < P; ++cc) cn[cc] = a.corr[size_t(q0 + cc) * a.ldcorr + jn];
+#pragma unroll 2
+          for (int rr = 0; rr < RW; ++rr) {
+            float w = Wb[rr * bwp + j];
+#pragma unroll
+            for (int cc = 0; cc < P; ++cc) {
+              const float d = elp[rr * (P + 1) + cc] * cv[cc];
+              w = w - d;
+            }
+            Wb[rr * bwp + j] = w;
+          }
+#pragma unroll
+          for (int cc = 0; cc < P; ++cc) cv[cc] = cn[cc];
+        }
+      }
+      if (more) {
+        corr_store(cq, t0, 192, vq);
+        if (a.dbl) corr_store(cpn, t0, 192, vp);
+      }
     }
     __syncthreads();
-    if (p0 + pw < a.bw) {  // panel p+1's columns get panel p's errors, then its corr block
+    if (more) {  // panel p+1's columns get panel p's errors (corr from LDS)
+      if (tid >= 64 && !a.dbl) corr_store(cpn, tid - 64, 192, vp);  // the chain is done with cp
       const int q0 = p0 + P, qw = min(P, a.bw - q0);
       const int jj = tid & 31;
-      if (jj < qw) apply_col(elc, p0, q0 + jj, tid >> 5, blockDim.x / 32);
-      load_cp(q0);
+      if (jj < qw) {
+        float cv[P];
+#pragma unroll
+        for (int cc = 0; cc < P; ++cc) cv[cc] = cq[cc * P + jj];
+        for (int rr = tid >> 5; rr < RW; rr += 256 / 32) {
+          float w = Wb[rr * bwp + q0 + jj];
+#pragma unroll
+          for (int cc = 0; cc < P; ++cc) {
+            const float d = elc[rr * (P + 1) + cc] * cv[cc];
+            w = w - d;
+          }
+          Wb[rr * bwp + q0 + jj] = w;
+        }
+      }
       __syncthreads();
     }
   }
@@ -543,7 +614,11 @@ __global__ void pack_zeros_kernel(const float *__restrict__ zero, int m, int G, 
   qz[size_t(gi) * nw + wi] = int32_t(uint32_t(acc & 0xffffffffu));
 }
 
-size_t block_smem(int bw) { return sizeof(float) * (size_t(RW) * (bw + 1) + 2 * RW * (P + 1) + P * P); }
+size_t block_smem(int bw, bool dbl = true) {
+  return sizeof(float) * (size_t(RW) * (bw + 1) + 2 * RW * (P + 1) + (dbl ? 3 : 2) * P * P);
+}
+// two diagonal corr buffers when the grid puts at most one workgroup on a CU
+bool block_dbl(int m) { return tg::cdiv(m, RW) <= tg::xcd_info().xcds * tg::xcd_info().cus_per_xcd; }
 
 constexpr int MAX_BLOCK = 2048;
 
@@ -605,7 +680,8 @@ extern "C" int tg_process_block(void *stream, const float *w, int ldw, const flo
   a.W = w; a.ldw = ldw; a.Q = q; a.ldq = ldq; a.codes = nullptr; a.ldc = 0; a.E = e; a.lde = lde;
   a.corr = corr; a.ldcorr = B; a.s = s; a.lds = lds; a.z = z; a.ldz = ldz;
   a.m = m; a.bw = B; a.minq = float(minq); a.maxq = float(maxq); a.code_off = 0;
-  hipLaunchKernelGGL((block_kernel<false, false>), dim3(tg::cdiv(m, RW)), dim3(256), block_smem(B),
+  a.dbl = block_dbl(m);
+  hipLaunchKernelGGL((block_kernel<false, false>), dim3(tg::cdiv(m, RW)), dim3(256), block_smem(B, a.dbl),
                      st, a);
   TG_LAUNCHED();
   return 0;
@@ -696,14 +772,15 @@ static int gptq_quantize_impl(bool loop, void *stream, const float *W, int m, in
     a.E = q.E; a.lde = bp; a.corr = q.corr; a.ldcorr = bp; a.dg = q.dg;
     a.scale = scale; a.zero = zero; a.perm = q.perm32; a.G = G; a.g = g; a.col0 = i1;
     a.m = m; a.bw = bw; a.minq = minq; a.maxq = maxq; a.code_off = code_off;
+    a.dbl = block_dbl(m);
     auto qtok = tg::prof_begin(st, tg::PROF_QBLOCK, 4.0 * 4.0 * double(m) * bw,
                                double(m) * bw * (bw - 1));
     if (loop)
       hipLaunchKernelGGL((block_kernel<true, true>), dim3(tg::cdiv(m, RW)), dim3(256),
-                         block_smem(bw), st, a);
+                         block_smem(bw, a.dbl), st, a);
     else
       hipLaunchKernelGGL((block_kernel<true, false>), dim3(tg::cdiv(m, RW)), dim3(256),
-                         block_smem(bw), st, a);
+                         block_smem(bw, a.dbl), st, a);
     tg::prof_end(st, qtok);
     TG_LAUNCHED();
     if (nc > 0) {
