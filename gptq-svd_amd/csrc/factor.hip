@@ -1582,6 +1582,52 @@ __global__ __launch_bounds__(64 * NWV) void potrf_inv_4w_kernel(double *__restri
   }
 }
 
+// X = U11^-1 (64 x 64 upper) from potrf_inv_block<.., false>'s factor (U's
+// strict upper part in sm.ut[l][i] = U[i][l], 1 / U_ll in sm.rinv) by
+// blocks instead of 64 dependent row steps: the eight 8 x 8 diagonal blocks
+// by back substitution (one thread per column, all at once), then three
+// levels of X12 = -X11 (U12 X22) over blocks of 16, 32, 64 -- 7 barriers.
+// xs: X (lower part zero); tmp: U12 X22 of the level.
+__device__ __forceinline__ void trinv64_blocked(PotrfSm &sm, double (*xs)[NU + 1],
+                                                double (*tmp)[NU + 1]) {
+  const int tid = threadIdx.x;
+  auto U = [&](int r, int c) { return r < c ? sm.ut[c][r] : 0.0; };  // strict upper
+  for (int e = tid; e < NU * NU; e += 256) xs[e >> 6][e & 63] = 0.0;
+  __syncthreads();
+  if (tid < NU) {
+    const int bb = 8 * (tid >> 3), c = tid & 7;
+    double x[8];
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      double acc = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int kk = i + 1; kk < 8; ++kk) acc = fma(-U(bb + i, bb + kk), x[kk], acc);
+      x[i] = (i <= c) ? acc * sm.rinv[bb + i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xs[bb + i][bb + c] = x[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 8; h < NU; h *= 2) {
+    const int nb = NU / (2 * h), cnt = nb * h * h;
+    for (int t = tid; t < cnt; t += 256) {  // T = U12 X22 (X22 upper: k <= c)
+      const int blk = t / (h * h), r = (t / h) % h, c = t % h, o = blk * 2 * h;
+      double acc = 0.0;
+      for (int kk = 0; kk <= c; ++kk) acc = fma(U(o + r, o + h + kk), xs[o + h + kk][o + h + c], acc);
+      tmp[o + r][o + h + c] = acc;
+    }
+    __syncthreads();
+    for (int t = tid; t < cnt; t += 256) {  // X12 = -X11 T (X11 upper: kk >= r)
+      const int blk = t / (h * h), r = (t / h) % h, c = t % h, o = blk * 2 * h;
+      double acc = 0.0;
+      for (int kk = r; kk < h; ++kk) acc = fma(xs[o + r][o + kk], tmp[o + kk][o + h + c], acc);
+      xs[o + r][o + h + c] = -acc;
+    }
+    __syncthreads();
+  }
+}
+
 // Fused panel step of chol_upper_rows (TG_CHOL_FUSED, the default): workgroup
 // t factors the panel's diagonal block itself (every workgroup the same
 // operations on the same block, so the same U11 and W in each) and forms its
@@ -1596,6 +1642,8 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double *__restrict__ U,
   constexpr int RW = NU / 4;
   __shared__ PotrfSm sm;
   __shared__ double gs[NU][NU + 1];  // the tile of G12 (row l, column j)
+  __shared__ double xs[NU][NU + 1];  // X = U11^-1
+  __shared__ double xt[NU][NU + 1];  // the inverse's level products
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6, lr = lane >> 4, lc = lane & 15;
   const int col0 = c0 + NU * int(blockIdx.x);
   // the tile first (its loads in flight through the factorisation)
@@ -1606,20 +1654,24 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double *__restrict__ U,
     tv[u] = U[size_t(p + min(r, pb - 1)) * ldu + min(col0 + cc, n - 1)];
   }
   double a[RW];
-  (void)potrf_inv_block<4, true>(U + size_t(p) * ldu + p, ldu, pb, sm, a);
+  (void)potrf_inv_block<4, false>(U + size_t(p) * ldu + p, ldu, pb, sm, a);
+  __syncthreads();  // sm.ut / sm.rinv complete
+  trinv64_blocked(sm, xs, xt);
 #pragma unroll
   for (int u = 0; u < NU * NU / 256; ++u) {
     const int e = tid + 256 * u, r = e >> 6, cc = e & 63;
     gs[r][cc] = (r < pb) ? tv[u] : 0.0;
   }
   __syncthreads();
-  // wave g: rows 16 g .. 16 g + 15 of P, four 16-column blocks, K = 64
+  // wave g: rows 16 g .. 16 g + 15 of P, four 16-column blocks, K = 64;
+  // W = X^T restricted to the block's pb rows and columns
   doublex4 acc[4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) acc[cb] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int k0 = 0; k0 < NU; k0 += 4) {
-    const double av = sm.ut[16 * g + lc][k0 + lr];  // W[row][k]
+    const int wi = 16 * g + lc, wk = k0 + lr;
+    const double av = (wi < pb && wk < pb) ? xs[wk][wi] : 0.0;  // W[row][k] = X[k][row]
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, gs[k0 + lr][16 * cb + lc], acc[cb], 0, 0, 0);
